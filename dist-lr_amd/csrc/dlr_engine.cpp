@@ -1,0 +1,561 @@
+// dlr_engine.cpp -- device engine of libdistlr_amd: one context per GPU/rank.
+//
+// Replaces, for the LR hot path:
+//   LR::Train / PullWeight_ / PushGradient_   src/lr.cc:28-45, 116-132
+//   KVStoreDistServer::DataHandle             src/main.cc:41-96
+//   DataIter per-epoch re-parse + copies      include/data_iter.h:16-55, main.cc:158-159
+// Weights stay resident and replicated; with world > 1 each rank serves one
+// key range: all-to-all of the pushed gradients (rank r receives every
+// rank's slice of its range), rank-ordered merge + SGD on the range, then
+// an in-place all-gather of the updated weights (the "pull").
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "dlr_internal.h"
+#include "dlr_kernels.h"
+
+namespace {
+
+constexpr int kTimers = 5;  // 0 margin, 1 gradient, 2 update, 3 exchange, 4 step
+constexpr int64_t kPad = 64;  // padding entries after col/val (16-B tail loads)
+
+struct DeviceBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+struct TrainShard {
+    bool loaded = false;
+    int64_t n_rows = 0, nnz = 0, B = 0;
+    std::vector<dlr::BatchSpan> plan;
+    // shard CSR
+    int64_t *row_ptr = nullptr;
+    int32_t *col = nullptr;
+    float *val = nullptr;
+    float *label = nullptr;
+    // materialised wrap batch (rows (start+i) mod N)
+    int64_t wrap_batch = -1;
+    int64_t *w_row_ptr = nullptr;
+    int32_t *w_col = nullptr;
+    float *w_val = nullptr;
+    float *w_label = nullptr;
+    // per-batch column-major copy
+    bool row16 = false;
+    uint32_t *cptr = nullptr;   // n_batches x (D+1)
+    void *crow = nullptr;
+    float *cval = nullptr;
+    std::vector<int64_t> coff;  // entry offset of each batch
+    int64_t bytes = 0;
+};
+
+struct TestShard {
+    bool loaded = false;
+    int64_t n_rows = 0, nnz = 0;
+    int64_t *row_ptr = nullptr;
+    int32_t *col = nullptr;
+    float *val = nullptr;
+    float *label = nullptr;
+    int grid = 0;
+    int64_t bytes = 0;
+};
+
+}  // namespace
+
+struct dlr_ctx {
+    int device = 0, rank = 0, world = 1;
+    int64_t D = 0, chunk = 0, Dpad = 0;
+    hipStream_t stream = nullptr;
+    ncclComm_t comm = nullptr;
+    float *w = nullptr;      // Dpad (replicated weights)
+    float *g = nullptr;      // Dpad (this rank's pushed gradient), world > 1
+    float *recv = nullptr;   // world x chunk, world > 1
+    float *resid = nullptr;  // max batch rows
+    int64_t resid_cap = 0;
+    unsigned long long *correct = nullptr;
+    double *ll = nullptr;       // [0] total, [1..] partials
+    int64_t ll_cap = 0;
+    unsigned long long *h_correct = nullptr;  // pinned
+    double *h_ll = nullptr;                   // pinned
+    TrainShard train;
+    TestShard test;
+    std::vector<void *> allocs;
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_pending;
+    size_t ev_next = 0;
+    double t_ms[kTimers] = {0};
+    int64_t t_n[kTimers] = {0};
+    std::string err;
+};
+
+namespace {
+
+int fail(dlr_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    dlr::set_error(msg);
+    return code;
+}
+
+#define HIPC(c, expr)                                                                                   \
+    do {                                                                                                \
+        hipError_t e_ = (expr);                                                                         \
+        if (e_ != hipSuccess)                                                                           \
+            return fail((c), DLR_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));             \
+    } while (0)
+
+#define NCCLC(c, expr)                                                                                  \
+    do {                                                                                                \
+        ncclResult_t r_ = (expr);                                                                       \
+        if (r_ != ncclSuccess) return fail((c), DLR_E_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+int dev_alloc(dlr_ctx *c, void **p, size_t bytes) {
+    *p = nullptr;
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(c, DLR_E_NOMEM, "hipMalloc(" + std::to_string(bytes) + " B): " + hipGetErrorString(e));
+    }
+    c->allocs.push_back(*p);
+    return DLR_OK;
+}
+
+void dev_free(dlr_ctx *c, void *p) {
+    if (!p) return;
+    auto it = std::find(c->allocs.begin(), c->allocs.end(), p);
+    if (it != c->allocs.end()) c->allocs.erase(it);
+    (void)hipFree(p);
+}
+
+template <typename T>
+int upload(dlr_ctx *c, T **dst, const T *src, size_t n, size_t pad = 0) {
+    int rc = dev_alloc(c, (void **)dst, (n + pad) * sizeof(T));
+    if (rc) return rc;
+    if (n) HIPC(c, hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+    if (pad) HIPC(c, hipMemset(*dst + n, 0, pad * sizeof(T)));
+    return DLR_OK;
+}
+
+void free_train(dlr_ctx *c) {
+    TrainShard &t = c->train;
+    for (void *p : {(void *)t.row_ptr, (void *)t.col, (void *)t.val, (void *)t.label, (void *)t.w_row_ptr,
+                    (void *)t.w_col, (void *)t.w_val, (void *)t.w_label, (void *)t.cptr, t.crow, (void *)t.cval})
+        dev_free(c, p);
+    t = TrainShard();
+}
+
+void free_test(dlr_ctx *c) {
+    TestShard &t = c->test;
+    for (void *p : {(void *)t.row_ptr, (void *)t.col, (void *)t.val, (void *)t.label}) dev_free(c, p);
+    t = TestShard();
+}
+
+// ---- timing: pairs of events around each launch, harvested on demand
+void time_begin(dlr_ctx *c, hipEvent_t *a) {
+    *a = nullptr;
+    if (!c->timing) return;
+    if (c->ev_next + 2 > c->ev_pool.size()) {
+        for (int i = 0; i < 256; ++i) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return;
+            c->ev_pool.push_back(e);
+        }
+    }
+    *a = c->ev_pool[c->ev_next++];
+    (void)hipEventRecord(*a, c->stream);
+}
+
+void time_end(dlr_ctx *c, int which, hipEvent_t a) {
+    if (!c->timing || !a) return;
+    hipEvent_t b = c->ev_pool[c->ev_next++];
+    (void)hipEventRecord(b, c->stream);
+    c->ev_pending.push_back({which, {a, b}});
+}
+
+void harvest(dlr_ctx *c) {
+    if (c->ev_pending.empty()) return;
+    (void)hipStreamSynchronize(c->stream);
+    for (auto &p : c->ev_pending) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, p.second.first, p.second.second) == hipSuccess) {
+            c->t_ms[p.first] += ms;
+            c->t_n[p.first] += 1;
+        }
+    }
+    c->ev_pending.clear();
+    c->ev_next = 0;
+}
+
+// Builds the column-major copy of every batch: a stable counting sort by
+// column of the batch's entries taken in batch-row order, so each column's
+// segment lists its rows in the order lr.cc:37 visits them.
+template <typename RowT>
+void build_csc(const dlr_dataset &ds, const std::vector<dlr::BatchSpan> &plan, int64_t D,
+               const std::vector<int64_t> &coff, std::vector<uint32_t> &cptr, std::vector<RowT> &crow,
+               std::vector<float> &cval, int nthreads) {
+    const int64_t nb = (int64_t)plan.size();
+    const int64_t N = ds.n_rows;
+    std::vector<std::thread> th;
+    nthreads = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, nb));
+    for (int t = 0; t < nthreads; ++t) {
+        th.emplace_back([&, t] {
+            std::vector<uint32_t> cnt((size_t)D + 1);
+            for (int64_t b = t; b < nb; b += nthreads) {
+                const dlr::BatchSpan &sp = plan[(size_t)b];
+                std::fill(cnt.begin(), cnt.end(), 0u);
+                for (int64_t i = 0; i < sp.rows; ++i) {
+                    const int64_t r = (sp.first_row + i) % N;
+                    for (int64_t k = ds.row_ptr[(size_t)r]; k < ds.row_ptr[(size_t)r + 1]; ++k)
+                        ++cnt[(size_t)ds.col[(size_t)k] + 1];
+                }
+                uint32_t *ptr = cptr.data() + (size_t)b * (size_t)(D + 1);
+                ptr[0] = 0;
+                for (int64_t j = 0; j < D; ++j) ptr[j + 1] = ptr[j] + cnt[(size_t)j + 1];
+                std::copy(ptr, ptr + D, cnt.begin());  // cursors
+                RowT *rr = crow.data() + coff[(size_t)b];
+                float *vv = cval.data() + coff[(size_t)b];
+                for (int64_t i = 0; i < sp.rows; ++i) {
+                    const int64_t r = (sp.first_row + i) % N;
+                    for (int64_t k = ds.row_ptr[(size_t)r]; k < ds.row_ptr[(size_t)r + 1]; ++k) {
+                        const uint32_t pos = cnt[(size_t)ds.col[(size_t)k]]++;
+                        rr[pos] = (RowT)i;
+                        vv[pos] = ds.val[(size_t)k];
+                    }
+                }
+            }
+        });
+    }
+    for (auto &x : th) x.join();
+}
+
+dlr::DevBatch batch_view(const dlr_ctx *c, int64_t b) {
+    const TrainShard &t = c->train;
+    const dlr::BatchSpan &sp = t.plan[(size_t)b];
+    if (b == t.wrap_batch) return {t.w_row_ptr, t.w_col, t.w_val, t.w_label, sp.rows};
+    return {t.row_ptr + sp.first_row, t.col, t.val, t.label + sp.first_row, sp.rows};
+}
+
+dlr::DevCsc csc_view(const dlr_ctx *c, int64_t b) {
+    const TrainShard &t = c->train;
+    const size_t esz = t.row16 ? 2 : 4;
+    return {t.cptr + (size_t)b * (size_t)(c->D + 1), (const char *)t.crow + esz * (size_t)t.coff[(size_t)b],
+            t.cval + t.coff[(size_t)b], t.row16};
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *dlr_last_error(const dlr_ctx *ctx) { return ctx ? ctx->err.c_str() : dlr::thread_error(); }
+
+int dlr_get_unique_id(void *id_out) {
+    if (!id_out) return DLR_E_ARG;
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(nullptr, DLR_E_RCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    memcpy(id_out, &id, sizeof(id));
+    return DLR_OK;
+}
+
+int dlr_create(int device, int rank, int world, const void *unique_id, int64_t D, dlr_ctx **out) {
+    if (!out || D <= 0 || world <= 0 || rank < 0 || rank >= world || (world > 1 && !unique_id))
+        return fail(nullptr, DLR_E_ARG, "dlr_create: bad argument");
+    *out = nullptr;
+    auto c = std::make_unique<dlr_ctx>();
+    c->device = device;
+    c->rank = rank;
+    c->world = world;
+    c->D = D;
+    c->chunk = (D + world - 1) / world;
+    c->Dpad = c->chunk * world;
+    HIPC(c.get(), hipSetDevice(device));
+    HIPC(c.get(), hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    int rc;
+    if ((rc = dev_alloc(c.get(), (void **)&c->w, (size_t)c->Dpad * 4))) return rc;
+    HIPC(c.get(), hipMemset(c->w, 0, (size_t)c->Dpad * 4));
+    if ((rc = dev_alloc(c.get(), (void **)&c->correct, 64))) return rc;
+    HIPC(c.get(), hipHostMalloc((void **)&c->h_correct, 64, hipHostMallocDefault));
+    HIPC(c.get(), hipHostMalloc((void **)&c->h_ll, 64, hipHostMallocDefault));
+    if (world > 1) {
+        if ((rc = dev_alloc(c.get(), (void **)&c->g, (size_t)c->Dpad * 4))) return rc;
+        if ((rc = dev_alloc(c.get(), (void **)&c->recv, (size_t)c->Dpad * 4))) return rc;
+        HIPC(c.get(), hipMemset(c->g, 0, (size_t)c->Dpad * 4));
+        ncclUniqueId id;
+        memcpy(&id, unique_id, sizeof(id));
+        NCCLC(c.get(), ncclCommInitRank(&c->comm, world, id, rank));
+    }
+    *out = c.release();
+    return DLR_OK;
+}
+
+void dlr_destroy(dlr_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->comm) ncclCommDestroy(ctx->comm);
+    for (void *p : ctx->allocs) (void)hipFree(p);
+    for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
+    if (ctx->h_correct) (void)hipHostFree(ctx->h_correct);
+    if (ctx->h_ll) (void)hipHostFree(ctx->h_ll);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int dlr_set_weights(dlr_ctx *c, const float *w, int64_t D) {
+    if (!c || !w || D != c->D) return fail(c, DLR_E_ARG, "dlr_set_weights: D mismatch");
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipMemcpyAsync(c->w, w, (size_t)D * 4, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return DLR_OK;
+}
+
+int dlr_get_weights(dlr_ctx *c, float *w, int64_t D) {
+    if (!c || !w || D != c->D) return fail(c, DLR_E_ARG, "dlr_get_weights: D mismatch");
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipMemcpyAsync(w, c->w, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return DLR_OK;
+}
+
+int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_t *n_batches) {
+    if (!c || !ds) return fail(c, DLR_E_ARG, "dlr_load_train: bad argument");
+    if (ds->D != c->D) return fail(c, DLR_E_ARG, "dlr_load_train: dataset D != context D");
+    if (batch_size == 0) return fail(c, DLR_E_ARG, "dlr_load_train: batch_size 0 (reference never terminates)");
+    if (ds->n_rows <= 0) return fail(c, DLR_E_ARG, "dlr_load_train: empty shard (reference never terminates)");
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    free_train(c);
+    TrainShard &t = c->train;
+    t.n_rows = ds->n_rows;
+    t.nnz = (int64_t)ds->col.size();
+    t.B = batch_size < 0 ? ds->n_rows : batch_size;
+    if (t.B > INT32_MAX) return fail(c, DLR_E_ARG, "dlr_load_train: batch too large");
+    t.plan = dlr::plan_batches(ds->n_rows, batch_size);
+    const int64_t nb = (int64_t)t.plan.size();
+    const int64_t D = c->D;
+    // Per-batch entry counts (every batch has exactly B rows).
+    t.coff.assign((size_t)nb + 1, 0);
+    for (int64_t b = 0; b < nb; ++b) {
+        const dlr::BatchSpan &sp = t.plan[(size_t)b];
+        int64_t e;
+        if (sp.contiguous) {
+            e = ds->row_ptr[(size_t)(sp.first_row + sp.rows)] - ds->row_ptr[(size_t)sp.first_row];
+        } else {
+            e = 0;
+            for (int64_t i = 0; i < sp.rows; ++i) {
+                const int64_t r = (sp.first_row + i) % ds->n_rows;
+                e += ds->row_ptr[(size_t)r + 1] - ds->row_ptr[(size_t)r];
+            }
+        }
+        if (e > (int64_t)UINT32_MAX) return fail(c, DLR_E_ARG, "dlr_load_train: batch has > 2^32 entries");
+        t.coff[(size_t)b + 1] = t.coff[(size_t)b] + e;
+    }
+    const double cptr_bytes = (double)nb * (double)(D + 1) * 4.0;
+    if (cptr_bytes > 64.0 * (1ull << 30))
+        return fail(c, DLR_E_NOMEM, "dlr_load_train: per-batch column pointers would need " +
+                                        std::to_string((long long)(cptr_bytes / (1 << 20))) +
+                                        " MiB (compacted column segments not implemented yet)");
+    int rc;
+    // Shard CSR.
+    if ((rc = upload(c, &t.row_ptr, ds->row_ptr.data(), (size_t)t.n_rows + 1))) return rc;
+    if ((rc = upload(c, &t.col, ds->col.data(), (size_t)t.nnz, kPad))) return rc;
+    if ((rc = upload(c, &t.val, ds->val.data(), (size_t)t.nnz, kPad))) return rc;
+    {
+        std::vector<float> lab(ds->label.begin(), ds->label.end());
+        if ((rc = upload(c, &t.label, lab.data(), lab.size()))) return rc;
+    }
+    // Materialise the (at most one) wrapping batch.
+    for (int64_t b = 0; b < nb; ++b) {
+        const dlr::BatchSpan &sp = t.plan[(size_t)b];
+        if (sp.contiguous) continue;
+        t.wrap_batch = b;
+        std::vector<int64_t> rp((size_t)sp.rows + 1);
+        std::vector<int32_t> cc;
+        std::vector<float> vv, ll((size_t)sp.rows);
+        cc.reserve((size_t)(t.coff[(size_t)b + 1] - t.coff[(size_t)b]));
+        vv.reserve(cc.capacity());
+        rp[0] = 0;
+        for (int64_t i = 0; i < sp.rows; ++i) {
+            const int64_t r = (sp.first_row + i) % ds->n_rows;
+            for (int64_t k = ds->row_ptr[(size_t)r]; k < ds->row_ptr[(size_t)r + 1]; ++k) {
+                cc.push_back(ds->col[(size_t)k]);
+                vv.push_back(ds->val[(size_t)k]);
+            }
+            rp[(size_t)i + 1] = (int64_t)cc.size();
+            ll[(size_t)i] = (float)ds->label[(size_t)r];
+        }
+        if ((rc = upload(c, &t.w_row_ptr, rp.data(), rp.size()))) return rc;
+        if ((rc = upload(c, &t.w_col, cc.data(), cc.size(), kPad))) return rc;
+        if ((rc = upload(c, &t.w_val, vv.data(), vv.size(), kPad))) return rc;
+        if ((rc = upload(c, &t.w_label, ll.data(), ll.size()))) return rc;
+        break;  // NextBatch wraps at most once per epoch
+    }
+    // Column-major copy of every batch.
+    t.row16 = t.B <= 65536;
+    const int64_t total = t.coff[(size_t)nb];
+    std::vector<uint32_t> cptr((size_t)nb * (size_t)(D + 1));
+    std::vector<float> cval((size_t)total);
+    const int nthreads = dlr::default_threads();
+    if (t.row16) {
+        std::vector<uint16_t> crow((size_t)total);
+        build_csc(*ds, t.plan, D, t.coff, cptr, crow, cval, nthreads);
+        if ((rc = upload(c, (uint16_t **)&t.crow, crow.data(), crow.size(), kPad))) return rc;
+    } else {
+        std::vector<uint32_t> crow((size_t)total);
+        build_csc(*ds, t.plan, D, t.coff, cptr, crow, cval, nthreads);
+        if ((rc = upload(c, (uint32_t **)&t.crow, crow.data(), crow.size(), kPad))) return rc;
+    }
+    if ((rc = upload(c, &t.cptr, cptr.data(), cptr.size()))) return rc;
+    if ((rc = upload(c, &t.cval, cval.data(), cval.size(), kPad))) return rc;
+    // Residual buffer.
+    if (c->resid_cap < t.B) {
+        dev_free(c, c->resid);
+        c->resid = nullptr;
+        if ((rc = dev_alloc(c, (void **)&c->resid, (size_t)t.B * 4))) return rc;
+        c->resid_cap = t.B;
+    }
+    t.bytes = (int64_t)((t.n_rows + 1) * 8 + (t.nnz + kPad) * 8 + t.n_rows * 4 + cptr.size() * 4 +
+                        (total + kPad) * ((t.row16 ? 2 : 4) + 4));
+    t.loaded = true;
+    if (n_batches) *n_batches = nb;
+    return DLR_OK;
+}
+
+int dlr_load_test(dlr_ctx *c, const dlr_dataset *ds) {
+    if (!c || !ds) return fail(c, DLR_E_ARG, "dlr_load_test: bad argument");
+    if (ds->D != c->D) return fail(c, DLR_E_ARG, "dlr_load_test: dataset D != context D");
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    free_test(c);
+    TestShard &t = c->test;
+    t.n_rows = ds->n_rows;
+    t.nnz = (int64_t)ds->col.size();
+    int rc;
+    if ((rc = upload(c, &t.row_ptr, ds->row_ptr.data(), (size_t)t.n_rows + 1))) return rc;
+    if ((rc = upload(c, &t.col, ds->col.data(), (size_t)t.nnz, kPad))) return rc;
+    if ((rc = upload(c, &t.val, ds->val.data(), (size_t)t.nnz, kPad))) return rc;
+    std::vector<float> lab(ds->label.begin(), ds->label.end());
+    if ((rc = upload(c, &t.label, lab.data(), lab.size()))) return rc;
+    t.grid = dlr::predict_grid(t.n_rows);
+    if (c->ll_cap < t.grid + 1) {
+        dev_free(c, c->ll);
+        c->ll = nullptr;
+        if ((rc = dev_alloc(c, (void **)&c->ll, (size_t)(t.grid + 1) * 8))) return rc;
+        c->ll_cap = t.grid + 1;
+    }
+    t.bytes = (int64_t)((t.n_rows + 1) * 8 + (t.nnz + kPad) * 8 + t.n_rows * 4);
+    t.loaded = true;
+    return DLR_OK;
+}
+
+int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
+    if (!c) return fail(c, DLR_E_ARG, "dlr_train_step: null context");
+    if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_step: no training shard loaded");
+    if (b < 0 || b >= (int64_t)c->train.plan.size()) return fail(c, DLR_E_ARG, "dlr_train_step: batch out of range");
+    if (mode < 0 || mode > 2) return fail(c, DLR_E_ARG, "dlr_train_step: bad mode");
+    HIPC(c, hipSetDevice(c->device));
+    const dlr::DevBatch bt = batch_view(c, b);
+    if (bt.rows > c->resid_cap) return fail(c, DLR_E_STATE, "dlr_train_step: residual buffer too small");
+    const dlr::DevCsc cs = csc_view(c, b);
+    hipEvent_t t_step, t0;
+    time_begin(c, &t_step);
+    time_begin(c, &t0);
+    HIPC(c, dlr::launch_margin_residual(bt, c->w, c->resid, c->stream));
+    time_end(c, 0, t0);
+    if (c->world == 1) {
+        time_begin(c, &t0);
+        HIPC(c, dlr::launch_grad(cs, c->D, c->resid, c->w, nullptr, bt.rows, lr, C, true, c->stream));
+        time_end(c, 1, t0);
+    } else {
+        time_begin(c, &t0);
+        HIPC(c, dlr::launch_grad(cs, c->D, c->resid, c->w, c->g, bt.rows, lr, C, false, c->stream));
+        time_end(c, 1, t0);
+        time_begin(c, &t0);
+        NCCLC(c, ncclAllToAll(c->g, c->recv, (size_t)c->chunk, ncclFloat32, c->comm, c->stream));
+        time_end(c, 3, t0);
+        int64_t kb, ke;
+        dlr_key_range(c->D, c->world, c->rank, &kb, &ke);
+        time_begin(c, &t0);
+        HIPC(c, dlr::launch_merge_update(c->recv, c->world, c->chunk, ke - kb, c->w + kb, lr, mode, c->stream));
+        time_end(c, 2, t0);
+        time_begin(c, &t0);
+        NCCLC(c, ncclAllGather(c->w + (int64_t)c->rank * c->chunk, c->w, (size_t)c->chunk, ncclFloat32, c->comm,
+                               c->stream));
+        time_end(c, 3, t0);
+    }
+    time_end(c, 4, t_step);
+    return DLR_OK;
+}
+
+int dlr_train_epoch(dlr_ctx *c, float lr, float C, int mode) {
+    if (!c) return DLR_E_ARG;
+    if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_epoch: no training shard loaded");
+    for (int64_t b = 0; b < (int64_t)c->train.plan.size(); ++b) {
+        int rc = dlr_train_step(c, b, lr, C, mode);
+        if (rc) return rc;
+    }
+    return DLR_OK;
+}
+
+int dlr_predict(dlr_ctx *c, int64_t *correct, int64_t *n_rows, double *logloss) {
+    if (!c) return DLR_E_ARG;
+    if (!c->test.loaded) return fail(c, DLR_E_STATE, "dlr_predict: no test shard loaded");
+    HIPC(c, hipSetDevice(c->device));
+    const TestShard &t = c->test;
+    HIPC(c, hipMemsetAsync(c->correct, 0, 8, c->stream));
+    const dlr::DevBatch bt{t.row_ptr, t.col, t.val, t.label, t.n_rows};
+    HIPC(c, dlr::launch_predict(bt, c->w, c->correct, c->ll + 1, c->ll, c->stream));
+    HIPC(c, hipMemcpyAsync(c->h_correct, c->correct, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(c->h_ll, c->ll, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    if (correct) *correct = (int64_t)*c->h_correct;
+    if (n_rows) *n_rows = t.n_rows;
+    if (logloss) *logloss = *c->h_ll;
+    return DLR_OK;
+}
+
+int dlr_sync(dlr_ctx *c) {
+    if (!c) return DLR_E_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return DLR_OK;
+}
+
+int dlr_timing(dlr_ctx *c, int enable) {
+    if (!c) return DLR_E_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    harvest(c);
+    c->timing = enable != 0;
+    for (int i = 0; i < kTimers; ++i) {
+        c->t_ms[i] = 0;
+        c->t_n[i] = 0;
+    }
+    return DLR_OK;
+}
+
+int dlr_kernel_time(dlr_ctx *c, int which, double *total_ms, int64_t *launches) {
+    if (!c || which < 0 || which >= kTimers) return DLR_E_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    harvest(c);
+    if (total_ms) *total_ms = c->t_ms[which];
+    if (launches) *launches = c->t_n[which];
+    return DLR_OK;
+}
+
+int dlr_memory_info(dlr_ctx *c, int64_t *train_bytes, int64_t *test_bytes) {
+    if (!c) return DLR_E_ARG;
+    if (train_bytes) *train_bytes = c->train.loaded ? c->train.bytes : 0;
+    if (test_bytes) *test_bytes = c->test.loaded ? c->test.bytes : 0;
+    return DLR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,340 @@
+"""ctypes binding of libdistlr_amd's C-ABI (include/distlr_amd.h).
+
+The library is built in-tree (``make -C dist-lr_amd``) and loaded from
+``dist-lr_amd/lib/libdistlr_amd.so``.  There is no fallback: if the library
+is missing, importing this module raises.  Import ``torch`` (if at all)
+BEFORE this module, so that the process has a single HIP runtime: the
+library binds to whichever ``libamdhip64.so.7`` is already loaded.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+LIB_PATH = os.path.join(PKG, "lib", "libdistlr_amd.so")
+
+MODE_SYNC_MEAN = 0
+MODE_SYNC_LAST = 1
+MODE_ASYNC = 2
+UNIQUE_ID_BYTES = 128
+
+# Exported symbols, in include/distlr_amd.h order (tests check the .so
+# exports every one of them).
+SYMBOLS = [
+    "dlr_to_int", "dlr_to_float", "dlr_split",
+    "dlr_dataset_load_libsvm", "dlr_dataset_from_csr", "dlr_dataset_generate",
+    "dlr_dataset_write_libsvm", "dlr_dataset_info", "dlr_dataset_view", "dlr_dataset_free",
+    "dlr_num_batches", "dlr_batch_rows",
+    "dlr_init_weight", "dlr_format_model", "dlr_key_range",
+    "dlr_get_unique_id", "dlr_create", "dlr_destroy", "dlr_last_error",
+    "dlr_set_weights", "dlr_get_weights", "dlr_load_train", "dlr_load_test",
+    "dlr_train_step", "dlr_train_epoch", "dlr_predict", "dlr_sync",
+    "dlr_timing", "dlr_kernel_time", "dlr_memory_info",
+]
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} not built: run `make -C dist-lr_amd` (or __graft_entry__.build())")
+
+lib = C.CDLL(LIB_PATH)
+
+i64 = C.c_int64
+P = C.c_void_p
+
+
+class GenSpec(C.Structure):
+    _fields_ = [
+        ("n_rows", C.c_int64),
+        ("num_feature_dim", C.c_int64),
+        ("nnz_per_row", C.c_int32),
+        ("value_mode", C.c_int32),
+        ("seed", C.c_uint64),
+        ("stream", C.c_uint64),
+        ("positive_frac", C.c_double),
+        ("label_noise", C.c_double),
+        ("nthreads", C.c_int32),
+    ]
+
+
+def _sig(name, res, *args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+_sig("dlr_to_int", C.c_int, C.c_char_p)
+_sig("dlr_to_float", C.c_float, C.c_char_p)
+_sig("dlr_split", C.c_int, C.c_char_p, C.c_char, C.c_char_p, C.c_int)
+_sig("dlr_dataset_load_libsvm", C.c_int, C.c_char_p, i64, C.c_int, C.POINTER(P))
+_sig("dlr_dataset_from_csr", C.c_int, i64, i64, P, P, P, P, C.POINTER(P))
+_sig("dlr_dataset_generate", C.c_int, C.POINTER(GenSpec), C.POINTER(P))
+_sig("dlr_dataset_write_libsvm", C.c_int, P, C.c_char_p, C.c_int)
+_sig("dlr_dataset_info", C.c_int, P, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64))
+_sig("dlr_dataset_view", C.c_int, P, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P))
+_sig("dlr_dataset_free", None, P)
+_sig("dlr_num_batches", i64, i64, i64)
+_sig("dlr_batch_rows", C.c_int, i64, i64, i64, P)
+_sig("dlr_init_weight", C.c_int, C.c_int, P, i64)
+_sig("dlr_format_model", C.c_int, P, i64, C.c_char_p, i64, C.POINTER(i64))
+_sig("dlr_key_range", C.c_int, i64, C.c_int, C.c_int, C.POINTER(i64), C.POINTER(i64))
+_sig("dlr_get_unique_id", C.c_int, P)
+_sig("dlr_create", C.c_int, C.c_int, C.c_int, C.c_int, P, i64, C.POINTER(P))
+_sig("dlr_destroy", None, P)
+_sig("dlr_last_error", C.c_char_p, P)
+_sig("dlr_set_weights", C.c_int, P, P, i64)
+_sig("dlr_get_weights", C.c_int, P, P, i64)
+_sig("dlr_load_train", C.c_int, P, P, i64, C.POINTER(i64))
+_sig("dlr_load_test", C.c_int, P, P)
+_sig("dlr_train_step", C.c_int, P, i64, C.c_float, C.c_float, C.c_int)
+_sig("dlr_train_epoch", C.c_int, P, C.c_float, C.c_float, C.c_int)
+_sig("dlr_predict", C.c_int, P, C.POINTER(i64), C.POINTER(i64), C.POINTER(C.c_double))
+_sig("dlr_sync", C.c_int, P)
+_sig("dlr_timing", C.c_int, P, C.c_int)
+_sig("dlr_kernel_time", C.c_int, P, C.c_int, C.POINTER(C.c_double), C.POINTER(i64))
+_sig("dlr_memory_info", C.c_int, P, C.POINTER(i64), C.POINTER(i64))
+
+
+class DLRError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+def _check(rc: int, ctx=None):
+    if rc < 0:
+        msg = lib.dlr_last_error(ctx)
+        raise DLRError(rc, msg.decode(errors="replace") if msg else "")
+    return rc
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(P)
+
+
+# ---------------------------------------------------------------- parsing
+
+def to_int(s: str | bytes) -> int:
+    return lib.dlr_to_int(s.encode() if isinstance(s, str) else s)
+
+
+def to_float(s: str | bytes) -> float:
+    return lib.dlr_to_float(s.encode() if isinstance(s, str) else s)
+
+
+def to_float_bits(s: str | bytes) -> int:
+    return int(np.float32(to_float(s)).view(np.uint32))
+
+
+def split(s: str | bytes, sep: str = ":") -> list[bytes]:
+    b = s.encode() if isinstance(s, str) else s
+    buf = C.create_string_buffer(2 * len(b) * (len(b) + 2) + 16)
+    n = _check(lib.dlr_split(b, sep.encode(), buf, len(buf)))
+    out, raw, pos = [], buf.raw, 0
+    for _ in range(n):
+        e = raw.index(b"\0", pos)
+        out.append(raw[pos:e])
+        pos = e + 1
+    return out
+
+
+# ---------------------------------------------------------------- datasets
+
+class Dataset:
+    """A host CSR shard owned by the library (DataIter's storage)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @property
+    def handle(self):
+        return self._h
+
+    @classmethod
+    def load_libsvm(cls, path: str, num_feature_dim: int, nthreads: int = 0) -> "Dataset":
+        h = P()
+        _check(lib.dlr_dataset_load_libsvm(path.encode(), num_feature_dim, nthreads, C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def from_csr(cls, row_ptr, col, val, label, num_feature_dim: int) -> "Dataset":
+        row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int64)
+        col = np.ascontiguousarray(col, dtype=np.int32)
+        val = np.ascontiguousarray(val, dtype=np.float32)
+        label = np.ascontiguousarray(label, dtype=np.int32)
+        h = P()
+        _check(lib.dlr_dataset_from_csr(len(row_ptr) - 1, num_feature_dim, _ptr(row_ptr), _ptr(col), _ptr(val),
+                                        _ptr(label), C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def generate(cls, n_rows: int, num_feature_dim: int, nnz_per_row: int, *, value_mode: int = 0,
+                 seed: int = 10, stream: int = 0, positive_frac: float = 0.24, label_noise: float = 0.05,
+                 nthreads: int = 0) -> "Dataset":
+        spec = GenSpec(n_rows, num_feature_dim, nnz_per_row, value_mode, seed, stream, positive_frac,
+                       label_noise, nthreads)
+        h = P()
+        _check(lib.dlr_dataset_generate(C.byref(spec), C.byref(h)))
+        return cls(h)
+
+    def write_libsvm(self, path: str, value_mode: int = 0) -> None:
+        _check(lib.dlr_dataset_write_libsvm(self._h, path.encode(), value_mode))
+
+    def info(self) -> Tuple[int, int, int]:
+        n, nnz, d = i64(), i64(), i64()
+        _check(lib.dlr_dataset_info(self._h, C.byref(n), C.byref(nnz), C.byref(d)))
+        return n.value, nnz.value, d.value
+
+    @property
+    def n_rows(self) -> int:
+        return self.info()[0]
+
+    def csr(self):
+        """Copies of (row_ptr int64, col int32, val float32, label int32)."""
+        n, nnz, _ = self.info()
+        rp, cc, vv, ll = P(), P(), P(), P()
+        _check(lib.dlr_dataset_view(self._h, C.byref(rp), C.byref(cc), C.byref(vv), C.byref(ll)))
+
+        def arr(p, count, ctype, dtype):
+            if count == 0:
+                return np.zeros(0, dtype=dtype)
+            return np.ctypeslib.as_array(C.cast(p, C.POINTER(ctype)), shape=(count,)).astype(dtype, copy=True)
+
+        return (arr(rp, n + 1, C.c_int64, np.int64), arr(cc, nnz, C.c_int32, np.int32),
+                arr(vv, nnz, C.c_float, np.float32), arr(ll, n, C.c_int32, np.int32))
+
+    def free(self):
+        if self._h:
+            lib.dlr_dataset_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def num_batches(n_rows: int, batch_size: int) -> int:
+    return lib.dlr_num_batches(n_rows, batch_size)
+
+
+def batch_rows(n_rows: int, batch_size: int, batch: int) -> np.ndarray:
+    B = n_rows if batch_size < 0 else batch_size
+    out = np.empty(B, dtype=np.int64)
+    _check(lib.dlr_batch_rows(n_rows, batch_size, batch, _ptr(out)))
+    return out
+
+
+def init_weight(num_feature_dim: int, random_state: int = 0) -> np.ndarray:
+    w = np.empty(num_feature_dim, dtype=np.float32)
+    _check(lib.dlr_init_weight(random_state, _ptr(w), num_feature_dim))
+    return w
+
+
+def format_model(w: np.ndarray) -> str:
+    w = np.ascontiguousarray(w, dtype=np.float32)
+    need = i64()
+    _check(lib.dlr_format_model(_ptr(w), len(w), None, 0, C.byref(need)))
+    buf = C.create_string_buffer(need.value + 1)
+    _check(lib.dlr_format_model(_ptr(w), len(w), buf, need.value + 1, C.byref(need)))
+    return buf.raw[: need.value].decode()
+
+
+def key_range(num_feature_dim: int, world: int, rank: int) -> Tuple[int, int]:
+    b, e = i64(), i64()
+    _check(lib.dlr_key_range(num_feature_dim, world, rank, C.byref(b), C.byref(e)))
+    return b.value, e.value
+
+
+def get_unique_id() -> bytes:
+    buf = C.create_string_buffer(UNIQUE_ID_BYTES)
+    _check(lib.dlr_get_unique_id(buf))
+    return buf.raw
+
+
+# ---------------------------------------------------------------- engine
+
+TIMER_MARGIN, TIMER_GRAD, TIMER_UPDATE, TIMER_EXCHANGE, TIMER_STEP = range(5)
+
+
+class Engine:
+    """One GPU context = one rank (dlr_ctx)."""
+
+    def __init__(self, num_feature_dim: int, device: int = 0, rank: int = 0, world: int = 1,
+                 unique_id: Optional[bytes] = None):
+        self.D = num_feature_dim
+        h = P()
+        uid = C.create_string_buffer(unique_id, UNIQUE_ID_BYTES) if unique_id is not None else None
+        _check(lib.dlr_create(device, rank, world, uid, num_feature_dim, C.byref(h)))
+        self._h = h
+        self.n_batches = 0
+
+    def _c(self, rc):
+        return _check(rc, self._h)
+
+    def set_weights(self, w: np.ndarray) -> None:
+        w = np.ascontiguousarray(w, dtype=np.float32)
+        self._c(lib.dlr_set_weights(self._h, _ptr(w), len(w)))
+
+    def get_weights(self) -> np.ndarray:
+        w = np.empty(self.D, dtype=np.float32)
+        self._c(lib.dlr_get_weights(self._h, _ptr(w), self.D))
+        return w
+
+    def load_train(self, ds: Dataset, batch_size: int) -> int:
+        nb = i64()
+        self._c(lib.dlr_load_train(self._h, ds.handle, batch_size, C.byref(nb)))
+        self.n_batches = nb.value
+        return nb.value
+
+    def load_test(self, ds: Dataset) -> None:
+        self._c(lib.dlr_load_test(self._h, ds.handle))
+
+    def train_step(self, batch: int, lr: float, C_: float = 1.0, mode: int = MODE_SYNC_MEAN) -> None:
+        self._c(lib.dlr_train_step(self._h, batch, lr, C_, mode))
+
+    def train_epoch(self, lr: float, C_: float = 1.0, mode: int = MODE_SYNC_MEAN) -> None:
+        self._c(lib.dlr_train_epoch(self._h, lr, C_, mode))
+
+    def predict(self) -> Tuple[int, int, float]:
+        c, n, ll = i64(), i64(), C.c_double()
+        self._c(lib.dlr_predict(self._h, C.byref(c), C.byref(n), C.byref(ll)))
+        return c.value, n.value, ll.value
+
+    def sync(self) -> None:
+        self._c(lib.dlr_sync(self._h))
+
+    def timing(self, enable: bool) -> None:
+        self._c(lib.dlr_timing(self._h, 1 if enable else 0))
+
+    def kernel_time(self, which: int) -> Tuple[float, int]:
+        ms, n = C.c_double(), i64()
+        self._c(lib.dlr_kernel_time(self._h, which, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def memory_info(self) -> Tuple[int, int]:
+        a, b = i64(), i64()
+        self._c(lib.dlr_memory_info(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def close(self) -> None:
+        if self._h:
+            lib.dlr_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

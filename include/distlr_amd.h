@@ -1,0 +1,191 @@
+/*
+ * distlr_amd.h -- C-ABI of the MI355X-native dist-lr training engine.
+ *
+ * This is the drop-in boundary for dist-lr's logistic-regression hot path
+ * (future-xy/dist-lr, reference at /root/reference).  Plain C types only:
+ * pointers, sizes, status codes.  No exceptions, no C++ or torch types cross
+ * it.  Every entry point names the reference interface it replaces.
+ *
+ * Conventions
+ *   - Return value: 0 = OK, < 0 = error (DLR_E_*).  dlr_last_error(ctx)
+ *     returns a message for the calling thread's last failure (ctx may be
+ *     NULL for failures that have no context yet).
+ *   - A dlr_ctx is one GPU = one rank, driven by exactly one host thread.
+ *   - The caller owns every host array it passes; the library owns device
+ *     buffers, datasets and contexts it returns (free with *_free/_destroy).
+ *   - Host-only entry points (parsing, batching, init, formatting, key
+ *     ranges) never touch a GPU and are safe without one.
+ */
+#ifndef DISTLR_AMD_H_
+#define DISTLR_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DLR_OK 0
+#define DLR_E_ARG (-1)      /* bad argument / shape mismatch            */
+#define DLR_E_IO (-2)       /* file cannot be opened / written          */
+#define DLR_E_PARSE (-3)    /* input the reference would hit UB on      */
+#define DLR_E_HIP (-4)      /* HIP runtime error                        */
+#define DLR_E_RCCL (-5)     /* RCCL error                               */
+#define DLR_E_NOMEM (-6)    /* host or device allocation failed         */
+#define DLR_E_STATE (-7)    /* call out of order (e.g. no data loaded)  */
+
+/* Server update semantics (main.cc:41-96, KVStoreDistServer::DataHandle). */
+#define DLR_MODE_SYNC_MEAN 0  /* intended sync merge: w -= fl32(lr*sum_r g_r)/W, sum in rank order */
+#define DLR_MODE_SYNC_LAST 1  /* what main.cc:71 does: only the last push (rank W-1) is applied /W */
+#define DLR_MODE_ASYNC 2      /* main.cc:79-84 per push, pushes applied in rank order           */
+
+typedef struct dlr_dataset dlr_dataset; /* host CSR shard (DataIter's storage) */
+typedef struct dlr_ctx dlr_ctx;         /* one GPU engine context (one rank)   */
+
+/* ------------------------------------------------------------------ */
+/* Host: reference parsing semantics (include/util.h, src/util.cc)      */
+/* ------------------------------------------------------------------ */
+
+/* replaces distlr::ToInt  -- src/util.cc:20-36 */
+int dlr_to_int(const char *str);
+/* replaces distlr::ToFloat -- src/util.cc:42-63 (digit accumulation, no sign/exponent) */
+float dlr_to_float(const char *str);
+/* replaces distlr::Split  -- src/util.cc:6-18; fields written NUL-separated
+ * into out; returns the field count, or DLR_E_ARG if cap is too small. */
+int dlr_split(const char *line, char separator, char *out, int cap);
+
+/* ------------------------------------------------------------------ */
+/* Host: datasets (include/data_iter.h, include/sample.h)              */
+/* ------------------------------------------------------------------ */
+
+/* replaces distlr::DataIter::DataIter(filename, num_feature_dim) --
+ * include/data_iter.h:16-35.  Parses a libsvm text shard into CSR with the
+ * reference's exact semantics (label = ToInt(tok0)==1; feature[ToInt(idx)-1]
+ * = ToFloat(val), last duplicate wins; a blank line reuses the previous
+ * token as its label).  Inputs the reference has undefined behaviour on
+ * (index outside [1,D], token without ':') return DLR_E_PARSE with the line
+ * number in the message.  nthreads <= 0 picks a default. */
+int dlr_dataset_load_libsvm(const char *path, int64_t num_feature_dim, int nthreads, dlr_dataset **out);
+
+/* Builds a dataset from caller CSR arrays (0-based ascending distinct
+ * columns per row; label 0/1).  Arrays are copied. */
+int dlr_dataset_from_csr(int64_t n_rows, int64_t num_feature_dim, const int64_t *row_ptr,
+                         const int32_t *col, const float *val, const int32_t *label, dlr_dataset **out);
+
+/* Seeded synthetic generator producing gen_data.py-shaped data
+ * (examples/gen_data.py:18-45 layout; see DESIGN.md "Synthetic data").
+ * value_mode 0: binary values "1"; 1: 4-decimal values in (0,1], held as
+ * ToFloat of their text so a written+reparsed file is bitwise identical.
+ * stream selects an independent row stream (part k of train, test, ...). */
+typedef struct dlr_gen_spec {
+    int64_t n_rows;
+    int64_t num_feature_dim;
+    int32_t nnz_per_row;    /* distinct uniform columns per row (<= D)   */
+    int32_t value_mode;     /* 0 binary, 1 four-decimal real             */
+    uint64_t seed;          /* data seed (planted model + rows)          */
+    uint64_t stream;        /* row stream id                             */
+    double positive_frac;   /* target fraction of +1 labels              */
+    double label_noise;     /* fraction of flipped labels                */
+    int32_t nthreads;       /* <= 0: default                             */
+} dlr_gen_spec;
+int dlr_dataset_generate(const dlr_gen_spec *spec, dlr_dataset **out);
+
+/* Writes a dataset as libsvm text ("+1 idx:val ...", 1-based indices). */
+int dlr_dataset_write_libsvm(const dlr_dataset *ds, const char *path, int value_mode);
+
+int dlr_dataset_info(const dlr_dataset *ds, int64_t *n_rows, int64_t *nnz, int64_t *num_feature_dim);
+/* Borrowed views of the CSR arrays (valid until dlr_dataset_free). */
+int dlr_dataset_view(const dlr_dataset *ds, const int64_t **row_ptr, const int32_t **col, const float **val,
+                     const int32_t **label);
+void dlr_dataset_free(dlr_dataset *ds);
+
+/* replaces DataIter::NextBatch/HasNext batching -- include/data_iter.h:40-59:
+ * ceil(N/B) batches per epoch (B < 0 means N); batch b holds rows
+ * (b*B + i) mod N, i in [0,B) (the last batch wraps to row 0). */
+int64_t dlr_num_batches(int64_t n_rows, int64_t batch_size);
+int dlr_batch_rows(int64_t n_rows, int64_t batch_size, int64_t batch, int64_t *rows_out);
+
+/* ------------------------------------------------------------------ */
+/* Host: model helpers (include/lr.h, src/lr.cc)                       */
+/* ------------------------------------------------------------------ */
+
+/* replaces LR::InitWeight_ -- src/lr.cc:92-98: srand(random_state);
+ * w_j = (float)rand()/(float)RAND_MAX.  glibc's TYPE_3 additive generator is
+ * restated here (thread-safe, no global state). */
+int dlr_init_weight(int random_state, float *w, int64_t num_feature_dim);
+
+/* replaces LR::SaveModel's text -- src/lr.cc:73-82: "D\n", each weight in
+ * default ostream format followed by ' ', then "\n".  Writes at most cap
+ * bytes; *needed receives the full length. */
+int dlr_format_model(const float *w, int64_t num_feature_dim, char *out, int64_t cap, int64_t *needed);
+
+/* Key-range ownership for the data-parallel exchange: rank r "serves" keys
+ * [begin, end) (the role of ps-lite's server key ranges, main.cc:98-101).
+ * Ranges are equal-sized chunks of ceil(D/world) (the last may be short or
+ * empty). */
+int dlr_key_range(int64_t num_feature_dim, int world, int rank, int64_t *begin, int64_t *end);
+
+/* ------------------------------------------------------------------ */
+/* Device engine (gfx950)                                              */
+/* ------------------------------------------------------------------ */
+
+/* RCCL bootstrap: rank 0 calls this and hands the 128 bytes to the others
+ * (replaces ps-lite's scheduler rendezvous, main.cc:173 ps::Start). */
+#define DLR_UNIQUE_ID_BYTES 128
+int dlr_get_unique_id(void *id_out);
+
+/* Creates the context of one rank on HIP device `device`.  world == 1 needs
+ * no unique id (NULL).  Replaces the worker-side construction in RunWorker
+ * (main.cc:135-138: KVWorker + LR) and the server (main.cc:116-122): with
+ * replicated weights each rank also serves its key range. */
+int dlr_create(int device, int rank, int world, const void *unique_id, int64_t num_feature_dim, dlr_ctx **out);
+void dlr_destroy(dlr_ctx *ctx);
+const char *dlr_last_error(const dlr_ctx *ctx);
+
+/* Weights: the initial push (main.cc:141-148) and PullWeight_ (lr.cc:116-124). */
+int dlr_set_weights(dlr_ctx *ctx, const float *w, int64_t num_feature_dim);
+int dlr_get_weights(dlr_ctx *ctx, float *w, int64_t num_feature_dim);
+
+/* K1: makes the shard resident in HBM with its batch plan for batch_size
+ * (DataIter + NextBatch, data_iter.h:16-59): CSR for the margin kernel and a
+ * per-batch column-major copy for the deterministic gradient.  Replaces the
+ * per-epoch re-parse + dense copies of main.cc:158-159.  *n_batches receives
+ * the batches per epoch. */
+int dlr_load_train(dlr_ctx *ctx, const dlr_dataset *ds, int64_t batch_size, int64_t *n_batches);
+/* Test shard (LR::Test's NextBatch(-1), lr.cc:49). */
+int dlr_load_test(dlr_ctx *ctx, const dlr_dataset *ds);
+
+/* One step of LR::Train's loop body (lr.cc:30-43) plus the server update
+ * (main.cc:57-84) for batch `batch` of the loaded shard: margin + sigmoid +
+ * residual (K2), segmented Xᵀr gradient + L2 (K3), key-range exchange over
+ * RCCL (world > 1), fused SGD update (K4).  Enqueued on the context's stream;
+ * returns without waiting.  lr/C are the server learning rate
+ * (LEARNING_RATE, main.cc:27) and LR's C (lr.h:10). */
+int dlr_train_step(dlr_ctx *ctx, int64_t batch, float learning_rate, float C, int mode);
+/* All batches of one epoch in order (LR::Train, lr.cc:28-45). */
+int dlr_train_epoch(dlr_ctx *ctx, float learning_rate, float C, int mode);
+
+/* LR::Test (lr.cc:47-63): counts (z > 0) == label over the test shard (K5);
+ * *logloss receives the summed log-loss (our addition; NULL to skip).
+ * Blocks until done. */
+int dlr_predict(dlr_ctx *ctx, int64_t *correct, int64_t *n_rows, double *logloss);
+
+/* Waits for all work on the context's stream. */
+int dlr_sync(dlr_ctx *ctx);
+
+/* Per-kernel timing with HIP events on the context's stream.  enable=1
+ * starts recording (clears totals); dlr_kernel_time returns the summed
+ * milliseconds and launch count of kernel `which` (0 margin, 1 gradient,
+ * 2 update/merge, 3 exchange, 4 step total) since enabling; syncs first. */
+int dlr_timing(dlr_ctx *ctx, int enable);
+int dlr_kernel_time(dlr_ctx *ctx, int which, double *total_ms, int64_t *launches);
+
+/* Device bytes resident for the loaded shards (for reporting). */
+int dlr_memory_info(dlr_ctx *ctx, int64_t *train_bytes, int64_t *test_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DISTLR_AMD_H_ */
