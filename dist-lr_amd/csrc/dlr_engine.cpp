@@ -12,6 +12,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -285,12 +286,19 @@ int dlr_create(int device, int rank, int world, const void *unique_id, int64_t D
     if ((rc = dev_alloc(c.get(), (void **)&c->correct, 64))) return rc;
     HIPC(c.get(), hipHostMalloc((void **)&c->h_correct, 64, hipHostMallocDefault));
     HIPC(c.get(), hipHostMalloc((void **)&c->h_ll, 64, hipHostMallocDefault));
-    if (world > 1) {
-        if ((rc = dev_alloc(c.get(), (void **)&c->g, (size_t)c->Dpad * 4))) return rc;
-        if ((rc = dev_alloc(c.get(), (void **)&c->recv, (size_t)c->Dpad * 4))) return rc;
-        HIPC(c.get(), hipMemset(c->g, 0, (size_t)c->Dpad * 4));
+    // Gradient + receive buffers serve both the RCCL exchange and the
+    // host-exchange (worker/server) entry points.
+    if ((rc = dev_alloc(c.get(), (void **)&c->g, (size_t)c->Dpad * 4))) return rc;
+    if ((rc = dev_alloc(c.get(), (void **)&c->recv, (size_t)c->Dpad * 4))) return rc;
+    HIPC(c.get(), hipMemset(c->g, 0, (size_t)c->Dpad * 4));
+    const char *force = getenv("DLR_FORCE_COLLECTIVES");
+    if (world > 1 || (force && strcmp(force, "1") == 0)) {
         ncclUniqueId id;
-        memcpy(&id, unique_id, sizeof(id));
+        if (world > 1) {
+            memcpy(&id, unique_id, sizeof(id));
+        } else {
+            NCCLC(c.get(), ncclGetUniqueId(&id));
+        }
         NCCLC(c.get(), ncclCommInitRank(&c->comm, world, id, rank));
     }
     *out = c.release();
@@ -471,7 +479,7 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
     time_begin(c, &t0);
     HIPC(c, dlr::launch_margin_residual(bt, c->w, c->resid, c->stream));
     time_end(c, 0, t0);
-    if (c->world == 1) {
+    if (!c->comm) {
         time_begin(c, &t0);
         HIPC(c, dlr::launch_grad(cs, c->D, c->resid, c->w, nullptr, bt.rows, lr, C, true, c->stream));
         time_end(c, 1, t0);
@@ -506,6 +514,36 @@ int dlr_train_epoch(dlr_ctx *c, float lr, float C, int mode) {
     return DLR_OK;
 }
 
+int dlr_worker_gradient(dlr_ctx *c, int64_t b, float C, float *grad_out, int64_t D) {
+    if (!c || !grad_out || D != c->D) return fail(c, DLR_E_ARG, "dlr_worker_gradient: bad argument");
+    if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_worker_gradient: no training shard loaded");
+    if (b < 0 || b >= (int64_t)c->train.plan.size())
+        return fail(c, DLR_E_ARG, "dlr_worker_gradient: batch out of range");
+    HIPC(c, hipSetDevice(c->device));
+    const dlr::DevBatch bt = batch_view(c, b);
+    const dlr::DevCsc cs = csc_view(c, b);
+    HIPC(c, dlr::launch_margin_residual(bt, c->w, c->resid, c->stream));
+    HIPC(c, dlr::launch_grad(cs, c->D, c->resid, c->w, c->g, bt.rows, 0.0f, C, false, c->stream));
+    HIPC(c, hipMemcpyAsync(grad_out, c->g, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return DLR_OK;
+}
+
+int dlr_server_apply(dlr_ctx *c, const float *grads, int W, int64_t D, float lr, int mode) {
+    if (!c || !grads || W <= 0 || D != c->D || mode < 0 || mode > 2)
+        return fail(c, DLR_E_ARG, "dlr_server_apply: bad argument");
+    HIPC(c, hipSetDevice(c->device));
+    float *buf = nullptr;
+    int rc = dev_alloc(c, (void **)&buf, (size_t)W * (size_t)D * 4);
+    if (rc) return rc;
+    hipError_t e = hipMemcpyAsync(buf, grads, (size_t)W * (size_t)D * 4, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = dlr::launch_merge_update(buf, W, D, D, c->w, lr, mode, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dev_free(c, buf);
+    if (e != hipSuccess) return fail(c, DLR_E_HIP, std::string("dlr_server_apply: ") + hipGetErrorString(e));
+    return DLR_OK;
+}
+
 int dlr_predict(dlr_ctx *c, int64_t *correct, int64_t *n_rows, double *logloss) {
     if (!c) return DLR_E_ARG;
     if (!c->test.loaded) return fail(c, DLR_E_STATE, "dlr_predict: no test shard loaded");
@@ -535,6 +573,12 @@ int dlr_timing(dlr_ctx *c, int enable) {
     HIPC(c, hipSetDevice(c->device));
     harvest(c);
     c->timing = enable != 0;
+    // Pre-create the events so recording never allocates inside a timed region.
+    while (c->timing && c->ev_pool.size() < 16384) {
+        hipEvent_t e;
+        HIPC(c, hipEventCreate(&e));
+        c->ev_pool.push_back(e);
+    }
     for (int i = 0; i < kTimers; ++i) {
         c->t_ms[i] = 0;
         c->t_n[i] = 0;

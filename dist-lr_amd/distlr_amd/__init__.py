@@ -33,7 +33,7 @@ SYMBOLS = [
     "dlr_init_weight", "dlr_format_model", "dlr_key_range",
     "dlr_get_unique_id", "dlr_create", "dlr_destroy", "dlr_last_error",
     "dlr_set_weights", "dlr_get_weights", "dlr_load_train", "dlr_load_test",
-    "dlr_train_step", "dlr_train_epoch", "dlr_predict", "dlr_sync",
+    "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
     "dlr_timing", "dlr_kernel_time", "dlr_memory_info",
 ]
 
@@ -92,6 +92,8 @@ _sig("dlr_load_train", C.c_int, P, P, i64, C.POINTER(i64))
 _sig("dlr_load_test", C.c_int, P, P)
 _sig("dlr_train_step", C.c_int, P, i64, C.c_float, C.c_float, C.c_int)
 _sig("dlr_train_epoch", C.c_int, P, C.c_float, C.c_float, C.c_int)
+_sig("dlr_worker_gradient", C.c_int, P, i64, C.c_float, P, i64)
+_sig("dlr_server_apply", C.c_int, P, P, C.c_int, i64, C.c_float, C.c_int)
 _sig("dlr_predict", C.c_int, P, C.POINTER(i64), C.POINTER(i64), C.POINTER(C.c_double))
 _sig("dlr_sync", C.c_int, P)
 _sig("dlr_timing", C.c_int, P, C.c_int)
@@ -300,6 +302,16 @@ class Engine:
 
     def train_epoch(self, lr: float, C_: float = 1.0, mode: int = MODE_SYNC_MEAN) -> None:
         self._c(lib.dlr_train_epoch(self._h, lr, C_, mode))
+
+    def worker_gradient(self, batch: int, C_: float = 1.0) -> np.ndarray:
+        g = np.empty(self.D, dtype=np.float32)
+        self._c(lib.dlr_worker_gradient(self._h, batch, C_, _ptr(g), self.D))
+        return g
+
+    def server_apply(self, grads, lr: float, mode: int = MODE_SYNC_MEAN) -> None:
+        G = np.ascontiguousarray(np.stack(grads) if isinstance(grads, (list, tuple)) else grads, dtype=np.float32)
+        assert G.ndim == 2 and G.shape[1] == self.D
+        self._c(lib.dlr_server_apply(self._h, _ptr(G), G.shape[0], self.D, lr, mode))
 
     def predict(self) -> Tuple[int, int, float]:
         c, n, ll = i64(), i64(), C.c_double()

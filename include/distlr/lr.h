@@ -1,0 +1,105 @@
+// distlr/lr.h -- drop-in for the reference's include/lr.h.
+//
+// Same class and methods (lr.h:8-54).  The single intentional API change:
+// the ps-lite handle ps::KVWorker<float>* becomes distlr::KVWorker*, a
+// handle on one rank of the MI355X engine (GPU, rank/world, RCCL id) that
+// also carries the server-side settings the reference reads in its
+// KVStoreDistServer (SYNC_MODE, LEARNING_RATE: main.cc:26-27).  As in the
+// reference, LR owns the handle it is given (lr.h:13-15 deletes it).
+#ifndef DISTLR_AMD_LR_H_
+#define DISTLR_AMD_LR_H_
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "distlr/data_iter.h"
+
+struct dlr_ctx;
+
+namespace distlr {
+
+// Replaces ps::KVWorker<float> + the server process.  world > 1 needs the
+// same 128-byte unique id on every rank (dlr_get_unique_id on rank 0).
+class KVWorker {
+   public:
+    KVWorker(int device, int rank, int world, const void *unique_id, float learning_rate, bool sync_mode,
+             int64_t num_feature_dim);
+    ~KVWorker();
+    KVWorker(const KVWorker &) = delete;
+    KVWorker &operator=(const KVWorker &) = delete;
+
+    dlr_ctx *ctx() const { return ctx_; }
+    int rank() const { return rank_; }
+    int world() const { return world_; }
+    float learning_rate() const { return learning_rate_; }
+    int mode() const;  // DLR_MODE_* from sync_mode
+    // Device residency cache: the shard currently resident for training
+    // (with its batch size) and for testing.
+    const Shard *train_shard = nullptr;
+    int64_t train_batch = 0;
+    int64_t train_batches = 0;
+    const Shard *test_shard = nullptr;
+    std::shared_ptr<Shard> train_keep, test_keep;
+
+   private:
+    dlr_ctx *ctx_ = nullptr;
+    int rank_, world_;
+    float learning_rate_;
+    bool sync_mode_;
+};
+
+class LR {
+   public:
+    explicit LR(int num_feature_dim, float learning_rate = 0.001, float C_ = 1, int random_state = 0);
+
+    virtual ~LR() { delete kv_; }
+
+    // Takes ownership; pushes this LR's initial weights (main.cc:141-148).
+    void SetKVWorker(KVWorker *kv);
+
+    void SetRank(int rank);
+
+    // lr.cc:28-45: one epoch over iter's remaining batches on the GPU
+    // (consumes iter like NextBatch does).
+    void Train(DataIter &iter, int num_iter, int batch_size);
+
+    // lr.cc:47-63: pulls the latest weights, evaluates the whole of iter on
+    // the GPU and prints "HH:MM:SS Iteration N, accuracy: A".
+    void Test(DataIter &iter, int num_iter);
+
+    // Last pulled weights (lr.cc:65-67).
+    std::vector<float> GetWeight();
+
+    KVWorker *GetKVWorker();
+
+    // lr.cc:73-82: text model of the last pulled weights.
+    bool SaveModel(std::string &filename);
+
+    // lr.cc:84-90
+    std::string DebugInfo();
+
+    // Not in the reference: the last Test's results.
+    int64_t last_correct() const { return last_correct_; }
+    int64_t last_total() const { return last_total_; }
+    double last_logloss() const { return last_logloss_; }
+
+   private:
+    void InitWeight_();
+    void PullWeight_();
+
+    int num_feature_dim_;
+    float learning_rate_;
+    float C_;
+    int random_state_;
+    int rank_ = 0;
+    std::vector<float> weight_;
+    KVWorker *kv_ = nullptr;
+    int64_t last_correct_ = 0, last_total_ = 0;
+    double last_logloss_ = 0;
+};
+
+}  // namespace distlr
+
+#endif  // DISTLR_AMD_LR_H_

@@ -136,7 +136,9 @@ int dlr_key_range(int64_t num_feature_dim, int world, int rank, int64_t *begin, 
 int dlr_get_unique_id(void *id_out);
 
 /* Creates the context of one rank on HIP device `device`.  world == 1 needs
- * no unique id (NULL).  Replaces the worker-side construction in RunWorker
+ * no unique id (NULL); with the environment variable DLR_FORCE_COLLECTIVES=1
+ * a world-1 context still runs the RCCL exchange path (a 1-rank
+ * communicator), for testing it on one GPU.  Replaces the worker-side construction in RunWorker
  * (main.cc:135-138: KVWorker + LR) and the server (main.cc:116-122): with
  * replicated weights each rank also serves its key range. */
 int dlr_create(int device, int rank, int world, const void *unique_id, int64_t num_feature_dim, dlr_ctx **out);
@@ -165,6 +167,17 @@ int dlr_load_test(dlr_ctx *ctx, const dlr_dataset *ds);
 int dlr_train_step(dlr_ctx *ctx, int64_t batch, float learning_rate, float C, int mode);
 /* All batches of one epoch in order (LR::Train, lr.cc:28-45). */
 int dlr_train_epoch(dlr_ctx *ctx, float learning_rate, float C, int mode);
+
+/* Parameter-server topology without RCCL (several contexts on one GPU, or a
+ * host-side exchange): the worker half and the server half of one step.
+ * dlr_worker_gradient: LR::Train's pushed vector for `batch` (lr.cc:34-43:
+ * K2 + K3 unfused, normalised + L2), copied to grad_out[D]; blocks.
+ * dlr_server_apply: KVStoreDistServer::DataHandle's update (main.cc:57-84)
+ * of the W pushes grads[W*D] (rank-major) to this context's weights (K4);
+ * blocks. */
+int dlr_worker_gradient(dlr_ctx *ctx, int64_t batch, float C, float *grad_out, int64_t num_feature_dim);
+int dlr_server_apply(dlr_ctx *ctx, const float *grads, int num_workers, int64_t num_feature_dim, float learning_rate,
+                     int mode);
 
 /* LR::Test (lr.cc:47-63): counts (z > 0) == label over the test shard (K5);
  * *logloss receives the summed log-loss (our addition; NULL to skip).
