@@ -241,8 +241,9 @@ void build_csc(const dlr_dataset &ds, const std::vector<dlr::BatchSpan> &plan, i
 dlr::DevBatch batch_view(const dlr_ctx *c, int64_t b) {
     const TrainShard &t = c->train;
     const dlr::BatchSpan &sp = t.plan[(size_t)b];
-    if (b == t.wrap_batch) return {t.w_row_ptr, t.w_col, t.w_val, t.w_label, sp.rows};
-    return {t.row_ptr + sp.first_row, t.col, t.val, t.label + sp.first_row, sp.rows};
+    const int64_t nnz = t.coff[(size_t)b + 1] - t.coff[(size_t)b];  // upper bound (aligned)
+    if (b == t.wrap_batch) return {t.w_row_ptr, t.w_col, t.w_val, t.w_label, sp.rows, nnz};
+    return {t.row_ptr + sp.first_row, t.col, t.val, t.label + sp.first_row, sp.rows, nnz};
 }
 
 dlr::DevCsc csc_view(const dlr_ctx *c, int64_t b) {
@@ -365,7 +366,8 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             }
         }
         if (e > (int64_t)UINT32_MAX) return fail(c, DLR_E_ARG, "dlr_load_train: batch has > 2^32 entries");
-        t.coff[(size_t)b + 1] = t.coff[(size_t)b] + e;
+        // 4-entry aligned batch bases: the kernels load entries 4 at a time.
+        t.coff[(size_t)b + 1] = (t.coff[(size_t)b] + e + 3) & ~int64_t(3);
     }
     const double cptr_bytes = (double)nb * (double)(D + 1) * 4.0;
     if (cptr_bytes > 64.0 * (1ull << 30))
@@ -550,7 +552,7 @@ int dlr_predict(dlr_ctx *c, int64_t *correct, int64_t *n_rows, double *logloss) 
     HIPC(c, hipSetDevice(c->device));
     const TestShard &t = c->test;
     HIPC(c, hipMemsetAsync(c->correct, 0, 8, c->stream));
-    const dlr::DevBatch bt{t.row_ptr, t.col, t.val, t.label, t.n_rows};
+    const dlr::DevBatch bt{t.row_ptr, t.col, t.val, t.label, t.n_rows, t.nnz};
     HIPC(c, dlr::launch_predict(bt, c->w, c->correct, c->ll + 1, c->ll, c->stream));
     HIPC(c, hipMemcpyAsync(c->h_correct, c->correct, 8, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipMemcpyAsync(c->h_ll, c->ll, 8, hipMemcpyDeviceToHost, c->stream));

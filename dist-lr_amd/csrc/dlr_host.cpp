@@ -316,7 +316,7 @@ extern "C" int dlr_dataset_load_libsvm(const char *path, int64_t num_feature_dim
 extern "C" int dlr_dataset_from_csr(int64_t n_rows, int64_t num_feature_dim, const int64_t *row_ptr,
                                     const int32_t *col, const float *val, const int32_t *label,
                                     dlr_dataset **out) {
-    if (!out || n_rows < 0 || num_feature_dim <= 0 || !row_ptr || !label) {
+    if (!out || n_rows < 0 || num_feature_dim <= 0 || !row_ptr || (n_rows > 0 && !label)) {
         set_error("dlr_dataset_from_csr: bad argument");
         return DLR_E_ARG;
     }
@@ -350,7 +350,7 @@ extern "C" int dlr_dataset_from_csr(int64_t n_rows, int64_t num_feature_dim, con
         ds->col.assign(col, col + nnz);
         ds->val.assign(val, val + nnz);
     }
-    ds->label.assign(label, label + n_rows);
+    if (n_rows > 0) ds->label.assign(label, label + n_rows);
     *out = ds.release();
     return DLR_OK;
 }

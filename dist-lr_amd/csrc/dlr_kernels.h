@@ -15,6 +15,7 @@ struct DevBatch {
     const float *val;
     const float *label;
     int64_t rows;
+    int64_t nnz;  // entries of the batch (row_ptr[rows] - row_ptr[0])
 };
 
 // One batch column-major: entries of column j are [ptr[j], ptr[j+1]) in

@@ -2,8 +2,9 @@
 //
 // Parity contract (DESIGN.md "Numerics"): every fp32 sum is
 // accumulated in the reference's order with separate multiply and add
-// (this file is compiled with -ffp-contract=off; tests check the ISA has no
-// v_fma in these kernels), so results are bitwise equal to src/lr.cc:
+// (this file is compiled with -ffp-contract=off; tests/test_abi.py checks
+// the ISA has no fused f32 op outside correctly-rounded divisions), so
+// results are bitwise equal to src/lr.cc:
 //   margin  z_i = sum_j w_j*x_ij, j ascending          (lr.cc:108-112)
 //   sigma_i = (float)(1/(1+exp(-(double)z_i)))          (lr.cc:113)
 //   r_i     = sigma_i - y_i                             (lr.cc:38)
@@ -11,14 +12,25 @@
 //   g_j     = fl32((double)G_j/B + (double)(fl32(C*w_j)/(float)B))  (lr.cc:40)
 //   update  w_j -= fl32(fl32(lr*g_j)/(float)W)          (main.cc:70-72)
 //
+// Both hot kernels are one primitive, an ORDERED SEGMENTED DOT: segment s
+// (a batch row for the margin, a feature column for the gradient) sums
+// fl32(table[idx_k] * val_k) over its entries k in storage order.  A wave
+// owns 64 consecutive segments, whose entries are contiguous.  Per window
+// of kWin entries the wave (1) loads idx/val ENTRY-parallel with 16-byte
+// loads (coalesced, balanced however ragged the segments are), (2) issues
+// every table gather of the window at once and forms the products, (3)
+// parks the products in LDS, and (4) each lane adds its own segment's
+// products in order.  Products do not depend on the order, the additions
+// do -- and those stay sequential, so the result is the reference's bits.
+//
 // Layout (DESIGN.md "Data layout in HBM"): the shard is resident as CSR
 // (row_ptr int64, col int32, val fp32, label fp32); each batch also has a
 // column-major copy (cptr uint32[D+1], batch-local row uint16/uint32, val
-// fp32) built once at load time, so the per-column gradient sums run in
-// batch-row order without atomics.
+// fp32) built once at load time.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "dlr_kernels.h"
 
@@ -27,8 +39,9 @@ namespace dlr {
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kMarginWaves = 4;    // waves per workgroup
-constexpr int kMarginWin = 1024;   // CSR entries staged per wave per window
+constexpr int kWaves = 4;      // waves per workgroup (independent)
+constexpr int kWin = 1024;     // entries per wave per window
+constexpr int kVec = 4;        // entries per lane per load
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -36,98 +49,152 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// z for the row owned by this lane.  One wave owns 64 consecutive batch
-// rows; their CSR entries are contiguous, so the wave stages them through
-// LDS in windows with 16-byte coalesced loads and every lane then walks its
-// own row in column order (the reference's summation order).
-__device__ __forceinline__ float wave_row_margin(const DevBatch &bt, const float *__restrict__ w, int64_t row0,
-                                                 int lane, int32_t *s_col, float *s_val, bool valid, int64_t my) {
-    const int64_t rlast = min(row0 + kWave, bt.rows);
-    const int64_t e0 = bt.row_ptr[row0];
-    const int64_t e1 = bt.row_ptr[rlast];
-    const int64_t a = valid ? bt.row_ptr[my] : e1;
-    const int64_t b = valid ? bt.row_ptr[my + 1] : e1;
-    float z = 0.0f;
-    for (int64_t ws = e0 & ~int64_t(3); ws < e1; ws += kMarginWin) {
+template <typename T>
+struct Vec4;
+template <>
+struct Vec4<int32_t> {
+    using type = int4;
+};
+template <>
+struct Vec4<uint32_t> {
+    using type = uint4;
+};
+template <>
+struct Vec4<uint16_t> {
+    using type = ushort4;
+};
+
+// Sum over this lane's segment [a, b) of fl32(table[idx[k]] * val[k]), in
+// k order.  The wave's entries are [e0, e1).  lds: kWin floats of this wave.
+// Only lanes < SEG own a segment; all 64 lanes load and gather.
+template <typename IdxT>
+__device__ __forceinline__ float ordered_segment_dot(int64_t e0, int64_t e1, int64_t a, int64_t b, int lane,
+                                                     const IdxT *__restrict__ idx, const float *__restrict__ val,
+                                                     const float *__restrict__ table, float *lds) {
+    using IV = typename Vec4<IdxT>::type;
+    constexpr int kT = kWin / (kVec * kWave);
+    constexpr int kChunk = kVec * kWave;  // entries per (t) step of the wave
+    const int64_t base = e0 & ~int64_t(kVec - 1);
+    float acc = 0.0f;
+    for (int64_t ws = base; ws < e1; ws += kWin) {
+        const int64_t left = e1 - ws;  // wave-uniform
+        // (1) index/value loads of the window's chunks that hold entries
+        // (wave-uniform skip), branch-free inside a chunk: a lane past the
+        // last entry re-reads the chunk's first vector (masked below).
+        IV iv[kT];
+        float4 v[kT];
 #pragma unroll
-        for (int t = 0; t < kMarginWin / (4 * kWave); ++t) {
-            const int o = (t * kWave + lane) * 4;
-            const int64_t g = ws + o;
-            if (g < e1) {
-                const int4 c = *reinterpret_cast<const int4 *>(bt.col + g);
-                const float4 v = *reinterpret_cast<const float4 *>(bt.val + g);
-                *reinterpret_cast<int4 *>(s_col + o) = c;
-                *reinterpret_cast<float4 *>(s_val + o) = v;
+        for (int t = 0; t < kT; ++t) {
+            if (t * kChunk < left) {
+                const int64_t e = ws + t * kChunk + lane * kVec;
+                const int64_t ec = e < e1 ? e : ws + t * kChunk;
+                iv[t] = *reinterpret_cast<const IV *>(idx + ec);
+                v[t] = *reinterpret_cast<const float4 *>(val + ec);
+            }
+        }
+        // (2) every gather of the window, then the products.  Entries outside
+        // [e0, e1) belong to no segment of this wave: index 0, product 0.
+        float g[kT][kVec];
+#pragma unroll
+        for (int t = 0; t < kT; ++t) {
+            if (t * kChunk < left) {
+                const int64_t e = ws + t * kChunk + lane * kVec;
+                const unsigned i0 = (e >= e0 && e < e1) ? (unsigned)iv[t].x : 0u;
+                const unsigned i1 = (e + 1 >= e0 && e + 1 < e1) ? (unsigned)iv[t].y : 0u;
+                const unsigned i2 = (e + 2 >= e0 && e + 2 < e1) ? (unsigned)iv[t].z : 0u;
+                const unsigned i3 = (e + 3 >= e0 && e + 3 < e1) ? (unsigned)iv[t].w : 0u;
+                g[t][0] = table[i0];
+                g[t][1] = table[i1];
+                g[t][2] = table[i2];
+                g[t][3] = table[i3];
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < kT; ++t) {
+            if (t * kChunk < left) {
+                const int o = t * kChunk + lane * kVec;
+                const int64_t e = ws + o;
+                float4 p;
+                p.x = (e >= e0 && e < e1) ? g[t][0] * v[t].x : 0.0f;
+                p.y = (e + 1 >= e0 && e + 1 < e1) ? g[t][1] * v[t].y : 0.0f;
+                p.z = (e + 2 >= e0 && e + 2 < e1) ? g[t][2] * v[t].z : 0.0f;
+                p.w = (e + 3 >= e0 && e + 3 < e1) ? g[t][3] * v[t].w : 0.0f;
+                *reinterpret_cast<float4 *>(lds + o) = p;
             }
         }
         wave_sync();
+        // (3) this lane's segment, in order; 8 LDS reads in flight per step.
         const int64_t lo = a > ws ? a : ws;
-        const int64_t hi = b < ws + kMarginWin ? b : ws + kMarginWin;
+        const int64_t hi = b < ws + kWin ? b : ws + kWin;
         int o = (int)(lo - ws);
         const int oe = (int)(hi - ws);
-        for (; o + 4 <= oe; o += 4) {
-            const float w0 = w[s_col[o]], w1 = w[s_col[o + 1]], w2 = w[s_col[o + 2]], w3 = w[s_col[o + 3]];
-            const float p0 = w0 * s_val[o];
-            z = z + p0;
-            const float p1 = w1 * s_val[o + 1];
-            z = z + p1;
-            const float p2 = w2 * s_val[o + 2];
-            z = z + p2;
-            const float p3 = w3 * s_val[o + 3];
-            z = z + p3;
+        for (; o + 8 <= oe; o += 8) {
+            const float x0 = lds[o], x1 = lds[o + 1], x2 = lds[o + 2], x3 = lds[o + 3];
+            const float x4 = lds[o + 4], x5 = lds[o + 5], x6 = lds[o + 6], x7 = lds[o + 7];
+            acc = acc + x0;
+            acc = acc + x1;
+            acc = acc + x2;
+            acc = acc + x3;
+            acc = acc + x4;
+            acc = acc + x5;
+            acc = acc + x6;
+            acc = acc + x7;
         }
-        for (; o < oe; ++o) {
-            const float p = w[s_col[o]] * s_val[o];
-            z = z + p;
-        }
+        for (; o < oe; ++o) acc = acc + lds[o];
         wave_sync();
     }
-    return z;
+    return acc;
 }
 
 __device__ __forceinline__ float sigmoid_ref(float z) {
     // lr.cc:113: 1. / (1. + exp(-z)) in double (glibc double exp there,
-    // OCML's correctly-rounded-to-<1ulp f64 exp here), returned as float.
+    // OCML's f64 exp here), returned as float.
     const double e = exp(-(double)z);
     return (float)(1.0 / (1.0 + e));
 }
 
-__global__ __launch_bounds__(kMarginWaves *kWave) void k_margin_residual(DevBatch bt, const float *__restrict__ w,
-                                                                         float *__restrict__ resid) {
-    __shared__ int32_t s_col[kMarginWaves][kMarginWin];
-    __shared__ float s_val[kMarginWaves][kMarginWin];
+// K2: margin + sigmoid + residual.  A wave owns SEG consecutive batch rows
+// (lane l < SEG owns row row0 + l); SEG < 64 gives small batches more waves
+// to hide latency with (the loads and gathers still use all 64 lanes).
+template <int SEG>
+__global__ __launch_bounds__(kWaves *kWave) void k_margin_residual(DevBatch bt, const float *__restrict__ w,
+                                                                   float *__restrict__ resid) {
+    __shared__ float s_p[kWaves][kWin];
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
-    const int64_t row0 = ((int64_t)blockIdx.x * kMarginWaves + wv) * kWave;
+    const int64_t row0 = ((int64_t)blockIdx.x * kWaves + wv) * SEG;
     if (row0 >= bt.rows) return;  // wave-uniform
     const int64_t my = row0 + lane;
-    const bool valid = my < bt.rows;
-    const float z = wave_row_margin(bt, w, row0, lane, s_col[wv], s_val[wv], valid, my);
-    if (valid) {
-        const float s = sigmoid_ref(z);
-        resid[my] = s - bt.label[my];
-    }
+    const bool valid = lane < SEG && my < bt.rows;
+    const float y = valid ? bt.label[my] : 0.0f;
+    const int64_t rlast = min(row0 + SEG, bt.rows);
+    const int64_t e0 = bt.row_ptr[row0], e1 = bt.row_ptr[rlast];
+    const int64_t a = valid ? bt.row_ptr[my] : e1, b = valid ? bt.row_ptr[my + 1] : e1;
+    const float z = ordered_segment_dot<int32_t>(e0, e1, a, b, lane, bt.col, bt.val, w, s_p[wv]);
+    if (valid) resid[my] = sigmoid_ref(z) - y;
 }
 
 __device__ __forceinline__ double softplus(double t) { return t > 0 ? t + log1p(exp(-t)) : log1p(exp(t)); }
 
-// LR::Test / Predict_ (lr.cc:47-63, 100-106): pred = z > 0; correct count by
-// wave ballot (integer atomics: order-free), log-loss partial per workgroup
-// in a fixed shuffle order (deterministic for a fixed grid).
-__global__ __launch_bounds__(kMarginWaves *kWave) void k_predict(DevBatch bt, const float *__restrict__ w,
-                                                                 unsigned long long *__restrict__ correct,
-                                                                 double *__restrict__ ll_part) {
-    __shared__ int32_t s_col[kMarginWaves][kMarginWin];
-    __shared__ float s_val[kMarginWaves][kMarginWin];
-    __shared__ double s_ll[kMarginWaves];
+// K5: LR::Test / Predict_ (lr.cc:47-63, 100-106): pred = z > 0; correct
+// count by wave ballot (integer atomics: order-free), log-loss partial per
+// workgroup in a fixed order (deterministic for a fixed grid).
+__global__ __launch_bounds__(kWaves *kWave) void k_predict(DevBatch bt, const float *__restrict__ w,
+                                                           unsigned long long *__restrict__ correct,
+                                                           double *__restrict__ ll_part) {
+    __shared__ float s_p[kWaves][kWin];
+    __shared__ double s_ll[kWaves];
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
-    const int64_t row0 = ((int64_t)blockIdx.x * kMarginWaves + wv) * kWave;
+    const int64_t row0 = ((int64_t)blockIdx.x * kWaves + wv) * kWave;
     double ll = 0.0;
     if (row0 < bt.rows) {
         const int64_t my = row0 + lane;
         const bool valid = my < bt.rows;
-        const float z = wave_row_margin(bt, w, row0, lane, s_col[wv], s_val[wv], valid, my);
+        const int64_t rlast = min(row0 + kWave, bt.rows);
+        const int64_t e0 = bt.row_ptr[row0], e1 = bt.row_ptr[rlast];
+        const int64_t a = valid ? bt.row_ptr[my] : e1, b = valid ? bt.row_ptr[my + 1] : e1;
+        const float z = ordered_segment_dot<int32_t>(e0, e1, a, b, lane, bt.col, bt.val, w, s_p[wv]);
         bool hit = false;
         if (valid) {
             const float y = bt.label[my];
@@ -144,7 +211,7 @@ __global__ __launch_bounds__(kMarginWaves *kWave) void k_predict(DevBatch bt, co
     __syncthreads();
     if (threadIdx.x == 0) {
         double t = 0.0;
-        for (int i = 0; i < kMarginWaves; ++i) t += s_ll[i];
+        for (int i = 0; i < kWaves; ++i) t += s_ll[i];
         ll_part[blockIdx.x] = t;
     }
 }
@@ -157,24 +224,29 @@ __global__ void k_sum_partials(const double *__restrict__ part, int n, double *_
     }
 }
 
-// K3 (+K4 when FUSED): one thread per feature column j walks the batch's
-// column-major segment in batch-row order, so G_j is the reference's
-// sequential fp32 sum; then the lr.cc:40 normalisation + L2 term.  FUSED
-// (world == 1) applies the server update in place: with W == 1,
-// fl32(fl32(lr*g)/1.0f) == fl32(lr*g) for every mode (main.cc:71, 81).
+// K3 (+K4 when FUSED): one lane per feature column, the column's segment
+// in batch-row order -> G_j is the reference's sequential fp32 sum; then
+// the lr.cc:40 normalisation + L2 term.  FUSED (single rank) applies the
+// server update in place: with W == 1, fl32(fl32(lr*g)/1.0f) == fl32(lr*g)
+// for every mode (main.cc:71, 81).
 template <typename RowT, bool FUSED>
-__global__ __launch_bounds__(256) void k_grad(DevCsc cs, const RowT *__restrict__ crow, int64_t D,
-                                              const float *__restrict__ resid, float *__restrict__ w,
-                                              float *__restrict__ gout, float Bf, double Bd, float lr, float C) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= D) return;
-    const uint32_t s = cs.ptr[j], e = cs.ptr[j + 1];
-    float G = 0.0f;
-    for (uint32_t k = s; k < e; ++k) {
-        const float p = resid[crow[k]] * cs.val[k];
-        G = G + p;
-    }
-    const float wj = w[j];
+__global__ __launch_bounds__(kWaves *kWave) void k_grad(DevCsc cs, const RowT *__restrict__ crow, int64_t D,
+                                                        const float *__restrict__ resid, float *__restrict__ w,
+                                                        float *__restrict__ gout, float Bf, double Bd, float lr,
+                                                        float C) {
+    __shared__ float s_p[kWaves][kWin];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    const int64_t j0 = ((int64_t)blockIdx.x * kWaves + wv) * kWave;
+    if (j0 >= D) return;  // wave-uniform
+    const int64_t j = j0 + lane;
+    const bool valid = j < D;
+    const float wj = valid ? w[j] : 0.0f;
+    const int64_t jl = min(j0 + kWave, D);
+    const int64_t e0 = cs.ptr[j0], e1 = cs.ptr[jl];
+    const int64_t a = valid ? (int64_t)cs.ptr[j] : e1, b = valid ? (int64_t)cs.ptr[j + 1] : e1;
+    const float G = ordered_segment_dot<RowT>(e0, e1, a, b, lane, crow, cs.val, resid, s_p[wv]);
+    if (!valid) return;
     const float cw = C * wj;
     const float l2 = cw / Bf;
     const float g = (float)((double)G / Bd + (double)l2);
@@ -216,20 +288,44 @@ inline unsigned grid_for(int64_t n, int per_block) { return (unsigned)((n + per_
 
 }  // namespace
 
+// Rows per wave for the margin: aim for about one window of entries per
+// wave (fewer, longer-running waves for short rows; more for long rows).
+int margin_seg(const DevBatch &bt) {
+    static const int forced = [] {
+        const char *e = getenv("DLR_MARGIN_SEG");
+        return e ? atoi(e) : 0;
+    }();
+    if (forced == 16 || forced == 32 || forced == 64) return forced;
+    if (bt.rows <= 0) return 64;
+    const double avg = (double)bt.nnz / (double)bt.rows;
+    if (avg * 64 <= kWin) return 64;
+    if (avg * 32 <= kWin) return 32;
+    return 16;
+}
+
 hipError_t launch_margin_residual(const DevBatch &bt, const float *w, float *resid, hipStream_t s) {
     if (bt.rows <= 0) return hipSuccess;
-    const unsigned grid = grid_for(bt.rows, kMarginWaves * kWave);
-    hipLaunchKernelGGL(k_margin_residual, dim3(grid), dim3(kMarginWaves * kWave), 0, s, bt, w, resid);
+    const dim3 blk(kWaves * kWave);
+    switch (margin_seg(bt)) {
+        case 16:
+            hipLaunchKernelGGL(k_margin_residual<16>, dim3(grid_for(bt.rows, kWaves * 16)), blk, 0, s, bt, w, resid);
+            break;
+        case 32:
+            hipLaunchKernelGGL(k_margin_residual<32>, dim3(grid_for(bt.rows, kWaves * 32)), blk, 0, s, bt, w, resid);
+            break;
+        default:
+            hipLaunchKernelGGL(k_margin_residual<64>, dim3(grid_for(bt.rows, kWaves * 64)), blk, 0, s, bt, w, resid);
+    }
     return hipGetLastError();
 }
 
-int predict_grid(int64_t rows) { return rows <= 0 ? 0 : (int)grid_for(rows, kMarginWaves * kWave); }
+int predict_grid(int64_t rows) { return rows <= 0 ? 0 : (int)grid_for(rows, kWaves * kWave); }
 
 hipError_t launch_predict(const DevBatch &bt, const float *w, unsigned long long *correct, double *ll_part,
                           double *ll_out, hipStream_t s) {
     const int grid = predict_grid(bt.rows);
     if (grid > 0)
-        hipLaunchKernelGGL(k_predict, dim3(grid), dim3(kMarginWaves * kWave), 0, s, bt, w, correct, ll_part);
+        hipLaunchKernelGGL(k_predict, dim3(grid), dim3(kWaves * kWave), 0, s, bt, w, correct, ll_part);
     hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(64), 0, s, ll_part, grid, ll_out);
     return hipGetLastError();
 }
@@ -237,25 +333,26 @@ hipError_t launch_predict(const DevBatch &bt, const float *w, unsigned long long
 hipError_t launch_grad(const DevCsc &cs, int64_t D, const float *resid, float *w, float *gout, int64_t B, float lr,
                        float C, bool fused, hipStream_t s) {
     if (D <= 0) return hipSuccess;
-    const unsigned grid = grid_for(D, 256);
+    const unsigned grid = grid_for(D, kWaves * kWave);
+    const dim3 blk(kWaves * kWave);
     const float Bf = (float)B;
     const double Bd = (double)B;
     if (cs.row16) {
         const uint16_t *r = static_cast<const uint16_t *>(cs.row);
         if (fused)
-            hipLaunchKernelGGL((k_grad<uint16_t, true>), dim3(grid), dim3(256), 0, s, cs, r, D, resid, w, gout, Bf,
-                               Bd, lr, C);
+            hipLaunchKernelGGL((k_grad<uint16_t, true>), dim3(grid), blk, 0, s, cs, r, D, resid, w, gout, Bf, Bd, lr,
+                               C);
         else
-            hipLaunchKernelGGL((k_grad<uint16_t, false>), dim3(grid), dim3(256), 0, s, cs, r, D, resid, w, gout, Bf,
-                               Bd, lr, C);
+            hipLaunchKernelGGL((k_grad<uint16_t, false>), dim3(grid), blk, 0, s, cs, r, D, resid, w, gout, Bf, Bd,
+                               lr, C);
     } else {
         const uint32_t *r = static_cast<const uint32_t *>(cs.row);
         if (fused)
-            hipLaunchKernelGGL((k_grad<uint32_t, true>), dim3(grid), dim3(256), 0, s, cs, r, D, resid, w, gout, Bf,
-                               Bd, lr, C);
+            hipLaunchKernelGGL((k_grad<uint32_t, true>), dim3(grid), blk, 0, s, cs, r, D, resid, w, gout, Bf, Bd, lr,
+                               C);
         else
-            hipLaunchKernelGGL((k_grad<uint32_t, false>), dim3(grid), dim3(256), 0, s, cs, r, D, resid, w, gout, Bf,
-                               Bd, lr, C);
+            hipLaunchKernelGGL((k_grad<uint32_t, false>), dim3(grid), blk, 0, s, cs, r, D, resid, w, gout, Bf, Bd,
+                               lr, C);
     }
     return hipGetLastError();
 }

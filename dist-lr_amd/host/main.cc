@@ -1,0 +1,167 @@
+// main.cc -- `distlr`, the drop-in for the reference's bin/distlr
+// (src/main.cc:124-181) on MI355X.
+//
+// Same configuration (environment variables, examples/local.sh:12-19):
+//   DATA_DIR, NUM_FEATURE_DIM, NUM_ITERATION, BATCH_SIZE, TEST_INTERVAL,
+//   SYNC_MODE ("1" = sync), LEARNING_RATE (parsed with ToFloat, main.cc:27)
+// and the worker count DMLC_NUM_WORKER (local.sh:24).  Same files:
+// DATA_DIR/train/part-00{r+1}, DATA_DIR/test/part-001,
+// DATA_DIR/models/part-00{r+1}.  Same output lines.
+//
+// Topology: one process, one thread per worker (rank).  With at least as
+// many GPUs as workers each rank owns a GPU and gradients are exchanged
+// over RCCL (all-to-all of key ranges + rank-ordered merge + all-gather);
+// with more workers than GPUs (e.g. local.sh's 2 workers on one GPU) the
+// workers share GPUs and exchange through the in-process ParamServer.
+// Optional: DISTLR_GPUS (GPUs to use), DISTLR_TOPOLOGY=ps|rccl,
+// DISTLR_SYNC_MERGE=last (main.cc:71 as written instead of the mean).
+// Missing variables are reported (the reference dereferences NULL).
+#include <hip/hip_runtime_api.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "distlr/data_iter.h"
+#include "distlr/lr.h"
+#include "distlr/util.h"
+#include "distlr_amd.h"
+
+namespace {
+
+std::mutex g_out;
+
+const char *need_env(const char *name) {
+    const char *v = getenv(name);
+    if (!v) {
+        std::cerr << "distlr: environment variable " << name << " is not set" << std::endl;
+        exit(2);
+    }
+    return v;
+}
+
+struct Config {
+    std::string root;
+    int num_feature_dim, num_iteration, batch_size, test_interval, workers;
+    bool sync_mode;
+    float learning_rate;
+};
+
+// main.cc:124-170 for one rank.
+void run_worker(const Config &cfg, int rank, distlr::KVWorker *kv, std::vector<int> *failed) {
+    try {
+        {
+            std::lock_guard<std::mutex> g(g_out);
+            std::cout << 0 << "I got a rank " << rank << std::endl;
+        }
+        distlr::LR lr = distlr::LR(cfg.num_feature_dim);
+        lr.SetKVWorker(kv);
+        lr.SetRank(rank);
+        {
+            std::lock_guard<std::mutex> g(g_out);
+            std::cout << "Worker[" << rank << "]: start working..." << std::endl;
+        }
+        for (int i = 0; i < cfg.num_iteration; ++i) {
+            std::string train_filename = cfg.root + "/train/part-00" + std::to_string(rank + 1);
+            distlr::DataIter iter(train_filename, cfg.num_feature_dim);
+            lr.Train(iter, i, cfg.batch_size);
+            if (rank == 0 && (i + 1) % cfg.test_interval == 0) {
+                std::string test_filename = cfg.root + "/test/part-001";
+                distlr::DataIter test_iter(test_filename, cfg.num_feature_dim);
+                std::lock_guard<std::mutex> g(g_out);
+                lr.Test(test_iter, i + 1);
+            }
+        }
+        std::string modelfile = cfg.root + "/models/part-00" + std::to_string(rank + 1);
+        lr.SaveModel(modelfile);
+    } catch (const std::exception &e) {
+        std::lock_guard<std::mutex> g(g_out);
+        std::cerr << "distlr: worker " << rank << ": " << e.what() << std::endl;
+        (*failed)[(size_t)rank] = 1;
+    }
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    (void)argc;
+    (void)argv;  // like the reference, configuration comes from the environment
+    Config cfg;
+    cfg.root = need_env("DATA_DIR");
+    cfg.num_feature_dim = distlr::ToInt(need_env("NUM_FEATURE_DIM"));
+    cfg.num_iteration = distlr::ToInt(need_env("NUM_ITERATION"));
+    cfg.batch_size = distlr::ToInt(need_env("BATCH_SIZE"));
+    cfg.test_interval = distlr::ToInt(need_env("TEST_INTERVAL"));
+    cfg.sync_mode = !strcmp(need_env("SYNC_MODE"), "1");
+    cfg.learning_rate = distlr::ToFloat(need_env("LEARNING_RATE"));
+    const char *nw = getenv("DMLC_NUM_WORKER");
+    cfg.workers = nw ? distlr::ToInt(nw) : 1;
+    if (cfg.workers < 1 || cfg.num_feature_dim < 1 || cfg.test_interval == 0) {
+        std::cerr << "distlr: bad configuration" << std::endl;
+        return 2;
+    }
+    std::cout << "Server mode: " << (cfg.sync_mode ? "sync" : "async") << std::endl;
+
+    int ngpu = 0;
+    if (hipGetDeviceCount(&ngpu) != hipSuccess || ngpu < 1) {
+        std::cerr << "distlr: no GPU visible" << std::endl;
+        return 3;
+    }
+    if (const char *g = getenv("DISTLR_GPUS")) ngpu = std::max(1, std::min(ngpu, atoi(g)));
+    std::string topo = getenv("DISTLR_TOPOLOGY") ? getenv("DISTLR_TOPOLOGY") : "";
+    const bool use_rccl = topo == "rccl" || (topo != "ps" && cfg.workers <= ngpu);
+    if (use_rccl && cfg.workers > ngpu) {
+        std::cerr << "distlr: DISTLR_TOPOLOGY=rccl needs one GPU per worker" << std::endl;
+        return 2;
+    }
+
+    std::vector<int> failed((size_t)cfg.workers, 0);
+    std::vector<std::thread> th;
+    std::unique_ptr<distlr::ParamServer> ps;
+    std::vector<distlr::KVWorker *> kvs((size_t)cfg.workers, nullptr);
+    try {
+        if (use_rccl) {
+            char uid[DLR_UNIQUE_ID_BYTES] = {0};
+            if (cfg.workers > 1 && dlr_get_unique_id(uid) != DLR_OK) {
+                std::cerr << "distlr: " << dlr_last_error(nullptr) << std::endl;
+                return 4;
+            }
+            // Communicator creation is collective: create every rank's
+            // context concurrently (this is the barrier of main.cc:150).
+            std::vector<std::thread> init;
+            std::vector<std::string> err((size_t)cfg.workers);
+            for (int r = 0; r < cfg.workers; ++r)
+                init.emplace_back([&, r] {
+                    try {
+                        kvs[(size_t)r] = new distlr::KVWorker(r, r, cfg.workers, uid, cfg.learning_rate,
+                                                              cfg.sync_mode, cfg.num_feature_dim);
+                    } catch (const std::exception &e) {
+                        err[(size_t)r] = e.what();
+                    }
+                });
+            for (auto &t : init) t.join();
+            for (auto &e : err)
+                if (!e.empty()) throw std::runtime_error(e);
+        } else {
+            ps.reset(new distlr::ParamServer(0, cfg.workers, cfg.learning_rate, cfg.sync_mode,
+                                             cfg.num_feature_dim));
+            for (int r = 0; r < cfg.workers; ++r)
+                kvs[(size_t)r] = new distlr::KVWorker(r % ngpu, r, ps.get(), cfg.learning_rate, cfg.sync_mode,
+                                                      cfg.num_feature_dim);
+        }
+    } catch (const std::exception &e) {
+        std::cerr << "distlr: " << e.what() << std::endl;
+        return 4;
+    }
+    for (int r = 0; r < cfg.workers; ++r) th.emplace_back(run_worker, std::cref(cfg), r, kvs[(size_t)r], &failed);
+    for (auto &t : th) t.join();
+    for (int f : failed)
+        if (f) return 1;
+    return 0;
+}

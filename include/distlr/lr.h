@@ -20,12 +20,41 @@ struct dlr_ctx;
 
 namespace distlr {
 
+// In-process parameter server for the parameter-server topology: W worker
+// threads that may share GPUs push their gradients, the server context
+// merges them in rank order once all W arrived (main.cc:57-84) and every
+// worker pulls the result.  Used when there are more workers than GPUs
+// (e.g. local.sh's 2 workers on one GPU); one GPU per worker uses RCCL.
+class ParamServer {
+   public:
+    ParamServer(int device, int num_workers, float learning_rate, bool sync_mode, int64_t num_feature_dim);
+    ~ParamServer();
+    ParamServer(const ParamServer &) = delete;
+    ParamServer &operator=(const ParamServer &) = delete;
+
+    // The first push initialises the weights (main.cc:50-56).
+    void Init(const std::vector<float> &w);
+    void Pull(std::vector<float> &w);
+    // Blocks until the step of all W pushes has been applied.
+    void Push(int rank, const std::vector<float> &grad);
+    int num_workers() const { return num_workers_; }
+
+   private:
+    struct State;
+    State *st_;
+    int num_workers_;
+};
+
 // Replaces ps::KVWorker<float> + the server process.  world > 1 needs the
 // same 128-byte unique id on every rank (dlr_get_unique_id on rank 0).
 class KVWorker {
    public:
     KVWorker(int device, int rank, int world, const void *unique_id, float learning_rate, bool sync_mode,
              int64_t num_feature_dim);
+    // Parameter-server topology: this worker's own context on `device`,
+    // exchanging through `ps` (not owned).
+    KVWorker(int device, int rank, ParamServer *ps, float learning_rate, bool sync_mode, int64_t num_feature_dim);
+    ParamServer *ps() const { return ps_; }
     ~KVWorker();
     KVWorker(const KVWorker &) = delete;
     KVWorker &operator=(const KVWorker &) = delete;
@@ -45,6 +74,7 @@ class KVWorker {
 
    private:
     dlr_ctx *ctx_ = nullptr;
+    ParamServer *ps_ = nullptr;
     int rank_, world_;
     float learning_rate_;
     bool sync_mode_;

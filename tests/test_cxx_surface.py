@@ -1,0 +1,65 @@
+"""The C++ drop-in surface (include/distlr/*.h: Split/ToInt/ToFloat,
+DataIter, Sample) against the reference-built goldens, through
+bin/distlr_tool (host only)."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+import pytest
+
+from conftest import GOLDEN, ROOT, read_golden_json
+from parse_format import sha
+
+TOOL = os.path.join(ROOT, "dist-lr_amd", "bin", "distlr_tool")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def built():
+    if not os.path.exists(TOOL):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "dist-lr_amd", "host")], check=True)
+
+
+def tool(*args) -> str:
+    return subprocess.run([TOOL, *map(str, args)], check=True, capture_output=True).stdout.decode("latin-1")
+
+
+def test_kat_matches_reference():
+    with open(os.path.join(GOLDEN, "kat.tsv"), encoding="latin-1") as f:
+        assert tool("kat", os.path.join(GOLDEN, "kat_strings.txt")) == f.read()
+
+
+def test_quirk_parse_and_batches_match_reference():
+    q = os.path.join(GOLDEN, "quirks", "quirks.libsvm")
+    with open(os.path.join(GOLDEN, "quirks", "quirks.parse.txt")) as f:
+        assert tool("parse", q, 10) == f.read()
+    for B in (3, 5, -1, 25):
+        with open(os.path.join(GOLDEN, "quirks", f"quirks.batches_B{B}.txt")) as f:
+            assert tool("batches", q, 10, B) == f.read()
+
+
+def test_parse_and_batch_digests_match_reference():
+    g = read_golden_json("golden.json")
+    for rel, meta in g["parse"].items():
+        assert sha(tool("parse", os.path.join(GOLDEN, rel), meta["D"])) == meta["sha256"], rel
+    for key, meta in g["batches"].items():
+        rel = key.split("@")[0]
+        assert sha(tool("batches", os.path.join(GOLDEN, rel), meta["D"], meta["B"])) == meta["sha256"], key
+
+
+def test_sample_debuginfo_format():
+    out = tool("debuginfo", os.path.join(GOLDEN, "quirks", "quirks.libsvm"), 10).splitlines()
+    # sample.h:49-57: label, then " i:v" with 0-based i and std::to_string(v)
+    assert out[0] == "1 0:0.500000 2:2.250000"
+    assert out[2] == "0 1:6273.000000 3:-29.500000"
+
+
+def test_bad_index_is_an_error(tmp_path):
+    p = tmp_path / "bad.libsvm"
+    p.write_text("+1 1:1 11:1\n")
+    r = subprocess.run([TOOL, "parse", str(p), "10"], capture_output=True)
+    assert r.returncode == 1 and b"outside [1, num_feature_dim]" in r.stderr
+
+
+def test_missing_file_is_empty_like_reference(tmp_path):
+    assert tool("parse", tmp_path / "nope", 10) == "n 0\n"
