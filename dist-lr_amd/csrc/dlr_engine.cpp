@@ -137,12 +137,17 @@ void dev_free(dlr_ctx *c, void *p) {
     (void)hipFree(p);
 }
 
+// Every setup copy/memset is ordered on the context's own stream: it is a
+// non-blocking stream, so null-stream operations (hipMemset/hipMemcpy) would
+// NOT be ordered before the kernels that follow.  The copy is synchronous
+// (pageable source), so `src` may be freed on return.
 template <typename T>
 int upload(dlr_ctx *c, T **dst, const T *src, size_t n, size_t pad = 0) {
     int rc = dev_alloc(c, (void **)dst, (n + pad) * sizeof(T));
     if (rc) return rc;
-    if (n) HIPC(c, hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
-    if (pad) HIPC(c, hipMemset(*dst + n, 0, pad * sizeof(T)));
+    if (n) HIPC(c, hipMemcpyAsync(*dst, src, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
+    if (pad) HIPC(c, hipMemsetAsync(*dst + n, 0, pad * sizeof(T), c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
     return DLR_OK;
 }
 
@@ -283,7 +288,7 @@ int dlr_create(int device, int rank, int world, const void *unique_id, int64_t D
     HIPC(c.get(), hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     int rc;
     if ((rc = dev_alloc(c.get(), (void **)&c->w, (size_t)c->Dpad * 4))) return rc;
-    HIPC(c.get(), hipMemset(c->w, 0, (size_t)c->Dpad * 4));
+    HIPC(c.get(), hipMemsetAsync(c->w, 0, (size_t)c->Dpad * 4, c->stream));
     if ((rc = dev_alloc(c.get(), (void **)&c->correct, 64))) return rc;
     HIPC(c.get(), hipHostMalloc((void **)&c->h_correct, 64, hipHostMallocDefault));
     HIPC(c.get(), hipHostMalloc((void **)&c->h_ll, 64, hipHostMallocDefault));
@@ -291,7 +296,8 @@ int dlr_create(int device, int rank, int world, const void *unique_id, int64_t D
     // host-exchange (worker/server) entry points.
     if ((rc = dev_alloc(c.get(), (void **)&c->g, (size_t)c->Dpad * 4))) return rc;
     if ((rc = dev_alloc(c.get(), (void **)&c->recv, (size_t)c->Dpad * 4))) return rc;
-    HIPC(c.get(), hipMemset(c->g, 0, (size_t)c->Dpad * 4));
+    HIPC(c.get(), hipMemsetAsync(c->g, 0, (size_t)c->Dpad * 4, c->stream));
+    HIPC(c.get(), hipStreamSynchronize(c->stream));
     const char *force = getenv("DLR_FORCE_COLLECTIVES");
     if (world > 1 || (force && strcmp(force, "1") == 0)) {
         ncclUniqueId id;
