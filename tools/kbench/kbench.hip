@@ -1,0 +1,802 @@
+// kbench.hip -- kernel-design microbenchmarks for the C2 train step
+// (B = 65,536 rows x 50 nnz over D = 1M features).  Development tool only:
+// times candidate margin / gradient kernels against the production ones
+// (dlr_kernels.hip, included below) and checks them bitwise.
+//
+//   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -I include -I dist-lr_amd/csrc \
+//         tools/kbench/kbench.hip -o tools/kbench/kbench && ./tools/kbench/kbench
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../dist-lr_amd/csrc/dlr_kernels.hip"
+
+#define CK(x)                                                                                         \
+    do {                                                                                              \
+        hipError_t e_ = (x);                                                                          \
+        if (e_ != hipSuccess) {                                                                       \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_));          \
+            exit(1);                                                                                  \
+        }                                                                                             \
+    } while (0)
+
+namespace kb {
+
+struct Rng {
+    uint64_t s;
+    uint64_t next() {
+        s += 0x9E3779B97F4A7C15ull;
+        uint64_t z = s;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    }
+    uint32_t below(uint32_t n) { return (uint32_t)((next() >> 32) * (uint64_t)n >> 32); }
+};
+
+__device__ __forceinline__ float sig(float z) {
+    const double e = exp(-(double)z);
+    return (float)(1.0 / (1.0 + e));
+}
+
+// ---------------- micro: streams and gathers
+__global__ __launch_bounds__(256) void mb_empty(float *out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && out[0] == 12345.0f) out[1] = 1.0f;
+}
+
+__global__ __launch_bounds__(256) void mb_stream(const int4 *idx, const float4 *val, float *out, int64_t n4) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= n4) return;
+    const int4 i = idx[t];
+    const float4 v = val[t];
+    out[t] = (float)(i.x + i.y + i.z + i.w) + v.x + v.y + v.z + v.w;
+}
+
+__global__ __launch_bounds__(256) void mb_gather(const int4 *idx, const float *table, unsigned mask, float *out,
+                                                 int64_t n4) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= n4) return;
+    const int4 i = idx[t];
+    out[t] = table[i.x & mask] + table[i.y & mask] + table[i.z & mask] + table[i.w & mask];
+}
+
+// Many gathers in flight per lane: G int4 index loads (grid-strided,
+// coalesced), then 4G gathers.
+template <int G>
+__global__ __launch_bounds__(256) void mb_gather_g(const int4 *idx, const float *table, unsigned mask, float *out,
+                                                   int64_t n4) {
+    const int64_t nth = (int64_t)gridDim.x * 256;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    float s = 0.0f;
+    for (int64_t base = t; base < n4; base += nth * G) {
+        int4 iv[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int64_t q = base + g * nth;
+            iv[g] = q < n4 ? idx[q] : make_int4(0, 0, 0, 0);
+        }
+        float x[G][4];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            x[g][0] = table[iv[g].x & mask];
+            x[g][1] = table[iv[g].y & mask];
+            x[g][2] = table[iv[g].z & mask];
+            x[g][3] = table[iv[g].w & mask];
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) s += x[g][0] + x[g][1] + x[g][2] + x[g][3];
+    }
+    out[t] = s;
+}
+
+// ---------------- K2 candidates
+// Lane per row, entries read straight from the row (4 at a time), U in flight.
+template <int U>
+__global__ __launch_bounds__(256) void k2_lpr(dlr::DevBatch bt, const float *__restrict__ w,
+                                              float *__restrict__ resid) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= bt.rows) return;
+    const int64_t a = bt.row_ptr[i], b = bt.row_ptr[i + 1];
+    const float y = bt.label[i];
+    float acc = 0.0f;
+    for (int64_t k = a; k < b; k += U) {
+        int c[U];
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            c[u] = bt.col[k + u];
+            v[u] = bt.val[k + u];
+        }
+        float g[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) g[u] = w[(k + u < b) ? c[u] : 0];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (k + u < b) acc = acc + g[u] * v[u];
+    }
+    resid[i] = sig(acc) - y;
+}
+
+// ---------------- K3 candidates
+// Lane per column: the column's segment read straight (U entries at a time).
+template <int U, bool FUSED>
+__global__ __launch_bounds__(256) void k3_lpc(dlr::DevCsc cs, const uint16_t *__restrict__ crow, int64_t D,
+                                              const float *__restrict__ resid, float *__restrict__ w,
+                                              float *__restrict__ gout, float Bf, double Bd, float lr, float C) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= D) return;
+    const uint32_t a = cs.ptr[j], b = cs.ptr[j + 1];
+    const float wj = w[j];
+    float acc = 0.0f;
+    for (uint32_t k = a; k < b; k += U) {
+        unsigned r[U];
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            r[u] = crow[k + u];
+            v[u] = cs.val[k + u];
+        }
+        float rr[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) rr[u] = resid[r[u]];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (k + u < b) acc = acc + rr[u] * v[u];
+    }
+    const float cw = C * wj;
+    const float l2 = cw / Bf;
+    const float g = (float)((double)acc / Bd + (double)l2);
+    if (FUSED) {
+        const float step = lr * g;
+        w[j] = wj - step;
+    } else {
+        gout[j] = g;
+    }
+}
+
+// K3 with the residual table in LDS: one 1024-thread workgroup per CU,
+// rows processed in phases of R rows (R*4 bytes of LDS).  Lane per column;
+// each lane prefetches U entries of its column into registers, then per
+// phase adds (in order) those whose row falls in the phase.  Columns with
+// more than U entries continue from global memory.
+template <int U, int NG, bool FUSED>
+__global__ __launch_bounds__(1024) void k3_lds(dlr::DevCsc cs, const uint16_t *__restrict__ crow, int64_t D, int64_t B,
+                                               int R, int gpw, const float *__restrict__ resid, float *__restrict__ w,
+                                               float *__restrict__ gout, float Bf, double Bd, float lr, float C) {
+    extern __shared__ __attribute__((aligned(16))) float s_r[];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int64_t g0 = (int64_t)blockIdx.x * gpw;
+    unsigned k[NG], b[NG], k0[NG];
+    float acc[NG];
+    unsigned short rr[NG][U];
+    float vv[NG][U];
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+        const int64_t g = g0 + wv + 16 * gi;
+        const int64_t j = g * 64 + lane;
+        const bool ok = (wv + 16 * gi) < gpw && j < D;
+        k[gi] = ok ? cs.ptr[j] : 0u;
+        b[gi] = ok ? cs.ptr[j + 1] : 0u;
+        k0[gi] = k[gi];
+        acc[gi] = 0.0f;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool in = k[gi] + u < b[gi];
+            rr[gi][u] = in ? crow[k[gi] + u] : (unsigned short)0;
+            vv[gi][u] = in ? cs.val[k[gi] + u] : 0.0f;
+        }
+    }
+    for (int64_t lo = 0; lo < B; lo += R) {
+        const int n = (int)min((int64_t)R, B - lo);
+        __syncthreads();
+        for (int i = threadIdx.x * 4; i < n; i += 4096) {
+            if (i + 4 <= n) {
+                *reinterpret_cast<float4 *>(s_r + i) = *reinterpret_cast<const float4 *>(resid + lo + i);
+            } else {
+                for (int q = i; q < n; ++q) s_r[q] = resid[lo + q];
+            }
+        }
+        __syncthreads();
+        const unsigned hi = (unsigned)(lo + n);
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const unsigned e = k0[gi] + u;
+                if (e < b[gi] && e >= k[gi] && rr[gi][u] < hi) {
+                    acc[gi] = acc[gi] + s_r[rr[gi][u] - (unsigned)lo] * vv[gi][u];
+                    k[gi] = e + 1;
+                }
+            }
+            // overflow: entries beyond the prefetched U
+            while (k[gi] >= k0[gi] + U && k[gi] < b[gi]) {
+                const unsigned r = crow[k[gi]];
+                if (r >= hi) break;
+                acc[gi] = acc[gi] + s_r[r - (unsigned)lo] * cs.val[k[gi]];
+                k[gi] += 1;
+            }
+        }
+    }
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+        const int64_t g = g0 + wv + 16 * gi;
+        const int64_t j = g * 64 + lane;
+        if ((wv + 16 * gi) >= gpw || j >= D) continue;
+        const float wj = w[j];
+        const float cw = C * wj;
+        const float l2 = cw / Bf;
+        const float gr = (float)((double)acc[gi] / Bd + (double)l2);
+        if (FUSED) {
+            const float step = lr * gr;
+            w[j] = wj - step;
+        } else {
+            gout[j] = gr;
+        }
+    }
+}
+
+// K3 windowed with the residual table in LDS (phases of R rows).  A wave
+// owns column groups of 64 (lane = column); per phase and per window of
+// kW entries it loads crow/cval entry-parallel (ushort4 + float4), forms
+// products for entries whose row is in the phase (others: a sentinel), and
+// each lane continues its column's ordered sum from where the previous
+// phase stopped, until the sentinel (rows ascend within a column, so the
+// in-phase entries are contiguous).
+constexpr unsigned kSentinel = 0x7FBADBADu;
+__device__ unsigned long long *g_stamp = nullptr;  // diagnostic builds only (MODE 9)
+__device__ __forceinline__ void stamp(int slot) {
+    if (threadIdx.x == 0) {
+        unsigned long long t = __builtin_amdgcn_s_memrealtime();
+        g_stamp[blockIdx.x * 8 + slot] = t;
+    }
+}
+template <int NG, int kW, bool FUSED>
+__global__ __launch_bounds__(1024) void k3_ldsw(dlr::DevCsc cs, const uint16_t *__restrict__ crow, int64_t D,
+                                                int64_t B, int R, int gpw, const float *__restrict__ resid,
+                                                float *__restrict__ w, float *__restrict__ gout, float Bf, double Bd,
+                                                float lr, float C) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float *s_r = smem;                       // R floats
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    float *s_p = smem + R + wv * kW;         // kW floats per wave
+    const int64_t g0 = (int64_t)blockIdx.x * gpw;
+    unsigned pos[NG], end[NG];
+    float acc[NG];
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+        const int64_t j = (g0 + wv + 16 * gi) * 64 + lane;
+        const bool ok = (wv + 16 * gi) < gpw && j < D;
+        pos[gi] = ok ? cs.ptr[j] : 0u;
+        end[gi] = ok ? cs.ptr[j + 1] : 0u;
+        acc[gi] = 0.0f;
+    }
+    for (int64_t lo = 0; lo < B; lo += R) {
+        const int n = (int)min((int64_t)R, B - lo);
+        __syncthreads();
+        for (int i = threadIdx.x * 4; i < n; i += 4096) {
+            if (i + 4 <= n) {
+                *reinterpret_cast<float4 *>(s_r + i) = *reinterpret_cast<const float4 *>(resid + lo + i);
+            } else {
+                for (int q = i; q < n; ++q) s_r[q] = resid[lo + q];
+            }
+        }
+        __syncthreads();
+        const unsigned ulo = (unsigned)lo, uhi = (unsigned)(lo + n);
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) {
+            if (wv + 16 * gi >= gpw) break;  // wave-uniform
+            const int64_t gcol = (g0 + wv + 16 * gi) * 64;
+            if (gcol >= D) break;
+            const int64_t jl = min(gcol + 64, D);
+            const unsigned e0 = cs.ptr[gcol], e1 = cs.ptr[jl];
+            bool open = pos[gi] < end[gi];
+            for (unsigned ws = e0 & ~3u; ws < e1; ws += kW) {
+                // (1) loads + (2) LDS gathers -> products (sentinel if out of phase)
+#pragma unroll
+                for (int t = 0; t < kW / 256; ++t) {
+                    const unsigned o = t * 256 + lane * 4;
+                    if (ws + t * 256 < e1) {
+                        const unsigned e = ws + o;
+                        const ushort4 r4 = *reinterpret_cast<const ushort4 *>(crow + e);
+                        const float4 v4 = *reinterpret_cast<const float4 *>(cs.val + e);
+                        float4 p;
+                        const unsigned r0 = r4.x, r1 = r4.y, r2 = r4.z, r3 = r4.w;
+                        p.x = (r0 >= ulo && r0 < uhi) ? s_r[r0 - ulo] * v4.x : __uint_as_float(kSentinel);
+                        p.y = (r1 >= ulo && r1 < uhi) ? s_r[r1 - ulo] * v4.y : __uint_as_float(kSentinel);
+                        p.z = (r2 >= ulo && r2 < uhi) ? s_r[r2 - ulo] * v4.z : __uint_as_float(kSentinel);
+                        p.w = (r3 >= ulo && r3 < uhi) ? s_r[r3 - ulo] * v4.w : __uint_as_float(kSentinel);
+                        *reinterpret_cast<float4 *>(s_p + o) = p;
+                    }
+                }
+                dlr::wave_sync();
+                // (3) ordered continuation of this lane's column
+                if (open) {
+                    unsigned o = pos[gi] > ws ? pos[gi] - ws : 0u;
+                    const unsigned oe = min(end[gi], ws + kW) - ws;
+                    if (pos[gi] < ws + kW) {
+                        float a = acc[gi];
+                        for (; o < oe; ++o) {
+                            const float x = s_p[o];
+                            if (__float_as_uint(x) == kSentinel) {
+                                open = false;
+                                break;
+                            }
+                            a = a + x;
+                        }
+                        acc[gi] = a;
+                        pos[gi] = ws + o;
+                    }
+                }
+                dlr::wave_sync();
+            }
+        }
+    }
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+        const int64_t j = (g0 + wv + 16 * gi) * 64 + lane;
+        if ((wv + 16 * gi) >= gpw || j >= D) continue;
+        const float wj = w[j];
+        const float cw = C * wj;
+        const float l2 = cw / Bf;
+        const float gr = (float)((double)acc[gi] / Bd + (double)l2);
+        if (FUSED) {
+            const float step = lr * gr;
+            w[j] = wj - step;
+        } else {
+            gout[j] = gr;
+        }
+    }
+}
+
+// K3 "prefetch": every load a wave needs is issued up front -- the first
+// window (256 entries) of each of its NG column groups, w, and its share of
+// the residual fills -- so the kernel pays about one memory latency; the
+// windows stay in registers across the row phases.  Groups with more than
+// one window continue through a separate slow path (its own loads), so the
+// fast path never waits for the next phase's fill loads.
+template <int NG, int FILL, bool FUSED, int MODE = 0>
+__global__ __launch_bounds__(1024) void k3_pf(dlr::DevCsc cs, const uint16_t *__restrict__ crow, int64_t D,
+                                              int64_t B, int gpw, const float *__restrict__ resid,
+                                              float *__restrict__ w, float *__restrict__ gout, float Bf, double Bd,
+                                              float lr, float C) {
+    constexpr int R = FILL * 4096;
+    constexpr int kW = 256;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float *s_r = smem;
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    float *s_p = smem + R + wv * kW;
+    const int64_t g0 = (int64_t)blockIdx.x * gpw;
+    unsigned pos[NG], end[NG], ws0[NG], e1[NG];
+    float acc[NG], wj[NG];
+    bool open[NG];
+    ushort4 rq[NG];
+    float4 vq[NG];
+    // Prologue: every load unconditional (clamped, in-bounds addresses;
+    // values selected afterwards) -- a load inside a divergent branch makes
+    // the compiler wait for it at the join.
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+        const int64_t gcol = (g0 + wv + 16 * gi) * 64;
+        const bool gv = (wv + 16 * gi) < gpw && gcol < D;
+        const int64_t gc = gcol < D ? gcol : D;
+        const int64_t j = gcol + lane;
+        const bool ok = gv && j < D;
+        const int64_t jc = j < D ? j : D - 1;
+        const unsigned p0 = cs.ptr[jc], p1 = cs.ptr[jc + 1];
+        const unsigned e0 = cs.ptr[gc], e1v = cs.ptr[min(gc + 64, D)];
+        const float wv_ = w[jc];
+        pos[gi] = ok ? p0 : 0u;
+        end[gi] = ok ? p1 : 0u;
+        e1[gi] = gv ? e1v : 0u;
+        ws0[gi] = gv ? (e0 & ~3u) : 0u;
+        acc[gi] = 0.0f;
+        wj[gi] = wv_;
+    }
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+        const unsigned e = ws0[gi] + lane * 4;
+        const bool in = e < e1[gi];
+        const unsigned ec = in ? e : (e1[gi] & ~3u);
+        const ushort4 r4 = *reinterpret_cast<const ushort4 *>(crow + ec);
+        const float4 v4 = *reinterpret_cast<const float4 *>(cs.val + ec);
+        rq[gi] = in ? r4 : make_ushort4(0, 0, 0, 0);
+        vq[gi] = in ? v4 : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float4 fr[FILL];
+    auto fill_load = [&](int64_t lo) {
+#pragma unroll
+        for (int f = 0; f < FILL; ++f) {
+            const int64_t i = lo + (int64_t)(f * 1024 + threadIdx.x) * 4;
+            fr[f] = *reinterpret_cast<const float4 *>(resid + i);  // resid padded to a multiple of R
+        }
+    };
+    // products of one 256-entry window (sentinel outside the phase), then
+    // each lane continues its column's ordered sum
+    auto window = [&](const ushort4 r4, const float4 v4, unsigned ws, unsigned ulo, unsigned uhi, int gi) {
+        float4 p;
+        const unsigned r0 = r4.x, r1 = r4.y, r2 = r4.z, r3 = r4.w;
+        p.x = (r0 >= ulo && r0 < uhi) ? s_r[r0 - ulo] * v4.x : __uint_as_float(kSentinel);
+        p.y = (r1 >= ulo && r1 < uhi) ? s_r[r1 - ulo] * v4.y : __uint_as_float(kSentinel);
+        p.z = (r2 >= ulo && r2 < uhi) ? s_r[r2 - ulo] * v4.z : __uint_as_float(kSentinel);
+        p.w = (r3 >= ulo && r3 < uhi) ? s_r[r3 - ulo] * v4.w : __uint_as_float(kSentinel);
+        *reinterpret_cast<float4 *>(s_p + lane * 4) = p;
+        dlr::wave_sync();
+        if (open[gi] && pos[gi] < ws + kW) {
+            unsigned o = pos[gi] - ws;
+            const unsigned oe = min(end[gi], ws + kW) - ws;
+            float a = acc[gi];
+            bool op = true;
+            while (op && o < oe) {
+                float x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = s_p[min(o + u, (unsigned)kW - 1)];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const bool take = op && (o < oe) && __float_as_uint(x[u]) != kSentinel;
+                    if (take) a = a + x[u];
+                    op = op && (o >= oe || take);
+                    o += take ? 1u : 0u;
+                }
+            }
+            open[gi] = op;
+            acc[gi] = a;
+            pos[gi] = ws + o;
+        }
+        dlr::wave_sync();
+    };
+    if (MODE == 9) stamp(0);
+    fill_load(0);
+    for (int64_t lo = 0; lo < B; lo += R) {
+        __syncthreads();
+        if (MODE == 9) stamp(1 + 2 * (int)(lo / R));
+#pragma unroll
+        for (int f = 0; f < FILL; ++f) *reinterpret_cast<float4 *>(s_r + (f * 1024 + threadIdx.x) * 4) = fr[f];
+        if (lo + R < B) fill_load(lo + R);  // next phase's fill in flight during this phase
+        __syncthreads();
+        const unsigned ulo = (unsigned)lo, uhi = (unsigned)min(lo + R, B);
+        if (MODE == 9) stamp(2 + 2 * (int)(lo / R));
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) open[gi] = pos[gi] < end[gi];
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) {
+            if ((wv + 16 * gi) >= gpw || (g0 + wv + 16 * gi) * 64 >= D) break;  // wave-uniform
+            window(rq[gi], vq[gi], ws0[gi], ulo, uhi, gi);
+        }
+        // slow path: groups with more than one window (their own loads)
+        for (int gi = 0; gi < NG; ++gi) {
+            if ((wv + 16 * gi) >= gpw || (g0 + wv + 16 * gi) * 64 >= D) break;
+            for (unsigned ws = ws0[gi] + kW; ws < e1[gi]; ws += kW) {
+                const unsigned e = ws + lane * 4;
+                const bool in = e < e1[gi];
+                const ushort4 r4 = in ? *reinterpret_cast<const ushort4 *>(crow + e) : make_ushort4(0, 0, 0, 0);
+                const float4 v4 = in ? *reinterpret_cast<const float4 *>(cs.val + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+                window(r4, v4, ws, ulo, uhi, gi);
+            }
+        }
+    }
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+        const int64_t j = (g0 + wv + 16 * gi) * 64 + lane;
+        if ((wv + 16 * gi) >= gpw || j >= D) continue;
+        const float cw = C * wj[gi];
+        const float l2 = cw / Bf;
+        const float gr = (float)((double)acc[gi] / Bd + (double)l2);
+        if (FUSED) {
+            const float step = lr * gr;
+            w[j] = wj[gi] - step;
+        } else {
+            gout[j] = gr;
+        }
+    }
+    if (MODE == 9) {
+        __syncthreads();
+        stamp(5);
+    }
+}
+
+}  // namespace kb
+
+using namespace kb;
+
+template <typename F>
+static float time_us(int reps, F &&launch) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i) launch();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(a, 0));
+    for (int i = 0; i < reps; ++i) launch();
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    CK(hipGetLastError());
+    return ms * 1000.0f / reps;
+}
+
+template <typename T>
+static T *dup(const std::vector<T> &h, size_t pad = 64) {
+    T *d = nullptr;
+    CK(hipMalloc(&d, (h.size() + pad) * sizeof(T)));
+    CK(hipMemset(d, 0, (h.size() + pad) * sizeof(T)));
+    CK(hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+    return d;
+}
+
+static int cmp_bits(const float *da, const float *db, size_t n, const char *what) {
+    std::vector<float> a(n), b(n);
+    CK(hipMemcpy(a.data(), da, n * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), db, n * 4, hipMemcpyDeviceToHost));
+    size_t bad = 0;
+    for (size_t i = 0; i < n; ++i)
+        if (memcmp(&a[i], &b[i], 4) != 0) ++bad;
+    printf("  check %-28s %s (%zu of %zu differ)\n", what, bad ? "MISMATCH" : "bitwise equal", bad, n);
+    return bad ? 1 : 0;
+}
+
+int main(int argc, char **argv) {
+    const int64_t B = argc > 1 ? atoll(argv[1]) : 65536;
+    const int64_t D = argc > 2 ? atoll(argv[2]) : 1000000;
+    const int nnz = argc > 3 ? atoi(argv[3]) : 50;
+    const int reps = argc > 4 ? atoi(argv[4]) : 200;
+    printf("kbench: B=%lld D=%lld nnz=%d reps=%d\n", (long long)B, (long long)D, nnz, reps);
+
+    // ---- host data: distinct sorted uniform columns, 4-decimal values
+    Rng rng{10};
+    std::vector<int64_t> rp(B + 1);
+    std::vector<int32_t> col;
+    std::vector<float> val;
+    std::vector<float> lab(B);
+    col.reserve(B * nnz);
+    val.reserve(B * nnz);
+    std::vector<int32_t> row;
+    for (int64_t i = 0; i < B; ++i) {
+        rp[i] = (int64_t)col.size();
+        row.clear();
+        while ((int)row.size() < nnz) {
+            int32_t c = (int32_t)rng.below((uint32_t)D);
+            if (std::find(row.begin(), row.end(), c) == row.end()) row.push_back(c);
+        }
+        std::sort(row.begin(), row.end());
+        for (int32_t c : row) {
+            col.push_back(c);
+            val.push_back((float)(1 + rng.below(10000)) * 1e-4f);
+        }
+        lab[i] = (float)(rng.below(4) == 0);
+    }
+    rp[B] = (int64_t)col.size();
+    const int64_t E = (int64_t)col.size();
+    // CSC (stable by row)
+    std::vector<uint32_t> cptr(D + 1, 0);
+    for (int64_t k = 0; k < E; ++k) ++cptr[col[k] + 1];
+    for (int64_t j = 0; j < D; ++j) cptr[j + 1] += cptr[j];
+    std::vector<uint32_t> cur(cptr.begin(), cptr.end() - 1);
+    std::vector<uint16_t> crow(E);
+    std::vector<float> cval(E);
+    for (int64_t i = 0; i < B; ++i)
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+            const uint32_t p = cur[col[k]]++;
+            crow[p] = (uint16_t)i;
+            cval[p] = val[k];
+        }
+    std::vector<float> w0(D);
+    for (int64_t j = 0; j < D; ++j) w0[j] = (float)rng.below(1 << 24) / (float)(1 << 24);
+
+    int64_t *d_rp = dup(rp);
+    int32_t *d_col = dup(col);
+    float *d_val = dup(val);
+    float *d_lab = dup(lab);
+    uint32_t *d_cptr = dup(cptr);
+    uint16_t *d_crow = dup(crow);
+    float *d_cval = dup(cval);
+    float *d_w = dup(w0);
+    float *d_w2 = dup(w0);
+    float *d_r = nullptr, *d_r2 = nullptr, *d_out = nullptr, *d_g = nullptr, *d_g2 = nullptr;
+    CK(hipMalloc(&d_r, B * 4));
+    CK(hipMalloc(&d_r2, B * 4));
+    CK(hipMalloc(&d_g, D * 4));
+    CK(hipMalloc(&d_g2, D * 4));
+    CK(hipMalloc(&d_out, (E / 4 + 1024) * 4));
+    const dlr::DevBatch bt{d_rp, d_col, d_val, d_lab, B, E};
+    const dlr::DevCsc cs{d_cptr, d_crow, d_cval, true};
+    const double mb_k2 = (double)E * 8 + B * 8;      // col+val, row_ptr+label
+    const double mb_k3 = (double)E * 6 + (D + 1) * 4 + D * 8;  // crow+cval, cptr, w r/w
+    printf("entries %lld; K2 bytes %.1f MB, K3 bytes %.1f MB\n", (long long)E, mb_k2 / 1e6, mb_k3 / 1e6);
+    auto rate = [](double bytes, float us) { return bytes / (us * 1e-6) / 1e9; };
+
+    // ---- micro
+    const int64_t n4 = E / 4;
+    const unsigned g4 = (unsigned)((n4 + 255) / 256);
+    float t;
+    t = time_us(reps, [&] { hipLaunchKernelGGL(mb_empty, dim3(1024), dim3(256), 0, 0, d_out); });
+    printf("mb_empty(1024 WG)          %8.2f us\n", t);
+    t = time_us(reps, [&] {
+        hipLaunchKernelGGL(mb_stream, dim3(g4), dim3(256), 0, 0, (const int4 *)d_col, (const float4 *)d_val, d_out, n4);
+    });
+    printf("mb_stream col+val          %8.2f us  %7.1f GB/s\n", t, rate(E * 8.0 + n4 * 4.0, t));
+    t = time_us(reps, [&] {
+        hipLaunchKernelGGL(mb_gather, dim3(g4), dim3(256), 0, 0, (const int4 *)d_col, d_w, 0xFFFFFFFFu, d_out, n4);
+    });
+    printf("mb_gather w (4 MB table)   %8.2f us  %7.1f Gelem/s\n", t, E / (t * 1e-6) / 1e9);
+    t = time_us(reps, [&] {
+        hipLaunchKernelGGL(mb_gather, dim3(g4), dim3(256), 0, 0, (const int4 *)d_col, d_w, 0xFFFFu, d_out, n4);
+    });
+    printf("mb_gather w&0xFFFF (256KB) %8.2f us  %7.1f Gelem/s\n", t, E / (t * 1e-6) / 1e9);
+    t = time_us(reps, [&] {
+        hipLaunchKernelGGL(mb_gather, dim3(g4), dim3(256), 0, 0, (const int4 *)d_col, d_w, 0x3FFu, d_out, n4);
+    });
+    printf("mb_gather w&0x3FF (4KB)    %8.2f us  %7.1f Gelem/s\n", t, E / (t * 1e-6) / 1e9);
+
+    for (unsigned mask : {0xFFFFFFFFu, 0xFFFFu, 0x3FFu}) {
+        for (int G : {1, 2, 4, 8}) {
+            for (int wpc : {8, 16, 32}) {  // waves per CU
+                const unsigned grid = 256u * (unsigned)wpc / 4u;
+                auto go = [&] {
+                    if (G == 1) hipLaunchKernelGGL(mb_gather_g<1>, dim3(grid), dim3(256), 0, 0, (const int4 *)d_col, d_w, mask, d_out, n4);
+                    if (G == 2) hipLaunchKernelGGL(mb_gather_g<2>, dim3(grid), dim3(256), 0, 0, (const int4 *)d_col, d_w, mask, d_out, n4);
+                    if (G == 4) hipLaunchKernelGGL(mb_gather_g<4>, dim3(grid), dim3(256), 0, 0, (const int4 *)d_col, d_w, mask, d_out, n4);
+                    if (G == 8) hipLaunchKernelGGL(mb_gather_g<8>, dim3(grid), dim3(256), 0, 0, (const int4 *)d_col, d_w, mask, d_out, n4);
+                };
+                t = time_us(reps, go);
+                printf("mb_gather_g mask=%08x G=%d waves/CU=%2d %8.2f us  %7.1f Gelem/s\n", mask, G, wpc, t, E / (t * 1e-6) / 1e9);
+            }
+        }
+    }
+    {   // HBM-cold stream: walk 26 MB windows of a 2 GiB buffer
+        const size_t big = (size_t)2 << 30;
+        char *d_big = nullptr;
+        CK(hipMalloc(&d_big, big));
+        CK(hipMemset(d_big, 1, big));
+        const size_t win = (size_t)E * 8;
+        const int nwin = (int)(big / win);
+        int k = 0;
+        t = time_us(reps, [&] {
+            const char *p = d_big + (size_t)(k++ % nwin) * win;
+            hipLaunchKernelGGL(mb_stream, dim3(g4), dim3(256), 0, 0, (const int4 *)p, (const float4 *)(p + win / 2), d_out, n4 / 2);
+        });
+        printf("mb_stream cold 26MB windows %8.2f us  %7.1f GB/s\n", t, rate(win + n4 * 2.0, t));
+        CK(hipFree(d_big));
+    }
+
+    // ---- K2
+    int bad = 0;
+    CK(hipMemcpy(d_w, w0.data(), D * 4, hipMemcpyHostToDevice));
+    for (int seg : {16, 32, 64}) {
+        setenv("DLR_MARGIN_SEG", seg == 16 ? "16" : seg == 32 ? "32" : "64", 1);
+        // margin_seg caches the env var on first use: launch the template directly.
+        const dim3 blk(256);
+        auto go = [&] {
+            if (seg == 16)
+                hipLaunchKernelGGL(dlr::k_margin_residual<16>, dim3((B + 63) / 64), blk, 0, 0, bt, d_w, d_r);
+            else if (seg == 32)
+                hipLaunchKernelGGL(dlr::k_margin_residual<32>, dim3((B + 127) / 128), blk, 0, 0, bt, d_w, d_r);
+            else
+                hipLaunchKernelGGL(dlr::k_margin_residual<64>, dim3((B + 255) / 256), blk, 0, 0, bt, d_w, d_r);
+        };
+        t = time_us(reps, go);
+        printf("K2 ref SEG=%-2d               %8.2f us  %7.1f GB/s\n", seg, t, rate(mb_k2, t));
+    }
+    hipLaunchKernelGGL(dlr::k_margin_residual<16>, dim3((B + 63) / 64), dim3(256), 0, 0, bt, d_w, d_r);
+    const unsigned gB = (unsigned)((B + 255) / 256);
+    t = time_us(reps, [&] { hipLaunchKernelGGL(k2_lpr<8>, dim3(gB), dim3(256), 0, 0, bt, d_w, d_r2); });
+    printf("K2 lane-per-row U=8        %8.2f us  %7.1f GB/s\n", t, rate(mb_k2, t));
+    bad |= cmp_bits(d_r, d_r2, B, "K2 lpr8 vs ref");
+    t = time_us(reps, [&] { hipLaunchKernelGGL(k2_lpr<16>, dim3(gB), dim3(256), 0, 0, bt, d_w, d_r2); });
+    printf("K2 lane-per-row U=16       %8.2f us  %7.1f GB/s\n", t, rate(mb_k2, t));
+    bad |= cmp_bits(d_r, d_r2, B, "K2 lpr16 vs ref");
+
+    // ---- K3 (unfused: output g, so repeated launches are idempotent)
+    const unsigned gD = (unsigned)((D + 255) / 256);
+    const float Bf = (float)B;
+    const double Bd = (double)B;
+    t = time_us(reps, [&] {
+        hipLaunchKernelGGL((dlr::k_grad<uint16_t, false>), dim3(gD), dim3(256), 0, 0, cs, d_crow, D, d_r, d_w, d_g, Bf,
+                           Bd, 0.2f, 1.0f);
+    });
+    printf("K3 ref                     %8.2f us  %7.1f GB/s\n", t, rate(mb_k3, t));
+    for (int u : {2, 4, 8}) {
+        auto go = [&] {
+            if (u == 2)
+                hipLaunchKernelGGL((k3_lpc<2, false>), dim3(gD), dim3(256), 0, 0, cs, d_crow, D, d_r, d_w, d_g2, Bf, Bd,
+                                   0.2f, 1.0f);
+            else if (u == 4)
+                hipLaunchKernelGGL((k3_lpc<4, false>), dim3(gD), dim3(256), 0, 0, cs, d_crow, D, d_r, d_w, d_g2, Bf, Bd,
+                                   0.2f, 1.0f);
+            else
+                hipLaunchKernelGGL((k3_lpc<8, false>), dim3(gD), dim3(256), 0, 0, cs, d_crow, D, d_r, d_w, d_g2, Bf, Bd,
+                                   0.2f, 1.0f);
+        };
+        t = time_us(reps, go);
+        printf("K3 lane-per-col U=%d        %8.2f us  %7.1f GB/s\n", u, t, rate(mb_k3, t));
+        bad |= cmp_bits(d_g, d_g2, D, "K3 lpc vs ref");
+    }
+    for (int R : {32768, 36864}) {
+        const int64_t ngroups = (D + 63) / 64;
+        const int G = 256;
+        const int gpw = (int)((ngroups + G - 1) / G);
+        const int NGn = (gpw + 15) / 16;
+        const size_t lds = (size_t)R * 4;
+        auto go = [&](int U) {
+            if (NGn <= 4 && U == 8)
+                hipLaunchKernelGGL((k3_lds<8, 4, false>), dim3(G), dim3(1024), lds, 0, cs, d_crow, D, B, R, gpw, d_r, d_w,
+                                   d_g2, Bf, Bd, 0.2f, 1.0f);
+            else if (NGn <= 4 && U == 4)
+                hipLaunchKernelGGL((k3_lds<4, 4, false>), dim3(G), dim3(1024), lds, 0, cs, d_crow, D, B, R, gpw, d_r, d_w,
+                                   d_g2, Bf, Bd, 0.2f, 1.0f);
+            else
+                printf("NG %d unsupported\n", NGn);
+        };
+        for (int U : {4, 8}) {
+            CK(hipMemset(d_g2, 0, D * 4));
+            t = time_us(reps, [&] { go(U); });
+            printf("K3 lds R=%d U=%d NG=%d        %8.2f us  %7.1f GB/s\n", R, U, NGn, t, rate(mb_k3, t));
+            bad |= cmp_bits(d_g, d_g2, D, "K3 lds vs ref");
+        }
+    }
+    for (int kW : {256, 512}) {
+        const int R = kW == 256 ? 36864 : 32768;
+        const int64_t ngroups = (D + 63) / 64;
+        const int G = 256;
+        const int gpw = (int)((ngroups + G - 1) / G);
+        const int NGn = (gpw + 15) / 16;
+        const size_t lds = (size_t)R * 4 + 16 * kW * 4;
+        CK(hipMemset(d_g2, 0, D * 4));
+        t = time_us(reps, [&] {
+            if (kW == 256)
+                hipLaunchKernelGGL((k3_ldsw<4, 256, false>), dim3(G), dim3(1024), lds, 0, cs, d_crow, D, B, R, gpw, d_r,
+                                   d_w, d_g2, Bf, Bd, 0.2f, 1.0f);
+            else
+                hipLaunchKernelGGL((k3_ldsw<4, 512, false>), dim3(G), dim3(1024), lds, 0, cs, d_crow, D, B, R, gpw, d_r,
+                                   d_w, d_g2, Bf, Bd, 0.2f, 1.0f);
+        });
+        printf("K3 ldsw kW=%d R=%d NG=%d    %8.2f us  %7.1f GB/s\n", kW, R, NGn, t, rate(mb_k3, t));
+        bad |= cmp_bits(d_g, d_g2, D, "K3 ldsw vs ref");
+    }
+    {
+        const int64_t ngroups = (D + 63) / 64;
+        const int G = 256;
+        const int gpw = (int)((ngroups + G - 1) / G);
+        const size_t lds = (size_t)8 * 4096 * 4 + 16 * 256 * 4;
+        CK(hipMemset(d_g2, 0, D * 4));
+        t = time_us(reps, [&] {
+            hipLaunchKernelGGL((k3_pf<4, 8, false>), dim3(G), dim3(1024), lds, 0, cs, d_crow, D, B, gpw, d_r, d_w, d_g2,
+                               Bf, Bd, 0.2f, 1.0f);
+        });
+        printf("K3 pf NG=4 R=32768           %8.2f us  %7.1f GB/s\n", t, rate(mb_k3, t));
+        bad |= cmp_bits(d_g, d_g2, D, "K3 pf vs ref");
+        const size_t lds2 = (size_t)1 * 4096 * 4 + 16 * 256 * 4;
+        t = time_us(reps, [&] { hipLaunchKernelGGL((k3_pf<4, 1, false, 0>), dim3(G), dim3(1024), lds2, 0, cs, d_crow, D, (int64_t)4096, gpw, d_r, d_w, d_g2, Bf, Bd, 0.2f, 1.0f); });
+        printf("K3 pf ablate: B=4096 1 phase %8.2f us\n", t);
+        {
+            unsigned long long *d_st = nullptr;
+            CK(hipMalloc(&d_st, G * 8 * 8));
+            CK(hipMemset(d_st, 0, G * 8 * 8));
+            CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), &d_st, sizeof(d_st)));
+            for (int it = 0; it < 20; ++it)
+                hipLaunchKernelGGL((k3_pf<4, 8, false, 9>), dim3(G), dim3(1024), lds, 0, cs, d_crow, D, B, gpw, d_r, d_w, d_g2, Bf, Bd, 0.2f, 1.0f);
+            CK(hipDeviceSynchronize());
+            std::vector<unsigned long long> st(G * 8);
+            CK(hipMemcpy(st.data(), d_st, G * 8 * 8, hipMemcpyDeviceToHost));
+            unsigned long long t0 = ~0ull;
+            for (int g = 0; g < G; ++g) t0 = std::min(t0, st[g * 8]);
+            // 100 MHz ticks -> us
+            const char *nm[6] = {"start", "fill0 in", "ph0 go", "fill1 in", "ph1 go", "end"};
+            for (int k = 0; k < 6; ++k) {
+                std::vector<double> v;
+                for (int g = 0; g < G; ++g) v.push_back((st[g * 8 + k] - t0) * 0.01);
+                std::sort(v.begin(), v.end());
+                printf("  stamp %-9s min %6.2f med %6.2f p90 %6.2f max %6.2f us\n", nm[k], v[0], v[G / 2], v[G * 9 / 10], v[G - 1]);
+            }
+        }
+    }
+    printf("%s\n", bad ? "SOME CHECKS FAILED" : "all checks bitwise equal");
+    return bad;
+}
