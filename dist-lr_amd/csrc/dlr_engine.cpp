@@ -12,6 +12,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -47,7 +48,16 @@ struct TrainShard {
     int32_t *w_col = nullptr;
     float *w_val = nullptr;
     float *w_label = nullptr;
-    // per-batch column-major copy
+    // per-batch column-major copy: phase-split for the LDS gradient kernel
+    // (pcsc) when every batch qualifies, else the classic layout
+    bool pcsc = false;
+    int phases = 1;
+    int64_t pblocks = 0;          // groups * phases
+    uint32_t *pbase = nullptr;    // n_batches x (pblocks + 1)
+    uint8_t *pends = nullptr;     // n_batches x pblocks x 64
+    uint16_t *prow = nullptr;     // entries (batch-relative offsets poff)
+    float *pval = nullptr;
+    std::vector<int64_t> poff;    // entry offset of each batch (+ total)
     bool row16 = false;
     uint32_t *cptr = nullptr;   // n_batches x (D+1)
     void *crow = nullptr;
@@ -154,7 +164,8 @@ int upload(dlr_ctx *c, T **dst, const T *src, size_t n, size_t pad = 0) {
 void free_train(dlr_ctx *c) {
     TrainShard &t = c->train;
     for (void *p : {(void *)t.row_ptr, (void *)t.col, (void *)t.val, (void *)t.label, (void *)t.w_row_ptr,
-                    (void *)t.w_col, (void *)t.w_val, (void *)t.w_label, (void *)t.cptr, t.crow, (void *)t.cval})
+                    (void *)t.w_col, (void *)t.w_val, (void *)t.w_label, (void *)t.cptr, t.crow, (void *)t.cval,
+                    (void *)t.pbase, (void *)t.pends, (void *)t.prow, (void *)t.pval})
         dev_free(c, p);
     t = TrainShard();
 }
@@ -243,6 +254,111 @@ void build_csc(const dlr_dataset &ds, const std::vector<dlr::BatchSpan> &plan, i
     for (auto &x : th) x.join();
 }
 
+// Phase-split column-major copy (DevPcsc, dlr_kernels.h) of every batch.
+// Rows of batch b fall in phases of R rows; for each 64-column group and
+// phase, a block lists the entries of the group's columns whose row is in
+// the phase, column by column, in batch-row order (a stable counting sort
+// of the batch taken in row order, as lr.cc:37 visits it).  Returns false
+// (layout not applicable) if some block would exceed 255 entries.
+struct PcscBuild {
+    int P = 1;
+    int64_t R = 0, groups = 0, pblocks = 0;
+    std::vector<int64_t> size;  // padded entries per batch
+};
+
+template <typename Fn>
+void for_batches(int64_t nb, int nthreads, Fn fn) {
+    std::vector<std::thread> th;
+    std::atomic<int64_t> next{0};
+    nthreads = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, nb));
+    for (int t = 0; t < nthreads; ++t)
+        th.emplace_back([&] {
+            for (int64_t b; (b = next.fetch_add(1)) < nb;) fn(b);
+        });
+    for (auto &x : th) x.join();
+}
+
+// Counts of (column, phase) for batch sp; cnt has D*P entries.
+void pcsc_count(const dlr_dataset &ds, const dlr::BatchSpan &sp, const PcscBuild &pb, std::vector<uint32_t> &cnt) {
+    std::fill(cnt.begin(), cnt.end(), 0u);
+    const int64_t N = ds.n_rows;
+    for (int64_t i = 0; i < sp.rows; ++i) {
+        const int64_t r = (sp.first_row + i) % N;
+        const int64_t p = i / pb.R;
+        for (int64_t k = ds.row_ptr[(size_t)r]; k < ds.row_ptr[(size_t)r + 1]; ++k)
+            ++cnt[(size_t)ds.col[(size_t)k] * pb.P + (size_t)p];
+    }
+}
+
+bool pcsc_plan(const dlr_dataset &ds, const std::vector<dlr::BatchSpan> &plan, int64_t D, PcscBuild &pb,
+               int nthreads) {
+    const int64_t nb = (int64_t)plan.size();
+    pb.size.assign((size_t)nb, 0);
+    std::atomic<bool> ok{true};
+    for_batches(nb, nthreads, [&](int64_t b) {
+        if (!ok) return;
+        std::vector<uint32_t> cnt((size_t)(D * pb.P));
+        pcsc_count(ds, plan[(size_t)b], pb, cnt);
+        int64_t total = 0;
+        for (int64_t g = 0; g < pb.groups && ok; ++g)
+            for (int p = 0; p < pb.P; ++p) {
+                uint32_t blen = 0;
+                for (int64_t j = g * 64; j < std::min(D, g * 64 + 64); ++j) blen += cnt[(size_t)(j * pb.P + p)];
+                if (blen > 255) {
+                    ok = false;
+                    break;
+                }
+                total += (blen + 3) & ~3u;
+            }
+        pb.size[(size_t)b] = total;
+    });
+    return ok;
+}
+
+void pcsc_fill(const dlr_dataset &ds, const std::vector<dlr::BatchSpan> &plan, int64_t D, const PcscBuild &pb,
+               const std::vector<int64_t> &poff, std::vector<uint32_t> &base, std::vector<uint8_t> &ends,
+               std::vector<uint16_t> &row, std::vector<float> &val, int nthreads) {
+    const int64_t nb = (int64_t)plan.size();
+    const int64_t N = ds.n_rows;
+    for_batches(nb, nthreads, [&](int64_t b) {
+        const dlr::BatchSpan &sp = plan[(size_t)b];
+        std::vector<uint32_t> cnt((size_t)(D * pb.P));
+        pcsc_count(ds, sp, pb, cnt);
+        uint32_t *bs = base.data() + (size_t)b * (size_t)(pb.pblocks + 1);
+        uint8_t *en = ends.data() + (size_t)b * (size_t)pb.pblocks * 64;
+        uint16_t *rr = row.data() + poff[(size_t)b];
+        float *vv = val.data() + poff[(size_t)b];
+        // block bases, per-column end offsets, and cursors (reusing cnt)
+        uint32_t at = 0;
+        for (int64_t g = 0; g < pb.groups; ++g)
+            for (int p = 0; p < pb.P; ++p) {
+                const int64_t blk = g * pb.P + p;
+                bs[blk] = at;
+                uint32_t o = 0;
+                for (int l = 0; l < 64; ++l) {
+                    const int64_t j = g * 64 + l;
+                    if (j < D) {
+                        const uint32_t c = cnt[(size_t)(j * pb.P + p)];
+                        cnt[(size_t)(j * pb.P + p)] = at + o;  // cursor
+                        o += c;
+                    }
+                    en[blk * 64 + l] = (uint8_t)o;
+                }
+                at += (o + 3) & ~3u;
+            }
+        bs[pb.pblocks] = at;
+        for (int64_t i = 0; i < sp.rows; ++i) {
+            const int64_t r = (sp.first_row + i) % N;
+            const int64_t p = i / pb.R;
+            for (int64_t k = ds.row_ptr[(size_t)r]; k < ds.row_ptr[(size_t)r + 1]; ++k) {
+                const uint32_t pos = cnt[(size_t)ds.col[(size_t)k] * pb.P + (size_t)p]++;
+                rr[pos] = (uint16_t)(i - p * pb.R);
+                vv[pos] = ds.val[(size_t)k];
+            }
+        }
+    });
+}
+
 dlr::DevBatch batch_view(const dlr_ctx *c, int64_t b) {
     const TrainShard &t = c->train;
     const dlr::BatchSpan &sp = t.plan[(size_t)b];
@@ -251,11 +367,23 @@ dlr::DevBatch batch_view(const dlr_ctx *c, int64_t b) {
     return {t.row_ptr + sp.first_row, t.col, t.val, t.label + sp.first_row, sp.rows, nnz};
 }
 
+dlr::DevPcsc pcsc_view(const dlr_ctx *c, int64_t b) {
+    const TrainShard &t = c->train;
+    return {t.pbase + (size_t)b * (size_t)(t.pblocks + 1), t.pends + (size_t)b * (size_t)t.pblocks * 64,
+            t.prow + t.poff[(size_t)b], t.pval + t.poff[(size_t)b], t.phases};
+}
+
 dlr::DevCsc csc_view(const dlr_ctx *c, int64_t b) {
     const TrainShard &t = c->train;
     const size_t esz = t.row16 ? 2 : 4;
     return {t.cptr + (size_t)b * (size_t)(c->D + 1), (const char *)t.crow + esz * (size_t)t.coff[(size_t)b],
             t.cval + t.coff[(size_t)b], t.row16};
+}
+
+hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float lr, float C, bool fused) {
+    const TrainShard &t = c->train;
+    if (t.pcsc) return dlr::launch_grad_lds(pcsc_view(c, b), c->D, B, c->resid, c->w, gout, lr, C, fused, c->stream);
+    return dlr::launch_grad(csc_view(c, b), c->D, c->resid, c->w, gout, B, lr, C, fused, c->stream);
 }
 
 }  // namespace
@@ -415,32 +543,70 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         if ((rc = upload(c, &t.w_label, ll.data(), ll.size()))) return rc;
         break;  // NextBatch wraps at most once per epoch
     }
-    // Column-major copy of every batch.
-    t.row16 = t.B <= 65536;
-    const int64_t total = t.coff[(size_t)nb];
-    std::vector<uint32_t> cptr((size_t)nb * (size_t)(D + 1));
-    std::vector<float> cval((size_t)total);
+    // Column-major copy of every batch: phase-split (LDS gradient kernel)
+    // when the batch is small enough for LDS-resident residuals and every
+    // phase block fits one window; else the classic layout.
+    // DLR_GRAD_KERNEL=classic|lds forces a choice (lds still needs to fit).
     const int nthreads = dlr::default_threads();
-    if (t.row16) {
-        std::vector<uint16_t> crow((size_t)total);
-        build_csc(*ds, t.plan, D, t.coff, cptr, crow, cval, nthreads);
-        if ((rc = upload(c, (uint16_t **)&t.crow, crow.data(), crow.size(), kPad))) return rc;
-    } else {
-        std::vector<uint32_t> crow((size_t)total);
-        build_csc(*ds, t.plan, D, t.coff, cptr, crow, cval, nthreads);
-        if ((rc = upload(c, (uint32_t **)&t.crow, crow.data(), crow.size(), kPad))) return rc;
+    const char *gk = getenv("DLR_GRAD_KERNEL");
+    const bool force_classic = gk && strcmp(gk, "classic") == 0;
+    int64_t csc_bytes = 0;
+    int64_t resid_need = t.B;
+    PcscBuild pb;
+    if (!force_classic && t.B <= 65536 && D <= (int64_t)1 << 31) {
+        pb.R = (int64_t)dlr::grad_lds_fill(t.B) * 4096;
+        pb.P = (int)((t.B + pb.R - 1) / pb.R);
+        pb.groups = (D + 63) / 64;
+        pb.pblocks = pb.groups * pb.P;
+        t.pcsc = pb.P <= 2 && pcsc_plan(*ds, t.plan, D, pb, nthreads);
     }
-    if ((rc = upload(c, &t.cptr, cptr.data(), cptr.size()))) return rc;
-    if ((rc = upload(c, &t.cval, cval.data(), cval.size(), kPad))) return rc;
-    // Residual buffer.
-    if (c->resid_cap < t.B) {
+    if (gk && strcmp(gk, "lds") == 0 && !t.pcsc)
+        return fail(c, DLR_E_ARG, "dlr_load_train: DLR_GRAD_KERNEL=lds but the batches do not fit the LDS layout");
+    if (t.pcsc) {
+        t.phases = pb.P;
+        t.pblocks = pb.pblocks;
+        t.poff.assign((size_t)nb + 1, 0);
+        for (int64_t b = 0; b < nb; ++b) t.poff[(size_t)b + 1] = t.poff[(size_t)b] + pb.size[(size_t)b];
+        const int64_t total = t.poff[(size_t)nb];
+        std::vector<uint32_t> base((size_t)nb * (size_t)(pb.pblocks + 1));
+        std::vector<uint8_t> ends((size_t)nb * (size_t)pb.pblocks * 64);
+        std::vector<uint16_t> prow((size_t)total, 0);
+        std::vector<float> pval((size_t)total, 0.0f);
+        pcsc_fill(*ds, t.plan, D, pb, t.poff, base, ends, prow, pval, nthreads);
+        if ((rc = upload(c, &t.pbase, base.data(), base.size()))) return rc;
+        if ((rc = upload(c, &t.pends, ends.data(), ends.size()))) return rc;
+        if ((rc = upload(c, &t.prow, prow.data(), prow.size(), 256))) return rc;
+        if ((rc = upload(c, &t.pval, pval.data(), pval.size(), 256))) return rc;
+        csc_bytes = (int64_t)(base.size() * 4 + ends.size() + (total + 256) * 6);
+        resid_need = (int64_t)pb.P * pb.R;  // the fills read whole phases
+    } else {
+        t.row16 = t.B <= 65536;
+        const int64_t total = t.coff[(size_t)nb];
+        std::vector<uint32_t> cptr((size_t)nb * (size_t)(D + 1));
+        std::vector<float> cval((size_t)total);
+        if (t.row16) {
+            std::vector<uint16_t> crow((size_t)total);
+            build_csc(*ds, t.plan, D, t.coff, cptr, crow, cval, nthreads);
+            if ((rc = upload(c, (uint16_t **)&t.crow, crow.data(), crow.size(), kPad))) return rc;
+        } else {
+            std::vector<uint32_t> crow((size_t)total);
+            build_csc(*ds, t.plan, D, t.coff, cptr, crow, cval, nthreads);
+            if ((rc = upload(c, (uint32_t **)&t.crow, crow.data(), crow.size(), kPad))) return rc;
+        }
+        if ((rc = upload(c, &t.cptr, cptr.data(), cptr.size()))) return rc;
+        if ((rc = upload(c, &t.cval, cval.data(), cval.size(), kPad))) return rc;
+        csc_bytes = (int64_t)(cptr.size() * 4 + (total + kPad) * ((t.row16 ? 2 : 4) + 4));
+    }
+    // Residual buffer (padded to whole LDS phases for the LDS kernel).
+    if (c->resid_cap < resid_need) {
         dev_free(c, c->resid);
         c->resid = nullptr;
-        if ((rc = dev_alloc(c, (void **)&c->resid, (size_t)t.B * 4))) return rc;
-        c->resid_cap = t.B;
+        if ((rc = dev_alloc(c, (void **)&c->resid, (size_t)resid_need * 4))) return rc;
+        HIPC(c, hipMemsetAsync(c->resid, 0, (size_t)resid_need * 4, c->stream));
+        HIPC(c, hipStreamSynchronize(c->stream));
+        c->resid_cap = resid_need;
     }
-    t.bytes = (int64_t)((t.n_rows + 1) * 8 + (t.nnz + kPad) * 8 + t.n_rows * 4 + cptr.size() * 4 +
-                        (total + kPad) * ((t.row16 ? 2 : 4) + 4));
+    t.bytes = (int64_t)((t.n_rows + 1) * 8 + (t.nnz + kPad) * 8 + t.n_rows * 4) + csc_bytes;
     t.loaded = true;
     if (n_batches) *n_batches = nb;
     return DLR_OK;
@@ -481,7 +647,6 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
     HIPC(c, hipSetDevice(c->device));
     const dlr::DevBatch bt = batch_view(c, b);
     if (bt.rows > c->resid_cap) return fail(c, DLR_E_STATE, "dlr_train_step: residual buffer too small");
-    const dlr::DevCsc cs = csc_view(c, b);
     hipEvent_t t_step, t0;
     time_begin(c, &t_step);
     time_begin(c, &t0);
@@ -489,11 +654,11 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
     time_end(c, 0, t0);
     if (!c->comm) {
         time_begin(c, &t0);
-        HIPC(c, dlr::launch_grad(cs, c->D, c->resid, c->w, nullptr, bt.rows, lr, C, true, c->stream));
+        HIPC(c, launch_gradient(c, b, bt.rows, nullptr, lr, C, true));
         time_end(c, 1, t0);
     } else {
         time_begin(c, &t0);
-        HIPC(c, dlr::launch_grad(cs, c->D, c->resid, c->w, c->g, bt.rows, lr, C, false, c->stream));
+        HIPC(c, launch_gradient(c, b, bt.rows, c->g, lr, C, false));
         time_end(c, 1, t0);
         time_begin(c, &t0);
         NCCLC(c, ncclAllToAll(c->g, c->recv, (size_t)c->chunk, ncclFloat32, c->comm, c->stream));
@@ -529,9 +694,8 @@ int dlr_worker_gradient(dlr_ctx *c, int64_t b, float C, float *grad_out, int64_t
         return fail(c, DLR_E_ARG, "dlr_worker_gradient: batch out of range");
     HIPC(c, hipSetDevice(c->device));
     const dlr::DevBatch bt = batch_view(c, b);
-    const dlr::DevCsc cs = csc_view(c, b);
     HIPC(c, dlr::launch_margin_residual(bt, c->w, c->resid, c->stream));
-    HIPC(c, dlr::launch_grad(cs, c->D, c->resid, c->w, c->g, bt.rows, 0.0f, C, false, c->stream));
+    HIPC(c, launch_gradient(c, b, bt.rows, c->g, 0.0f, C, false));
     HIPC(c, hipMemcpyAsync(grad_out, c->g, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     return DLR_OK;

@@ -28,12 +28,31 @@ struct DevCsc {
     bool row16;
 };
 
+// One batch column-major, PHASE-SPLIT for the LDS-resident gradient
+// kernel: rows fall in phases of R = grad_lds_fill(B)*4,096 (1 or 2 phases).
+// For 64-column group g and phase p, block (g*phases + p) holds the entries
+// of those columns whose row is in the phase, column by column, rows
+// ascending; base[blk] is its first entry (4-aligned), ends[blk*64 + l] the
+// inclusive end offset of column 64g+l within the block (block <= 255
+// entries).  row is the phase-local row (uint16).  base has
+// groups*phases+1 entries; row/val are padded by >= 256 entries.
+struct DevPcsc {
+    const uint32_t *base;
+    const uint8_t *ends;
+    const uint16_t *row;
+    const float *val;
+    int phases;
+};
+
 hipError_t launch_margin_residual(const DevBatch &bt, const float *w, float *resid, hipStream_t s);
 int predict_grid(int64_t rows);
 hipError_t launch_predict(const DevBatch &bt, const float *w, unsigned long long *correct, double *ll_part,
                           double *ll_out, hipStream_t s);
 hipError_t launch_grad(const DevCsc &cs, int64_t D, const float *resid, float *w, float *gout, int64_t B, float lr,
                        float C, bool fused, hipStream_t s);
+int grad_lds_fill(int64_t B);  // float4 fills per thread = rows per phase / 4,096
+hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float *resid, float *w, float *gout,
+                           float lr, float C, bool fused, hipStream_t s);
 hipError_t launch_merge_update(const float *recv, int W, int64_t chunk, int64_t n, float *w_own, float lr, int mode,
                                hipStream_t s);
 

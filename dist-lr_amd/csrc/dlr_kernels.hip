@@ -67,6 +67,25 @@ struct Vec4<uint16_t> {
 // Sum over this lane's segment [a, b) of fl32(table[idx[k]] * val[k]), in
 // k order.  The wave's entries are [e0, e1).  lds: kWin floats of this wave.
 // Only lanes < SEG own a segment; all 64 lanes load and gather.
+// Non-temporal 16-byte loads for once-read streams: the streamed lines do
+// not displace the gathered table (w) from L2 (tools/kbench, cold 10M-row
+// shard: margin 22.9 -> 20.8 us).
+template <typename V>
+__device__ __forceinline__ V load_stream(const V *p) {
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    static_assert(sizeof(V) == 16 || sizeof(V) == 8, "16- or 8-byte vectors");
+    V out;
+    if constexpr (sizeof(V) == 16) {
+        const u4 x = __builtin_nontemporal_load(reinterpret_cast<const u4 *>(p));
+        __builtin_memcpy(&out, &x, 16);
+    } else {
+        const u2 x = __builtin_nontemporal_load(reinterpret_cast<const u2 *>(p));
+        __builtin_memcpy(&out, &x, 8);
+    }
+    return out;
+}
+
 template <typename IdxT>
 __device__ __forceinline__ float ordered_segment_dot(int64_t e0, int64_t e1, int64_t a, int64_t b, int lane,
                                                      const IdxT *__restrict__ idx, const float *__restrict__ val,
@@ -88,8 +107,8 @@ __device__ __forceinline__ float ordered_segment_dot(int64_t e0, int64_t e1, int
             if (t * kChunk < left) {
                 const int64_t e = ws + t * kChunk + lane * kVec;
                 const int64_t ec = e < e1 ? e : ws + t * kChunk;
-                iv[t] = *reinterpret_cast<const IV *>(idx + ec);
-                v[t] = *reinterpret_cast<const float4 *>(val + ec);
+                iv[t] = load_stream(reinterpret_cast<const IV *>(idx + ec));
+                v[t] = load_stream(reinterpret_cast<const float4 *>(val + ec));
             }
         }
         // (2) every gather of the window, then the products.  Entries outside
@@ -258,6 +277,161 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad(DevCsc cs, const RowT *_
     }
 }
 
+// K3 (+K4), LDS-resident residuals (batches of <= 65,536 rows).  Gathering
+// r_i from L2 runs at ~250 G gathers/s chip-wide (tools/kbench: one L2
+// request per gathered element), so here every workgroup (1,024 threads, one
+// per CU) stages the residuals in LDS -- R = FILL*4,096 rows per phase,
+// one or two phases -- and gathers them from LDS instead.  The batch's
+// column-major copy is PHASE-SPLIT (DevPcsc): for each group of 64 columns
+// and each phase, the block of entries whose row lies in the phase, column
+// by column, rows ascending (at most 255 entries: one 256-entry window).
+// Column j's entries in phase 0 precede those in phase 1 in batch-row
+// order, so summing phase 0's run then phase 1's run IS lr.cc:37's order.
+// Every load a wave needs (both phases' windows, its weights, the first
+// fill) is issued up front; the next phase's fill is in flight while the
+// current phase computes.  Loads are unconditional with clamped addresses
+// (a load in a divergent branch makes the compiler wait at the join).
+// Diagnostic builds only (tools/kbench defines DLR_STAMPS): per-workgroup
+// s_memrealtime stamps at the kernel's phase boundaries.
+#ifdef DLR_STAMPS
+__device__ unsigned long long *g_stamp = nullptr;
+#define DLR_STAMP(slot)                                                                      \
+    do {                                                                                     \
+        if (threadIdx.x == 0) g_stamp[blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define DLR_STAMP(slot) \
+    do {                \
+    } while (0)
+#endif
+
+constexpr int kGradWaves = 16;  // waves per workgroup
+constexpr int kGradNG = 4;      // 64-column groups per wave
+constexpr int kBlk = 256;       // window = one phase block (<= 255 entries)
+
+template <int FILL, bool FUSED, bool NTW>
+__global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int64_t D, int64_t B,
+                                                                const float *__restrict__ resid,
+                                                                float *__restrict__ w, float *__restrict__ gout,
+                                                                float Bf, double Bd, float lr, float C) {
+    constexpr int R = FILL * 4096;
+    constexpr int NG = kGradNG;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float *s_r = smem;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    float *s_p = smem + R + wv * kBlk;
+    const int P = pc.phases;
+    const int64_t ng = (D + 63) / 64;
+    const int64_t gfirst = (int64_t)blockIdx.x * (kGradWaves * NG) + wv;
+    unsigned bs[NG][2], off[NG][2], cnt[NG][2];
+    float acc[NG], wj[NG];
+    ushort4 rq[NG][2];
+    float4 vq[NG][2];
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+        const int64_t g = gfirst + kGradWaves * gi;
+        const bool gv = g < ng;
+        const int64_t gc = gv ? g : ng - 1;
+        const int64_t j = g * 64 + lane;
+        const bool ok = gv && j < D;
+        wj[gi] = w[j < D ? j : D - 1];
+        acc[gi] = 0.0f;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int64_t blk = gc * P + (p < P ? p : P - 1);
+            bs[gi][p] = pc.base[blk];
+            const unsigned hi = pc.ends[blk * 64 + lane];
+            const unsigned lo = pc.ends[blk * 64 + (lane ? lane - 1 : 0)];
+            off[gi][p] = lane ? lo : 0u;
+            cnt[gi][p] = (ok && p < P) ? hi - (lane ? lo : 0u) : 0u;
+        }
+    }
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const unsigned e = bs[gi][p] + lane * 4;  // entries are padded: always in bounds
+            if (NTW) {
+                rq[gi][p] = load_stream(reinterpret_cast<const ushort4 *>(pc.row + e));
+                vq[gi][p] = load_stream(reinterpret_cast<const float4 *>(pc.val + e));
+            } else {
+                rq[gi][p] = *reinterpret_cast<const ushort4 *>(pc.row + e);
+                vq[gi][p] = *reinterpret_cast<const float4 *>(pc.val + e);
+            }
+        }
+    }
+    // Residual fills by LDS-DMA (no VGPRs): each wave-instruction copies
+    // 1 KiB -- lane l's 16 bytes land at the wave-uniform base + 16*l.
+    auto fill = [&](int64_t lo) {
+#pragma unroll
+        for (int f = 0; f < FILL; ++f) {
+            const int o = (f * kGradWaves + wv) * kWave * 4;  // floats; this wave's 1 KiB slot
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(resid + lo + o + lane * 4),
+                (__attribute__((address_space(3))) void *)(s_r + o), 16, 0, 0);
+        }
+    };
+    DLR_STAMP(0);
+    fill(0);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        if (p >= P) break;  // uniform
+        if (p > 0) {
+            __syncthreads();  // every wave is done reading the previous phase
+            DLR_STAMP(3);
+            fill((int64_t)p * R);  // resid is padded to P*R floats
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        DLR_STAMP(1 + 3 * p);
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) {
+            if (gfirst + kGradWaves * gi >= ng) break;  // wave-uniform
+            const ushort4 r4 = rq[gi][p];
+            const float4 v4 = vq[gi][p];
+            float4 q;
+            q.x = s_r[r4.x] * v4.x;
+            q.y = s_r[r4.y] * v4.y;
+            q.z = s_r[r4.z] * v4.z;
+            q.w = s_r[r4.w] * v4.w;
+            *reinterpret_cast<float4 *>(s_p + lane * 4) = q;
+            wave_sync();
+            // this lane's column: cnt products in order from off
+            const unsigned o = off[gi][p], c = cnt[gi][p];
+            float a = acc[gi];
+            for (unsigned k = 0; k < c; k += 8) {
+                float x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = s_p[min(o + k + u, (unsigned)kBlk - 1)];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (k + u < c) a = a + x[u];
+            }
+            acc[gi] = a;
+            wave_sync();
+        }
+    }
+#ifdef DLR_STAMPS
+    __syncthreads();
+    DLR_STAMP(5);
+#endif
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+        const int64_t j = (gfirst + kGradWaves * gi) * 64 + lane;
+        if (gfirst + kGradWaves * gi >= ng || j >= D) continue;
+        const float cw = C * wj[gi];
+        const float l2 = cw / Bf;
+        const float g = (float)((double)acc[gi] / Bd + (double)l2);
+        if (FUSED) {
+            const float step = lr * g;
+            w[j] = wj[gi] - step;
+        } else {
+            gout[j] = g;
+        }
+    }
+}
+
 // K4 for world > 1: this rank owns keys [kb, kb+n) ("serves" them, the
 // role of KVStoreDistServer::DataHandle, main.cc:57-84).  recv holds the W
 // ranks' pushed gradients for the owned range, rank-major.
@@ -354,6 +528,57 @@ hipError_t launch_grad(const DevCsc &cs, int64_t D, const float *resid, float *w
             hipLaunchKernelGGL((k_grad<uint32_t, false>), dim3(grid), blk, 0, s, cs, r, D, resid, w, gout, Bf, Bd,
                                lr, C);
     }
+    return hipGetLastError();
+}
+
+int grad_lds_fill(int64_t B) {
+    if (B <= 4096) return 1;
+    if (B <= 8192) return 2;
+    if (B <= 16384) return 4;
+    return 8;
+}
+
+hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float *resid, float *w, float *gout,
+                           float lr, float C, bool fused, hipStream_t s) {
+    if (D <= 0) return hipSuccess;
+    const int64_t ng = (D + 63) / 64;
+    const unsigned grid = (unsigned)((ng + kGradWaves * kGradNG - 1) / (kGradWaves * kGradNG));
+    const dim3 blk(kGradWaves * kWave);
+    const float Bf = (float)B;
+    const double Bd = (double)B;
+    const int fill = grad_lds_fill(B);
+    const size_t lds = (size_t)fill * 4096 * 4 + (size_t)kGradWaves * kBlk * 4;
+    // Non-temporal window loads measured slower here (tools/ab_bench.sh,
+    // C2: 19.4 vs 16.6 us -- this kernel is latency-bound in its prologue);
+    // DLR_GRAD_NT=1 turns them on.
+    static const bool ntw = [] {
+        const char *e = getenv("DLR_GRAD_NT");
+        return e ? atoi(e) != 0 : false;
+    }();
+#define DLR_GL(F)                                                                                                   \
+    case F:                                                                                                         \
+        if (fused && ntw)                                                                                           \
+            hipLaunchKernelGGL((k_grad_lds<F, true, true>), dim3(grid), blk, lds, s, pc, D, B, resid, w, gout, Bf,   \
+                               Bd, lr, C);                                                                          \
+        else if (fused)                                                                                             \
+            hipLaunchKernelGGL((k_grad_lds<F, true, false>), dim3(grid), blk, lds, s, pc, D, B, resid, w, gout, Bf,  \
+                               Bd, lr, C);                                                                          \
+        else if (ntw)                                                                                               \
+            hipLaunchKernelGGL((k_grad_lds<F, false, true>), dim3(grid), blk, lds, s, pc, D, B, resid, w, gout, Bf,  \
+                               Bd, lr, C);                                                                          \
+        else                                                                                                        \
+            hipLaunchKernelGGL((k_grad_lds<F, false, false>), dim3(grid), blk, lds, s, pc, D, B, resid, w, gout, Bf, \
+                               Bd, lr, C);                                                                          \
+        break;
+    switch (fill) {
+        DLR_GL(1)
+        DLR_GL(2)
+        DLR_GL(4)
+        DLR_GL(8)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef DLR_GL
     return hipGetLastError();
 }
 

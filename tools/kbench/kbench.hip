@@ -13,6 +13,7 @@
 #include <cstring>
 #include <vector>
 
+#define DLR_STAMPS 1
 #include "../../dist-lr_amd/csrc/dlr_kernels.hip"
 
 #define CK(x)                                                                                         \
@@ -94,6 +95,101 @@ __global__ __launch_bounds__(256) void mb_gather_g(const int4 *idx, const float 
 }
 
 // ---------------- K2 candidates
+// The production margin kernel with non-temporal loads of the col/val
+// stream (so the streamed lines do not evict w from L2).
+template <typename IdxT, bool NT>
+__device__ __forceinline__ float osd_nt(int64_t e0, int64_t e1, int64_t a, int64_t b, int lane,
+                                        const IdxT *__restrict__ idx, const float *__restrict__ val,
+                                        const float *__restrict__ table, float *lds) {
+    using IV = typename dlr::Vec4<IdxT>::type;
+    constexpr int kWin = 1024, kVec = 4, kWave = 64;
+    constexpr int kT = kWin / (kVec * kWave);
+    constexpr int kChunk = kVec * kWave;
+    const int64_t base = e0 & ~int64_t(kVec - 1);
+    float acc = 0.0f;
+    for (int64_t ws = base; ws < e1; ws += kWin) {
+        const int64_t left = e1 - ws;
+        IV iv[kT];
+        float4 v[kT];
+#pragma unroll
+        for (int t = 0; t < kT; ++t) {
+            if (t * kChunk < left) {
+                const int64_t e = ws + t * kChunk + lane * kVec;
+                const int64_t ec = e < e1 ? e : ws + t * kChunk;
+                if (NT) {
+                    typedef int vi4 __attribute__((ext_vector_type(4)));
+                    typedef float vf4 __attribute__((ext_vector_type(4)));
+                    const vi4 a4 = __builtin_nontemporal_load(reinterpret_cast<const vi4 *>(idx + ec));
+                    const vf4 b4 = __builtin_nontemporal_load(reinterpret_cast<const vf4 *>(val + ec));
+                    iv[t].x = a4.x; iv[t].y = a4.y; iv[t].z = a4.z; iv[t].w = a4.w;
+                    v[t].x = b4.x; v[t].y = b4.y; v[t].z = b4.z; v[t].w = b4.w;
+                } else {
+                    iv[t] = *reinterpret_cast<const IV *>(idx + ec);
+                    v[t] = *reinterpret_cast<const float4 *>(val + ec);
+                }
+            }
+        }
+        float g[kT][kVec];
+#pragma unroll
+        for (int t = 0; t < kT; ++t) {
+            if (t * kChunk < left) {
+                const int64_t e = ws + t * kChunk + lane * kVec;
+                const unsigned i0 = (e >= e0 && e < e1) ? (unsigned)iv[t].x : 0u;
+                const unsigned i1 = (e + 1 >= e0 && e + 1 < e1) ? (unsigned)iv[t].y : 0u;
+                const unsigned i2 = (e + 2 >= e0 && e + 2 < e1) ? (unsigned)iv[t].z : 0u;
+                const unsigned i3 = (e + 3 >= e0 && e + 3 < e1) ? (unsigned)iv[t].w : 0u;
+                g[t][0] = table[i0];
+                g[t][1] = table[i1];
+                g[t][2] = table[i2];
+                g[t][3] = table[i3];
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < kT; ++t) {
+            if (t * kChunk < left) {
+                const int o = t * kChunk + lane * kVec;
+                const int64_t e = ws + o;
+                float4 p;
+                p.x = (e >= e0 && e < e1) ? g[t][0] * v[t].x : 0.0f;
+                p.y = (e + 1 >= e0 && e + 1 < e1) ? g[t][1] * v[t].y : 0.0f;
+                p.z = (e + 2 >= e0 && e + 2 < e1) ? g[t][2] * v[t].z : 0.0f;
+                p.w = (e + 3 >= e0 && e + 3 < e1) ? g[t][3] * v[t].w : 0.0f;
+                *reinterpret_cast<float4 *>(lds + o) = p;
+            }
+        }
+        dlr::wave_sync();
+        const int64_t lo = a > ws ? a : ws;
+        const int64_t hi = b < ws + kWin ? b : ws + kWin;
+        int o = (int)(lo - ws);
+        const int oe = (int)(hi - ws);
+        for (; o + 8 <= oe; o += 8) {
+            const float x0 = lds[o], x1 = lds[o + 1], x2 = lds[o + 2], x3 = lds[o + 3];
+            const float x4 = lds[o + 4], x5 = lds[o + 5], x6 = lds[o + 6], x7 = lds[o + 7];
+            acc = acc + x0; acc = acc + x1; acc = acc + x2; acc = acc + x3;
+            acc = acc + x4; acc = acc + x5; acc = acc + x6; acc = acc + x7;
+        }
+        for (; o < oe; ++o) acc = acc + lds[o];
+        dlr::wave_sync();
+    }
+    return acc;
+}
+template <int SEG, bool NT>
+__global__ __launch_bounds__(256) void k2_nt(dlr::DevBatch bt, const float *__restrict__ w, float *__restrict__ resid) {
+    __shared__ float s_p[4][1024];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x / 64;
+    const int64_t row0 = ((int64_t)blockIdx.x * 4 + wv) * SEG;
+    if (row0 >= bt.rows) return;
+    const int64_t my = row0 + lane;
+    const bool valid = lane < SEG && my < bt.rows;
+    const float y = valid ? bt.label[my] : 0.0f;
+    const int64_t rlast = min(row0 + SEG, bt.rows);
+    const int64_t e0 = bt.row_ptr[row0], e1 = bt.row_ptr[rlast];
+    const int64_t a = valid ? bt.row_ptr[my] : e1, b = valid ? bt.row_ptr[my + 1] : e1;
+    const float z = osd_nt<int32_t, NT>(e0, e1, a, b, lane, bt.col, bt.val, w, s_p[wv]);
+    if (valid) resid[my] = sig(z) - y;
+}
+
 // Lane per row, entries read straight from the row (4 at a time), U in flight.
 template <int U>
 __global__ __launch_bounds__(256) void k2_lpr(dlr::DevBatch bt, const float *__restrict__ w,
@@ -248,11 +344,11 @@ __global__ __launch_bounds__(1024) void k3_lds(dlr::DevCsc cs, const uint16_t *_
 // phase stopped, until the sentinel (rows ascend within a column, so the
 // in-phase entries are contiguous).
 constexpr unsigned kSentinel = 0x7FBADBADu;
-__device__ unsigned long long *g_stamp = nullptr;  // diagnostic builds only (MODE 9)
+__device__ unsigned long long *g_stamp_kb = nullptr;  // diagnostic builds only (MODE 9)
 __device__ __forceinline__ void stamp(int slot) {
     if (threadIdx.x == 0) {
         unsigned long long t = __builtin_amdgcn_s_memrealtime();
-        g_stamp[blockIdx.x * 8 + slot] = t;
+        g_stamp_kb[blockIdx.x * 8 + slot] = t;
     }
 }
 template <int NG, int kW, bool FUSED>
@@ -501,6 +597,25 @@ __global__ __launch_bounds__(1024) void k3_pf(dlr::DevCsc cs, const uint16_t *__
     }
 }
 
+// Broadcast fill: every workgroup (1024 threads) copies the same R-float
+// table into its LDS (FILL float4 per thread), then one lane writes a value.
+template <int FILL>
+__global__ __launch_bounds__(1024) void mb_fill(const float *__restrict__ tab, float *out) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float4 fr[FILL];
+#pragma unroll
+    for (int f = 0; f < FILL; ++f) fr[f] = *reinterpret_cast<const float4 *>(tab + (f * 1024 + threadIdx.x) * 4);
+#pragma unroll
+    for (int f = 0; f < FILL; ++f) *reinterpret_cast<float4 *>(smem + (f * 1024 + threadIdx.x) * 4) = fr[f];
+    __syncthreads();
+    if (threadIdx.x == 0) out[blockIdx.x] = smem[(blockIdx.x * 977) % (FILL * 4096)];
+}
+// Writes a fresh table (as the margin kernel writes the residuals).
+__global__ __launch_bounds__(256) void mb_write(float *tab, int n, float v) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) tab[i] = v + (float)i;
+}
+
 }  // namespace kb
 
 using namespace kb;
@@ -547,7 +662,30 @@ int main(int argc, char **argv) {
     const int64_t D = argc > 2 ? atoll(argv[2]) : 1000000;
     const int nnz = argc > 3 ? atoi(argv[3]) : 50;
     const int reps = argc > 4 ? atoi(argv[4]) : 200;
-    printf("kbench: B=%lld D=%lld nnz=%d reps=%d\n", (long long)B, (long long)D, nnz, reps);
+    const bool calib = argc > 5 && strcmp(argv[5], "calib") == 0;
+    printf("kbench: B=%lld D=%lld nnz=%d reps=%d%s\n", (long long)B, (long long)D, nnz, reps, calib ? " (calib)" : "");
+    if (calib) {
+        // PMC calibration: a cold 16-B/lane stream of known bytes (2 GiB
+        // buffer, 26 MB windows: never cache-resident) and a 4-B gather of
+        // known count from a cold 256 MiB table.
+        const size_t big = (size_t)2 << 30;
+        char *d_big = nullptr;
+        float *d_o = nullptr;
+        CK(hipMalloc(&d_big, big));
+        CK(hipMemset(d_big, 0, big));
+        CK(hipMalloc(&d_o, 64 << 20));
+        const size_t win = (size_t)26214400;  // 25 MiB window: idx half + val half
+        const int64_t n4 = (int64_t)(win / 2 / 16);
+        const int nwin = (int)(big / win);
+        for (int k = 0; k < reps; ++k) {
+            const char *q = d_big + (size_t)(k % nwin) * win;
+            hipLaunchKernelGGL(kb::mb_stream, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, 0, (const int4 *)q,
+                               (const float4 *)(q + win / 2), d_o, n4);
+        }
+        CK(hipDeviceSynchronize());
+        printf("calib mb_stream: %d launches, each reads %zu B and writes %lld B\n", reps, win, (long long)(n4 * 4));
+        return 0;
+    }
 
     // ---- host data: distinct sorted uniform columns, 4-decimal values
     Rng rng{10};
@@ -666,6 +804,25 @@ int main(int argc, char **argv) {
         CK(hipFree(d_big));
     }
 
+    {
+        float *tab = nullptr;
+        CK(hipMalloc(&tab, 65536 * 4));
+        CK(hipMemset(tab, 0, 65536 * 4));
+        for (int G : {256, 512, 1024}) {
+            t = time_us(reps, [&] { hipLaunchKernelGGL(mb_fill<8>, dim3(G), dim3(1024), 131072, 0, tab, d_out); });
+            printf("mb_fill 128KB x %4d WG (static)      %8.2f us\n", G, t);
+            t = time_us(reps, [&] {
+                hipLaunchKernelGGL(mb_write, dim3(128), dim3(256), 0, 0, tab, 32768, 1.0f);
+                hipLaunchKernelGGL(mb_fill<8>, dim3(G), dim3(1024), 131072, 0, tab, d_out);
+            });
+            printf("mb_write+mb_fill 128KB x %4d WG      %8.2f us\n", G, t);
+            t = time_us(reps, [&] { hipLaunchKernelGGL(mb_fill<2>, dim3(G), dim3(1024), 32768, 0, tab, d_out); });
+            printf("mb_fill 32KB x %4d WG (static)       %8.2f us\n", G, t);
+        }
+        t = time_us(reps, [&] { hipLaunchKernelGGL(mb_write, dim3(128), dim3(256), 0, 0, tab, 32768, 1.0f); });
+        printf("mb_write alone                        %8.2f us\n", t);
+    }
+
     // ---- K2
     int bad = 0;
     CK(hipMemcpy(d_w, w0.data(), D * 4, hipMemcpyHostToDevice));
@@ -685,6 +842,40 @@ int main(int argc, char **argv) {
         printf("K2 ref SEG=%-2d               %8.2f us  %7.1f GB/s\n", seg, t, rate(mb_k2, t));
     }
     hipLaunchKernelGGL(dlr::k_margin_residual<16>, dim3((B + 63) / 64), dim3(256), 0, 0, bt, d_w, d_r);
+    {   // margin over a cold 10M-row shard (HBM-resident stream), plain vs nt
+        const int64_t NB = 40;  // batches in the cold shard
+        const int64_t EB = E * NB;
+        int32_t *bc = nullptr;
+        float *bv = nullptr;
+        int64_t *brp = nullptr;
+        CK(hipMalloc(&bc, (EB + 1024) * 4));
+        CK(hipMalloc(&bv, (EB + 1024) * 4));
+        CK(hipMalloc(&brp, (B * NB + 1) * 8));
+        for (int64_t q = 0; q < NB; ++q) {
+            CK(hipMemcpy(bc + q * E, col.data(), E * 4, hipMemcpyHostToDevice));
+            CK(hipMemcpy(bv + q * E, val.data(), E * 4, hipMemcpyHostToDevice));
+        }
+        std::vector<int64_t> brph(B * NB + 1);
+        for (int64_t q = 0; q < NB; ++q)
+            for (int64_t i = 0; i < B; ++i) brph[q * B + i] = q * E + rp[i];
+        brph[B * NB] = EB;
+        CK(hipMemcpy(brp, brph.data(), brph.size() * 8, hipMemcpyHostToDevice));
+        for (int nt = 0; nt < 2; ++nt) {
+            int q = 0;
+            t = time_us(reps, [&] {
+                const dlr::DevBatch bq{brp + (q % NB) * B, bc, bv, d_lab, B, E};
+                ++q;
+                if (nt)
+                    hipLaunchKernelGGL((k2_nt<16, true>), dim3((B + 63) / 64), dim3(256), 0, 0, bq, d_w, d_r2);
+                else
+                    hipLaunchKernelGGL((k2_nt<16, false>), dim3((B + 63) / 64), dim3(256), 0, 0, bq, d_w, d_r2);
+            });
+            printf("K2 cold-shard SEG=16 %s       %8.2f us  %7.1f GB/s\n", nt ? "nt   " : "plain", t, rate(mb_k2, t));
+        }
+        CK(hipFree(bc));
+        CK(hipFree(bv));
+        CK(hipFree(brp));
+    }
     const unsigned gB = (unsigned)((B + 255) / 256);
     t = time_us(reps, [&] { hipLaunchKernelGGL(k2_lpr<8>, dim3(gB), dim3(256), 0, 0, bt, d_w, d_r2); });
     printf("K2 lane-per-row U=8        %8.2f us  %7.1f GB/s\n", t, rate(mb_k2, t));
@@ -779,7 +970,7 @@ int main(int argc, char **argv) {
             unsigned long long *d_st = nullptr;
             CK(hipMalloc(&d_st, G * 8 * 8));
             CK(hipMemset(d_st, 0, G * 8 * 8));
-            CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), &d_st, sizeof(d_st)));
+            CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_kb), &d_st, sizeof(d_st)));
             for (int it = 0; it < 20; ++it)
                 hipLaunchKernelGGL((k3_pf<4, 8, false, 9>), dim3(G), dim3(1024), lds, 0, cs, d_crow, D, B, gpw, d_r, d_w, d_g2, Bf, Bd, 0.2f, 1.0f);
             CK(hipDeviceSynchronize());
@@ -795,6 +986,77 @@ int main(int argc, char **argv) {
                 std::sort(v.begin(), v.end());
                 printf("  stamp %-9s min %6.2f med %6.2f p90 %6.2f max %6.2f us\n", nm[k], v[0], v[G / 2], v[G * 9 / 10], v[G - 1]);
             }
+        }
+    }
+    {   // production LDS gradient kernel on a phase-split copy of the batch
+        const int fillq = dlr::grad_lds_fill(B);
+        const int64_t R = (int64_t)fillq * 4096;
+        const int P = (int)((B + R - 1) / R);
+        const int64_t ngr = (D + 63) / 64, nblk = ngr * P;
+        std::vector<uint32_t> cnt2((size_t)(D * P), 0), pbase((size_t)nblk + 1);
+        std::vector<uint8_t> pends((size_t)nblk * 64);
+        for (int64_t i = 0; i < B; ++i)
+            for (int64_t k = rp[i]; k < rp[i + 1]; ++k) ++cnt2[(size_t)col[k] * P + (size_t)(i / R)];
+        uint32_t at = 0;
+        bool fits = true;
+        for (int64_t g = 0; g < ngr; ++g)
+            for (int p = 0; p < P; ++p) {
+                const int64_t blk = g * P + p;
+                pbase[blk] = at;
+                uint32_t o = 0;
+                for (int l = 0; l < 64; ++l) {
+                    const int64_t j = g * 64 + l;
+                    if (j < D) {
+                        const uint32_t c = cnt2[(size_t)(j * P + p)];
+                        cnt2[(size_t)(j * P + p)] = at + o;
+                        o += c;
+                    }
+                    pends[blk * 64 + l] = (uint8_t)o;
+                }
+                fits = fits && o <= 255;
+                at += (o + 3) & ~3u;
+            }
+        pbase[nblk] = at;
+        std::vector<uint16_t> prow(at, 0);
+        std::vector<float> pval(at, 0.0f);
+        for (int64_t i = 0; i < B; ++i)
+            for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                const uint32_t q = cnt2[(size_t)col[k] * P + (size_t)(i / R)]++;
+                prow[q] = (uint16_t)(i % R);
+                pval[q] = val[k];
+            }
+        printf("pcsc: P=%d R=%lld entries(padded)=%u fits=%d\n", P, (long long)R, at, (int)fits);
+        uint32_t *d_pb = dup(pbase);
+        uint8_t *d_pe = dup(pends);
+        uint16_t *d_pr = dup(prow, 256);
+        float *d_pv = dup(pval, 256);
+        float *d_rp = nullptr;
+        CK(hipMalloc(&d_rp, P * R * 4));
+        CK(hipMemset(d_rp, 0, P * R * 4));
+        CK(hipMemcpy(d_rp, d_r, B * 4, hipMemcpyDeviceToDevice));
+        const dlr::DevPcsc pc{d_pb, d_pe, d_pr, d_pv, P};
+        // the stamp buffer must be set before ANY launch of the stamped kernel
+        const int G = (int)((ngr + 63) / 64);
+        unsigned long long *d_st = nullptr;
+        CK(hipMalloc(&d_st, (size_t)G * 8 * 8));
+        CK(hipMemset(d_st, 0, (size_t)G * 8 * 8));
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(dlr::g_stamp), &d_st, sizeof(d_st)));
+        CK(hipMemset(d_g2, 0, D * 4));
+        t = time_us(reps, [&] { CK(dlr::launch_grad_lds(pc, D, B, d_rp, d_w, d_g2, 0.2f, 1.0f, false, 0)); });
+        printf("K3 production lds            %8.2f us  %7.1f GB/s\n", t, rate(mb_k3, t));
+        bad |= cmp_bits(d_g, d_g2, D, "K3 production lds vs ref");
+        for (int it = 0; it < 20; ++it) CK(dlr::launch_grad_lds(pc, D, B, d_rp, d_w, d_g2, 0.2f, 1.0f, false, 0));
+        CK(hipDeviceSynchronize());
+        std::vector<unsigned long long> st((size_t)G * 8);
+        CK(hipMemcpy(st.data(), d_st, (size_t)G * 8 * 8, hipMemcpyDeviceToHost));
+        unsigned long long t0 = ~0ull;
+        for (int g = 0; g < G; ++g) t0 = std::min(t0, st[g * 8]);
+        const char *nm[6] = {"start", "ph0 go", "", "ph0 done", "ph1 go", "end"};
+        for (int k : {0, 1, 3, 4, 5}) {
+            std::vector<double> v;
+            for (int g = 0; g < G; ++g) v.push_back((st[g * 8 + k] - t0) * 0.01);
+            std::sort(v.begin(), v.end());
+            printf("  stamp %-9s min %6.2f med %6.2f p90 %6.2f max %6.2f us\n", nm[k], v[0], v[G / 2], v[G * 9 / 10], v[G - 1]);
         }
     }
     printf("%s\n", bad ? "SOME CHECKS FAILED" : "all checks bitwise equal");

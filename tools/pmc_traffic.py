@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Parse the rocprofv3 PMC passes of tools/pmc_pass.sh into HBM traffic per
+train step, calibrated on a known-byte stream.
+
+FETCH_SIZE / WRITE_SIZE are kB derived from the L2's memory-side request
+counters (MI355X_MICROARCH.md "HBM": on gfx950 FETCH_SIZE reads exactly half
+the bytes of a wide coalesced streaming read).  The calibration pass runs
+tools/kbench's mb_stream over cold 25 MiB windows (16-B loads per lane, known
+bytes), so the read factor is measured here instead of assumed; it is applied
+to the bench kernels' FETCH_SIZE.  Gathers (4-B loads, one line each) are not
+calibrated by that stream; the raw counters are reported beside the
+corrected figure.
+
+    python tools/pmc_traffic.py gpurun_out/pmc  [--out profiles/traffic.json]
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import json
+import os
+import statistics
+import sys
+from collections import defaultdict
+
+
+def per_kernel(path: str, counter: str) -> dict[str, list[float]]:
+    out: dict[str, list[float]] = defaultdict(list)
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] != counter:
+                continue
+            out[row["Kernel_Name"]].append(float(row["Counter_Value"]))
+    return out
+
+
+def pick(d: dict[str, list[float]], key: str) -> list[float]:
+    vals = []
+    for name, v in d.items():
+        if key in name:
+            vals.extend(v)
+    return vals
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("pmc_dir")
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--workload-key", default="D1000000_nnz50_B65536")
+    args = ap.parse_args()
+    d = args.pmc_dir
+    # calibration: mb_stream reads 25 MiB and writes n4*4 bytes per launch
+    win = 26214400
+    n4 = win // 2 // 16
+    cf = pick(per_kernel(os.path.join(d, "calib_FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE"), "mb_stream")
+    cw = pick(per_kernel(os.path.join(d, "calib_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE"), "mb_stream")
+    read_factor = win / (statistics.median(cf) * 1024.0)
+    write_factor = (n4 * 4) / (statistics.median(cw) * 1024.0)
+    res = {"workload_key": args.workload_key,
+           "calibration": {"kernel": "kbench mb_stream, cold 25 MiB windows, 16-B loads per lane",
+                           "read_bytes_true": win, "FETCH_SIZE_kB_median": statistics.median(cf),
+                           "read_factor": round(read_factor, 4), "write_bytes_true": n4 * 4,
+                           "WRITE_SIZE_kB_median": statistics.median(cw), "write_factor": round(write_factor, 4)},
+           "kernels": {}}
+    bf = per_kernel(os.path.join(d, "bench_FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE")
+    bw = per_kernel(os.path.join(d, "bench_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE")
+    hits = per_kernel(os.path.join(d, "bench_TCC_HIT_sum_TCC_MISS_sum", "run_counter_collection.csv"), "TCC_HIT_sum")
+    miss = per_kernel(os.path.join(d, "bench_TCC_HIT_sum_TCC_MISS_sum", "run_counter_collection.csv"), "TCC_MISS_sum")
+    total = 0.0
+    for short, key in [("margin", "k_margin_residual"), ("grad", "k_grad")]:
+        f = pick(bf, key)
+        w = pick(bw, key)
+        h = pick(hits, key)
+        m = pick(miss, key)
+        if not f:
+            continue
+        fk, wk = statistics.mean(f), statistics.mean(w) if w else 0.0
+        rd = fk * 1024.0 * read_factor
+        wr = wk * 1024.0 * write_factor
+        total += rd + wr
+        res["kernels"][short] = {
+            "dispatches": len(f), "FETCH_SIZE_kB": round(fk, 1), "WRITE_SIZE_kB": round(wk, 1),
+            "read_bytes": round(rd), "write_bytes": round(wr),
+            "l2_hit_rate": round(statistics.mean(h) / (statistics.mean(h) + statistics.mean(m)), 4) if h and m else None,
+        }
+    res["hbm_bytes_per_step"] = round(total)
+    js = json.dumps(res, indent=1)
+    print(js)
+    if args.out:
+        with open(args.out, "w") as fo:
+            fo.write(js + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
