@@ -58,6 +58,13 @@ struct TrainShard {
     uint16_t *prow = nullptr;     // entries (batch-relative offsets poff)
     float *pval = nullptr;
     std::vector<int64_t> poff;    // entry offset of each batch (+ total)
+    // touched-column layout (huge D, small batches): per batch the touched
+    // columns tcols[tcoff[b] .. +tncols[b]), segment pointers in cptr at
+    // tpoff[b] (tncols[b]+1 entries), entries at coff[b] in crow/cval
+    bool touched = false;
+    uint32_t *tcols = nullptr;
+    std::vector<int64_t> tcoff, tncols, tpoff;
+    int64_t tcap = 0;           // max touched columns of a batch (all ranks)
     bool row16 = false;
     uint32_t *cptr = nullptr;   // n_batches x (D+1)
     void *crow = nullptr;
@@ -96,6 +103,14 @@ struct dlr_ctx {
     double *h_ll = nullptr;                   // pinned
     TrainShard train;
     TestShard test;
+    // touched-layout step buffers: newv (world 1: new weights of the touched
+    // columns); sparse exchange (world > 1): send block [count|cols|g],
+    // all-gathered blocks, merged (col, new weight) per entry
+    float *newv = nullptr;
+    uint32_t *xsend = nullptr, *xrecv = nullptr, *xcols = nullptr;
+    float *xnewv = nullptr;
+    int64_t xcap = 0;
+    dlr::RankSizes rs{};
     std::vector<void *> allocs;
     // timing
     bool timing = false;
@@ -165,9 +180,17 @@ void free_train(dlr_ctx *c) {
     TrainShard &t = c->train;
     for (void *p : {(void *)t.row_ptr, (void *)t.col, (void *)t.val, (void *)t.label, (void *)t.w_row_ptr,
                     (void *)t.w_col, (void *)t.w_val, (void *)t.w_label, (void *)t.cptr, t.crow, (void *)t.cval,
-                    (void *)t.pbase, (void *)t.pends, (void *)t.prow, (void *)t.pval})
+                    (void *)t.pbase, (void *)t.pends, (void *)t.prow, (void *)t.pval, (void *)t.tcols})
         dev_free(c, p);
     t = TrainShard();
+}
+
+void free_touched_bufs(dlr_ctx *c) {
+    for (void *p : {(void *)c->newv, (void *)c->xsend, (void *)c->xrecv, (void *)c->xcols, (void *)c->xnewv})
+        dev_free(c, p);
+    c->newv = c->xnewv = nullptr;
+    c->xsend = c->xrecv = c->xcols = nullptr;
+    c->xcap = 0;
 }
 
 void free_test(dlr_ctx *c) {
@@ -210,6 +233,42 @@ void harvest(dlr_ctx *c) {
     }
     c->ev_pending.clear();
     c->ev_next = 0;
+}
+
+// Load-time collectives (all ranks call dlr_load_train together): max of
+// an int64 over ranks, and an all-gather of one float per rank.
+int coll_max_i64(dlr_ctx *c, int64_t *v) {
+    if (!c->comm) return DLR_OK;
+    int64_t *d = nullptr;
+    int rc = dev_alloc(c, (void **)&d, 16);
+    if (rc) return rc;
+    int64_t h = *v;
+    hipError_t e = hipMemcpyAsync(d, &h, 8, hipMemcpyHostToDevice, c->stream);
+    ncclResult_t r = e == hipSuccess ? ncclAllReduce(d, d, 1, ncclInt64, ncclMax, c->comm, c->stream) : ncclSuccess;
+    if (e == hipSuccess && r == ncclSuccess) e = hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dev_free(c, d);
+    if (r != ncclSuccess) return fail(c, DLR_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    if (e != hipSuccess) return fail(c, DLR_E_HIP, std::string("coll_max_i64: ") + hipGetErrorString(e));
+    *v = h;
+    return DLR_OK;
+}
+
+int coll_gather_f32(dlr_ctx *c, float v, std::vector<float> &out) {
+    const int W = c->comm ? c->world : 1;
+    out.assign((size_t)W, v);
+    if (!c->comm) return DLR_OK;
+    float *d = nullptr;
+    int rc = dev_alloc(c, (void **)&d, (size_t)(W + 1) * 4);
+    if (rc) return rc;
+    hipError_t e = hipMemcpyAsync(d + W, &v, 4, hipMemcpyHostToDevice, c->stream);
+    ncclResult_t r = e == hipSuccess ? ncclAllGather(d + W, d, 1, ncclFloat32, c->comm, c->stream) : ncclSuccess;
+    if (e == hipSuccess && r == ncclSuccess) e = hipMemcpyAsync(out.data(), d, (size_t)W * 4, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dev_free(c, d);
+    if (r != ncclSuccess) return fail(c, DLR_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+    if (e != hipSuccess) return fail(c, DLR_E_HIP, std::string("coll_gather_f32: ") + hipGetErrorString(e));
+    return DLR_OK;
 }
 
 // Builds the column-major copy of every batch: a stable counting sort by
@@ -359,6 +418,43 @@ void pcsc_fill(const dlr_dataset &ds, const std::vector<dlr::BatchSpan> &plan, i
     });
 }
 
+// Touched-column copy of one batch: the batch's entries sorted by (column,
+// batch row) -- a stable sort of the batch in row order, so each column's
+// segment lists its rows in the order lr.cc:37 visits them.
+struct TouchedBatch {
+    std::vector<uint32_t> cols, ptr;
+    std::vector<uint32_t> row;
+    std::vector<float> val;
+};
+
+void touched_batch(const dlr_dataset &ds, const dlr::BatchSpan &sp, TouchedBatch &tb) {
+    const int64_t N = ds.n_rows;
+    struct E {
+        uint32_t col, row;
+        float val;
+    };
+    std::vector<E> es;
+    for (int64_t i = 0; i < sp.rows; ++i) {
+        const int64_t r = (sp.first_row + i) % N;
+        for (int64_t k = ds.row_ptr[(size_t)r]; k < ds.row_ptr[(size_t)r + 1]; ++k)
+            es.push_back({(uint32_t)ds.col[(size_t)k], (uint32_t)i, ds.val[(size_t)k]});
+    }
+    std::stable_sort(es.begin(), es.end(), [](const E &a, const E &b) { return a.col < b.col; });
+    tb.cols.clear();
+    tb.ptr.clear();
+    tb.row.resize(es.size());
+    tb.val.resize(es.size());
+    for (size_t k = 0; k < es.size(); ++k) {
+        if (k == 0 || es[k].col != es[k - 1].col) {
+            tb.cols.push_back(es[k].col);
+            tb.ptr.push_back((uint32_t)k);
+        }
+        tb.row[k] = es[k].row;
+        tb.val[k] = es[k].val;
+    }
+    tb.ptr.push_back((uint32_t)es.size());
+}
+
 dlr::DevBatch batch_view(const dlr_ctx *c, int64_t b) {
     const TrainShard &t = c->train;
     const dlr::BatchSpan &sp = t.plan[(size_t)b];
@@ -376,8 +472,9 @@ dlr::DevPcsc pcsc_view(const dlr_ctx *c, int64_t b) {
 dlr::DevCsc csc_view(const dlr_ctx *c, int64_t b) {
     const TrainShard &t = c->train;
     const size_t esz = t.row16 ? 2 : 4;
-    return {t.cptr + (size_t)b * (size_t)(c->D + 1), (const char *)t.crow + esz * (size_t)t.coff[(size_t)b],
-            t.cval + t.coff[(size_t)b], t.row16};
+    const size_t po = t.touched ? (size_t)t.tpoff[(size_t)b] : (size_t)b * (size_t)(c->D + 1);
+    return {t.cptr + po, (const char *)t.crow + esz * (size_t)t.coff[(size_t)b], t.cval + t.coff[(size_t)b],
+            t.row16};
 }
 
 hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float lr, float C, bool fused) {
@@ -503,12 +600,24 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         // 4-entry aligned batch bases: the kernels load entries 4 at a time.
         t.coff[(size_t)b + 1] = (t.coff[(size_t)b] + e + 3) & ~int64_t(3);
     }
-    const double cptr_bytes = (double)nb * (double)(D + 1) * 4.0;
-    if (cptr_bytes > 64.0 * (1ull << 30))
-        return fail(c, DLR_E_NOMEM, "dlr_load_train: per-batch column pointers would need " +
-                                        std::to_string((long long)(cptr_bytes / (1 << 20))) +
-                                        " MiB (compacted column segments not implemented yet)");
+    // Layout: the touched-column copy when the batches touch few of the D
+    // columns (per-batch arrays over all D would dominate); decided
+    // collectively, since it also picks the exchange (sparse all-gather vs
+    // key-range all-to-all).  DLR_GRAD_KERNEL=touched forces it.
     int rc;
+    const char *gk = getenv("DLR_GRAD_KERNEL");
+    {
+        const int64_t epb = std::max<int64_t>(1, t.coff[(size_t)nb] / std::max<int64_t>(1, nb));
+        int64_t want = (gk && strcmp(gk, "touched") == 0) ? 1 : (gk ? 0 : (D > 8 * epb ? 1 : 0));
+        if ((rc = coll_max_i64(c, &want))) return rc;
+        t.touched = want != 0;
+        if (c->comm && c->world > dlr::kMaxRanks)
+            return fail(c, DLR_E_ARG, "dlr_load_train: more than 16 ranks");
+    }
+    const double cptr_bytes = (double)nb * (double)(D + 1) * 4.0;
+    if (!t.touched && cptr_bytes > 64.0 * (1ull << 30))
+        return fail(c, DLR_E_NOMEM, "dlr_load_train: per-batch column pointers would need " +
+                                        std::to_string((long long)(cptr_bytes / (1 << 20))) + " MiB");
     // Shard CSR.
     if ((rc = upload(c, &t.row_ptr, ds->row_ptr.data(), (size_t)t.n_rows + 1))) return rc;
     if ((rc = upload(c, &t.col, ds->col.data(), (size_t)t.nnz, kPad))) return rc;
@@ -548,8 +657,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
     // phase block fits one window; else the classic layout.
     // DLR_GRAD_KERNEL=classic|lds forces a choice (lds still needs to fit).
     const int nthreads = dlr::default_threads();
-    const char *gk = getenv("DLR_GRAD_KERNEL");
-    const bool force_classic = gk && strcmp(gk, "classic") == 0;
+    const bool force_classic = t.touched || (gk && strcmp(gk, "classic") == 0);
     int64_t csc_bytes = 0;
     int64_t resid_need = t.B;
     PcscBuild pb;
@@ -579,6 +687,70 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         if ((rc = upload(c, &t.pval, pval.data(), pval.size(), 256))) return rc;
         csc_bytes = (int64_t)(base.size() * 4 + ends.size() + (total + 256) * 6);
         resid_need = (int64_t)pb.P * pb.R;  // the fills read whole phases
+    } else if (t.touched) {
+        t.row16 = t.B <= 65536;
+        std::vector<TouchedBatch> tbs((size_t)nb);
+        for_batches(nb, nthreads, [&](int64_t b) { touched_batch(*ds, t.plan[(size_t)b], tbs[(size_t)b]); });
+        t.tcoff.assign((size_t)nb + 1, 0);
+        t.tpoff.assign((size_t)nb + 1, 0);
+        t.tncols.assign((size_t)nb, 0);
+        int64_t cap = 1;
+        for (int64_t b = 0; b < nb; ++b) {
+            const int64_t n = (int64_t)tbs[(size_t)b].cols.size();
+            t.tncols[(size_t)b] = n;
+            t.tcoff[(size_t)b + 1] = t.tcoff[(size_t)b] + n;
+            t.tpoff[(size_t)b + 1] = t.tpoff[(size_t)b] + n + 1;
+            cap = std::max(cap, n);
+        }
+        if ((rc = coll_max_i64(c, &cap))) return rc;
+        t.tcap = cap;
+        const int64_t total = t.coff[(size_t)nb];
+        std::vector<uint32_t> tcols((size_t)t.tcoff[(size_t)nb]), tptr((size_t)t.tpoff[(size_t)nb]);
+        std::vector<float> cval((size_t)total, 0.0f);
+        std::vector<uint32_t> crow32;
+        std::vector<uint16_t> crow16;
+        if (t.row16)
+            crow16.assign((size_t)total, 0);
+        else
+            crow32.assign((size_t)total, 0);
+        for (int64_t b = 0; b < nb; ++b) {
+            const TouchedBatch &tb = tbs[(size_t)b];
+            std::copy(tb.cols.begin(), tb.cols.end(), tcols.begin() + t.tcoff[(size_t)b]);
+            std::copy(tb.ptr.begin(), tb.ptr.end(), tptr.begin() + t.tpoff[(size_t)b]);
+            const size_t o = (size_t)t.coff[(size_t)b];
+            std::copy(tb.val.begin(), tb.val.end(), cval.begin() + o);
+            for (size_t k = 0; k < tb.row.size(); ++k) {
+                if (t.row16)
+                    crow16[o + k] = (uint16_t)tb.row[k];
+                else
+                    crow32[o + k] = tb.row[k];
+            }
+        }
+        tbs.clear();
+        if ((rc = upload(c, &t.tcols, tcols.data(), tcols.size(), 64))) return rc;
+        if ((rc = upload(c, &t.cptr, tptr.data(), tptr.size()))) return rc;
+        if (t.row16) {
+            if ((rc = upload(c, (uint16_t **)&t.crow, crow16.data(), crow16.size(), kPad))) return rc;
+        } else {
+            if ((rc = upload(c, (uint32_t **)&t.crow, crow32.data(), crow32.size(), kPad))) return rc;
+        }
+        if ((rc = upload(c, &t.cval, cval.data(), cval.size(), kPad))) return rc;
+        csc_bytes = (int64_t)(tcols.size() * 4 + tptr.size() * 4 + (total + kPad) * ((t.row16 ? 2 : 4) + 4));
+        // step buffers and every rank's batch size (L2 term of its pushes)
+        free_touched_bufs(c);
+        std::vector<float> bs;
+        if ((rc = coll_gather_f32(c, (float)t.B, bs))) return rc;
+        c->rs.W = (int)bs.size();
+        for (int r = 0; r < c->rs.W; ++r) c->rs.Bf[r] = bs[(size_t)r];
+        if ((rc = dev_alloc(c, (void **)&c->newv, (size_t)cap * 4))) return rc;
+        if (c->comm) {
+            const int64_t stride = 1 + 2 * cap;
+            if ((rc = dev_alloc(c, (void **)&c->xsend, (size_t)stride * 4))) return rc;
+            if ((rc = dev_alloc(c, (void **)&c->xrecv, (size_t)stride * 4 * c->world))) return rc;
+            if ((rc = dev_alloc(c, (void **)&c->xcols, (size_t)cap * 4 * c->world))) return rc;
+            if ((rc = dev_alloc(c, (void **)&c->xnewv, (size_t)cap * 4 * c->world))) return rc;
+        }
+        c->xcap = cap;
     } else {
         t.row16 = t.B <= 65536;
         const int64_t total = t.coff[(size_t)nb];
@@ -652,7 +824,42 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
     time_begin(c, &t0);
     HIPC(c, dlr::launch_margin_residual(bt, c->w, c->resid, c->stream));
     time_end(c, 0, t0);
-    if (!c->comm) {
+    if (c->train.touched) {
+        // touched columns (ordered gradient), then the dense L2 pass over
+        // all D, then the touched columns' new weights (dlr_kernels.hip
+        // "Touched-column layout").
+        const TrainShard &t = c->train;
+        const int64_t n = t.tncols[(size_t)b];
+        const uint32_t *cols = t.tcols + t.tcoff[(size_t)b];
+        const dlr::DevCsc cs = csc_view(c, b);
+        if (!c->comm) {
+            time_begin(c, &t0);
+            HIPC(c, dlr::launch_grad_touched(cs, cols, n, c->resid, c->w, c->newv, bt.rows, lr, C, true, c->stream));
+            time_end(c, 1, t0);
+            time_begin(c, &t0);
+            HIPC(c, dlr::launch_dense_l2(c->w, c->D, c->rs, lr, C, mode, c->stream));
+            HIPC(c, dlr::launch_scatter(c->w, cols, c->newv, n, c->stream));
+            time_end(c, 2, t0);
+        } else {
+            // sparse exchange: all-gather every rank's [count | cols | g]
+            const int64_t cap = c->xcap, stride = 1 + 2 * cap;
+            time_begin(c, &t0);
+            HIPC(c, dlr::launch_grad_touched(cs, cols, n, c->resid, c->w, (float *)(c->xsend + 1 + cap), bt.rows,
+                                             0.0f, C, false, c->stream));
+            time_end(c, 1, t0);
+            HIPC(c, hipMemsetD32Async(c->xsend, (int)n, 1, c->stream));
+            HIPC(c, hipMemcpyAsync(c->xsend + 1, cols, (size_t)n * 4, hipMemcpyDeviceToDevice, c->stream));
+            time_begin(c, &t0);
+            NCCLC(c, ncclAllGather(c->xsend, c->xrecv, (size_t)stride, ncclUint32, c->comm, c->stream));
+            time_end(c, 3, t0);
+            time_begin(c, &t0);
+            HIPC(c, dlr::launch_sparse_merge(c->xrecv, cap, stride, c->w, c->rs, lr, C, mode, c->xcols, c->xnewv,
+                                             c->stream));
+            HIPC(c, dlr::launch_dense_l2(c->w, c->D, c->rs, lr, C, mode, c->stream));
+            HIPC(c, dlr::launch_scatter(c->w, c->xcols, c->xnewv, (int64_t)c->world * cap, c->stream));
+            time_end(c, 2, t0);
+        }
+    } else if (!c->comm) {
         time_begin(c, &t0);
         HIPC(c, launch_gradient(c, b, bt.rows, nullptr, lr, C, true));
         time_end(c, 1, t0);
@@ -695,7 +902,18 @@ int dlr_worker_gradient(dlr_ctx *c, int64_t b, float C, float *grad_out, int64_t
     HIPC(c, hipSetDevice(c->device));
     const dlr::DevBatch bt = batch_view(c, b);
     HIPC(c, dlr::launch_margin_residual(bt, c->w, c->resid, c->stream));
-    HIPC(c, launch_gradient(c, b, bt.rows, c->g, 0.0f, C, false));
+    if (c->train.touched) {
+        // full pushed vector: the L2 term everywhere, the touched columns' g
+        const TrainShard &t = c->train;
+        const int64_t n = t.tncols[(size_t)b];
+        const uint32_t *cols = t.tcols + t.tcoff[(size_t)b];
+        HIPC(c, dlr::launch_grad_touched(csc_view(c, b), cols, n, c->resid, c->w, c->newv, bt.rows, 0.0f, C, false,
+                                         c->stream));
+        HIPC(c, dlr::launch_l2_fill(c->g, c->w, c->D, (float)bt.rows, C, c->stream));
+        HIPC(c, dlr::launch_scatter(c->g, cols, c->newv, n, c->stream));
+    } else {
+        HIPC(c, launch_gradient(c, b, bt.rows, c->g, 0.0f, C, false));
+    }
     HIPC(c, hipMemcpyAsync(grad_out, c->g, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     return DLR_OK;
@@ -765,6 +983,12 @@ int dlr_kernel_time(dlr_ctx *c, int which, double *total_ms, int64_t *launches) 
     if (total_ms) *total_ms = c->t_ms[which];
     if (launches) *launches = c->t_n[which];
     return DLR_OK;
+}
+
+int dlr_train_layout(dlr_ctx *c) {
+    if (!c) return DLR_E_ARG;
+    if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_layout: no training shard loaded");
+    return c->train.touched ? DLR_LAYOUT_TOUCHED : c->train.pcsc ? DLR_LAYOUT_LDS : DLR_LAYOUT_CLASSIC;
 }
 
 int dlr_memory_info(dlr_ctx *c, int64_t *train_bytes, int64_t *test_bytes) {

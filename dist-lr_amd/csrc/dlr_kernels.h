@@ -44,6 +44,14 @@ struct DevPcsc {
     int phases;
 };
 
+// Batch size of every rank (the L2 term of rank r's push is
+// fl32(C*w)/(float)B_r); at most kMaxRanks ranks.
+constexpr int kMaxRanks = 16;
+struct RankSizes {
+    float Bf[kMaxRanks];
+    int W;
+};
+
 hipError_t launch_margin_residual(const DevBatch &bt, const float *w, float *resid, hipStream_t s);
 int predict_grid(int64_t rows);
 hipError_t launch_predict(const DevBatch &bt, const float *w, unsigned long long *correct, double *ll_part,
@@ -53,6 +61,16 @@ hipError_t launch_grad(const DevCsc &cs, int64_t D, const float *resid, float *w
 int grad_lds_fill(int64_t B);  // float4 fills per thread = rows per phase / 4,096
 hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float *resid, float *w, float *gout,
                            float lr, float C, bool fused, hipStream_t s);
+// Touched-column layout (dlr_kernels.hip "Touched-column layout"): cs.ptr
+// spans the ncols touched columns cols[] of the batch.
+hipError_t launch_grad_touched(const DevCsc &cs, const uint32_t *cols, int64_t ncols, const float *resid,
+                               const float *w, float *out, int64_t B, float lr, float C, bool fused, hipStream_t s);
+hipError_t launch_dense_l2(float *w, int64_t D, const RankSizes &rs, float lr, float C, int mode, hipStream_t s);
+hipError_t launch_l2_fill(float *g, const float *w, int64_t D, float Bf, float C, hipStream_t s);
+hipError_t launch_scatter(float *w, const uint32_t *cols, const float *newv, int64_t n, hipStream_t s);
+hipError_t launch_sparse_merge(const uint32_t *lists, int64_t cap, int64_t stride, const float *w,
+                               const RankSizes &rs, float lr, float C, int mode, uint32_t *out_cols, float *out_newv,
+                               hipStream_t s);
 hipError_t launch_merge_update(const float *recv, int W, int64_t chunk, int64_t n, float *w_own, float lr, int mode,
                                hipStream_t s);
 

@@ -29,6 +29,7 @@
 // fp32) built once at load time.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 
@@ -432,6 +433,197 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     }
 }
 
+// ---------------------------------------------------------------------------
+// Touched-column layout (huge D, small batches: BASELINE C5, 2^28 features,
+// B = 1,024).  The batch's column-major copy lists only the columns the
+// batch touches (cols[s], ascending) -- a per-batch array over all D would
+// not fit.  The reference still applies the L2 term to EVERY weight every
+// step (lr.cc:40 runs j over all D; for an untouched column G_j = +0, so
+// g_j = fl32(fl32(C*w_j)/(float)B) exactly), so the step is:
+//   K3t  touched columns: ordered gradient (as k_grad), g or the new w
+//   K4d  a streaming pass over all D applying the L2-only update
+//   K4s  scatter of the touched columns' new weights (overwrites K4d's)
+// K4d reads and writes 8 bytes per weight: it is the HBM-bound kernel here.
+
+// K3t: segment s = column cols[s].  FUSED (one rank): out[s] = new w of the
+// column (w - fl32(lr*g)); else out[s] = g (this rank's pushed gradient).
+template <typename RowT, bool FUSED>
+__global__ __launch_bounds__(kWaves *kWave) void k_grad_touched(DevCsc cs, const RowT *__restrict__ crow,
+                                                                const uint32_t *__restrict__ cols, int64_t ncols,
+                                                                const float *__restrict__ resid,
+                                                                const float *__restrict__ w, float *__restrict__ out,
+                                                                float Bf, double Bd, float lr, float C) {
+    __shared__ float s_p[kWaves][kWin];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    const int64_t s0 = ((int64_t)blockIdx.x * kWaves + wv) * kWave;
+    if (s0 >= ncols) return;  // wave-uniform
+    const int64_t sg = s0 + lane;
+    const bool valid = sg < ncols;
+    const int64_t sl = min(s0 + kWave, ncols);
+    const int64_t e0 = cs.ptr[s0], e1 = cs.ptr[sl];
+    const int64_t a = valid ? (int64_t)cs.ptr[sg] : e1, b = valid ? (int64_t)cs.ptr[sg + 1] : e1;
+    const float G = ordered_segment_dot<RowT>(e0, e1, a, b, lane, crow, cs.val, resid, s_p[wv]);
+    if (!valid) return;
+    const float wj = w[cols[sg]];
+    const float cw = C * wj;
+    const float l2 = cw / Bf;
+    const float g = (float)((double)G / Bd + (double)l2);
+    if (FUSED) {
+        const float step = lr * g;
+        out[sg] = wj - step;
+    } else {
+        out[sg] = g;
+    }
+}
+
+// The server update of one weight given the W ranks' pushes g_r
+// (main.cc:57-84; modes as k_merge_update).  single: one rank, no merge
+// (w -= fl32(lr*g), main.cc:71/81 with W = 1).
+__device__ __forceinline__ float server_apply(float wj, const float *g, int W, float lr, int mode, bool single) {
+    if (single) {
+        const float step = lr * g[0];
+        return wj - step;
+    }
+    const float Wf = (float)W;
+    if (mode == 2) {
+        for (int r = 0; r < W; ++r) {
+            const float step = lr * g[r];
+            wj = wj - step;
+        }
+        return wj;
+    }
+    if (mode == 1) {
+        const float step = lr * g[W - 1];
+        return wj - step / Wf;
+    }
+    float m = 0.0f;
+    for (int r = 0; r < W; ++r) m = m + g[r];
+    const float step = lr * m;
+    return wj - step / Wf;
+}
+
+// The update of a weight no rank touched: every push is rank r's L2 term
+// l2_r = fl32(fl32(C*w)/(float)B_r) (server_apply with g_r = l2_r).
+__device__ __forceinline__ float l2_only_update(float wj, const RankSizes &rs, float lr, float C, int mode) {
+    const float cw = C * wj;
+    if (rs.W == 1) {
+        const float l2 = cw / rs.Bf[0];
+        const float step = lr * l2;
+        return wj - step;
+    }
+    const float Wf = (float)rs.W;
+    if (mode == 2) {
+        for (int r = 0; r < rs.W; ++r) {
+            const float l2 = cw / rs.Bf[r];
+            const float step = lr * l2;
+            wj = wj - step;
+        }
+        return wj;
+    }
+    if (mode == 1) {
+        const float l2 = cw / rs.Bf[rs.W - 1];
+        const float step = lr * l2;
+        return wj - step / Wf;
+    }
+    float m = 0.0f;
+    for (int r = 0; r < rs.W; ++r) m = m + cw / rs.Bf[r];
+    const float step = lr * m;
+    return wj - step / Wf;
+}
+
+// K4d: every weight gets the L2-only update of the W ranks; touched columns
+// are overwritten afterwards by K4s.  16-byte non-temporal loads and stores
+// (every byte is touched once).
+__global__ __launch_bounds__(256) void k_dense_l2(float *__restrict__ w, int64_t D, RankSizes rs, float lr,
+                                                  float C, int mode) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const int64_t n4 = D / 4;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += stride) {
+        f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(w) + q);
+        v.x = l2_only_update(v.x, rs, lr, C, mode);
+        v.y = l2_only_update(v.y, rs, lr, C, mode);
+        v.z = l2_only_update(v.z, rs, lr, C, mode);
+        v.w = l2_only_update(v.w, rs, lr, C, mode);
+        __builtin_nontemporal_store(v, reinterpret_cast<f4 *>(w) + q);
+    }
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < (D & 3)) w[n4 * 4 + t] = l2_only_update(w[n4 * 4 + t], rs, lr, C, mode);
+}
+
+// The pushed vector of an untouched column: g_j = fl32(fl32(C*w_j)/(float)B)
+// (lr.cc:40 with G_j = +0), for the parameter-server topology's full push.
+__global__ __launch_bounds__(256) void k_l2_fill(float *__restrict__ g, const float *__restrict__ w, int64_t D,
+                                                 float Bf, float C) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= D) return;
+    const float cw = C * w[j];
+    g[j] = cw / Bf;
+}
+
+// K4s: w[cols[s]] = newv[s] for s < n (cols[s] == UINT32_MAX: skip).
+__global__ __launch_bounds__(256) void k_scatter(float *__restrict__ w, const uint32_t *__restrict__ cols,
+                                                 const float *__restrict__ newv, int64_t n) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const uint32_t c = cols[s];
+    if (c != 0xFFFFFFFFu) w[c] = newv[s];
+}
+
+__device__ __forceinline__ int64_t find_col(const uint32_t *cols, int64_t n, uint32_t c) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (cols[mid] < c)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return (lo < n && cols[lo] == c) ? lo : -1;
+}
+
+// Sparse exchange merge (world > 1, touched layout).  The all-gathered
+// lists: rank r's block of `stride` words = [count | cols[cap] | g[cap]].
+// Entry (r, s) owns its column iff no lower rank touched it; the owner
+// computes the column's new weight from all W pushes (a rank that did not
+// touch it pushed the L2 term) in rank order, and writes (col, newv) for
+// K4s; non-owners write col = UINT32_MAX.
+__global__ __launch_bounds__(256) void k_sparse_merge(const uint32_t *__restrict__ lists, int64_t cap, int64_t stride,
+                                                      const float *__restrict__ w, RankSizes rs, float lr, float C,
+                                                      int mode, uint32_t *__restrict__ out_cols,
+                                                      float *__restrict__ out_newv) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int W = rs.W;
+    if (idx >= (int64_t)W * cap) return;
+    const int r = (int)(idx / cap);
+    const int64_t s = idx - (int64_t)r * cap;
+    const uint32_t *blk = lists + (int64_t)r * stride;
+    const int64_t n = blk[0];
+    if (s >= n) {
+        out_cols[idx] = 0xFFFFFFFFu;
+        return;
+    }
+    const uint32_t c = blk[1 + s];
+    for (int q = 0; q < r; ++q) {
+        const uint32_t *bq = lists + (int64_t)q * stride;
+        if (find_col(bq + 1, bq[0], c) >= 0) {
+            out_cols[idx] = 0xFFFFFFFFu;
+            return;
+        }
+    }
+    const float wj = w[c];
+    const float cw = C * wj;
+    float g[kMaxRanks];
+    for (int q = 0; q < W; ++q) {
+        const uint32_t *bq = lists + (int64_t)q * stride;
+        const int64_t k = q == r ? s : find_col(bq + 1, bq[0], c);
+        g[q] = k >= 0 ? __uint_as_float(bq[1 + cap + k]) : cw / rs.Bf[q];
+    }
+    out_cols[idx] = c;
+    out_newv[idx] = server_apply(wj, g, W, lr, mode, false);
+}
+
 // K4 for world > 1: this rank owns keys [kb, kb+n) ("serves" them, the
 // role of KVStoreDistServer::DataHandle, main.cc:57-84).  recv holds the W
 // ranks' pushed gradients for the owned range, rank-major.
@@ -579,6 +771,61 @@ hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float 
             return hipErrorInvalidValue;
     }
 #undef DLR_GL
+    return hipGetLastError();
+}
+
+hipError_t launch_grad_touched(const DevCsc &cs, const uint32_t *cols, int64_t ncols, const float *resid,
+                               const float *w, float *out, int64_t B, float lr, float C, bool fused, hipStream_t s) {
+    if (ncols <= 0) return hipSuccess;
+    const unsigned grid = grid_for(ncols, kWaves * kWave);
+    const dim3 blk(kWaves * kWave);
+    const float Bf = (float)B;
+    const double Bd = (double)B;
+#define DLR_GT(RT, F)                                                                                          \
+    hipLaunchKernelGGL((k_grad_touched<RT, F>), dim3(grid), blk, 0, s, cs, static_cast<const RT *>(cs.row), cols, \
+                       ncols, resid, w, out, Bf, Bd, lr, C)
+    if (cs.row16) {
+        if (fused)
+            DLR_GT(uint16_t, true);
+        else
+            DLR_GT(uint16_t, false);
+    } else {
+        if (fused)
+            DLR_GT(uint32_t, true);
+        else
+            DLR_GT(uint32_t, false);
+    }
+#undef DLR_GT
+    return hipGetLastError();
+}
+
+hipError_t launch_dense_l2(float *w, int64_t D, const RankSizes &rs, float lr, float C, int mode, hipStream_t s) {
+    if (D <= 0) return hipSuccess;
+    const int64_t work = std::max<int64_t>(D / 4, 4);
+    const unsigned grid = (unsigned)std::min<int64_t>((work + 255) / 256, 256 * 8);
+    hipLaunchKernelGGL(k_dense_l2, dim3(grid), dim3(256), 0, s, w, D, rs, lr, C, mode);
+    return hipGetLastError();
+}
+
+hipError_t launch_l2_fill(float *g, const float *w, int64_t D, float Bf, float C, hipStream_t s) {
+    if (D <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_l2_fill, dim3(grid_for(D, 256)), dim3(256), 0, s, g, w, D, Bf, C);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter(float *w, const uint32_t *cols, const float *newv, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scatter, dim3(grid_for(n, 256)), dim3(256), 0, s, w, cols, newv, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_sparse_merge(const uint32_t *lists, int64_t cap, int64_t stride, const float *w,
+                               const RankSizes &rs, float lr, float C, int mode, uint32_t *out_cols, float *out_newv,
+                               hipStream_t s) {
+    const int64_t n = (int64_t)rs.W * cap;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sparse_merge, dim3(grid_for(n, 256)), dim3(256), 0, s, lists, cap, stride, w, rs, lr, C,
+                       mode, out_cols, out_newv);
     return hipGetLastError();
 }
 

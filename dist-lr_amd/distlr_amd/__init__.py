@@ -22,6 +22,7 @@ MODE_SYNC_MEAN = 0
 MODE_SYNC_LAST = 1
 MODE_ASYNC = 2
 UNIQUE_ID_BYTES = 128
+LAYOUT_CLASSIC, LAYOUT_LDS, LAYOUT_TOUCHED = 0, 1, 2
 
 # Exported symbols, in include/distlr_amd.h order (tests check the .so
 # exports every one of them).
@@ -34,7 +35,7 @@ SYMBOLS = [
     "dlr_get_unique_id", "dlr_create", "dlr_destroy", "dlr_last_error",
     "dlr_set_weights", "dlr_get_weights", "dlr_load_train", "dlr_load_test",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
-    "dlr_timing", "dlr_kernel_time", "dlr_memory_info",
+    "dlr_timing", "dlr_kernel_time", "dlr_train_layout", "dlr_memory_info",
 ]
 
 if not os.path.exists(LIB_PATH):
@@ -98,6 +99,7 @@ _sig("dlr_predict", C.c_int, P, C.POINTER(i64), C.POINTER(i64), C.POINTER(C.c_do
 _sig("dlr_sync", C.c_int, P)
 _sig("dlr_timing", C.c_int, P, C.c_int)
 _sig("dlr_kernel_time", C.c_int, P, C.c_int, C.POINTER(C.c_double), C.POINTER(i64))
+_sig("dlr_train_layout", C.c_int, P)
 _sig("dlr_memory_info", C.c_int, P, C.POINTER(i64), C.POINTER(i64))
 
 
@@ -328,6 +330,12 @@ class Engine:
         ms, n = C.c_double(), i64()
         self._c(lib.dlr_kernel_time(self._h, which, C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+    def train_layout(self) -> int:
+        """LAYOUT_CLASSIC / LAYOUT_LDS / LAYOUT_TOUCHED of the loaded shard."""
+        rc = lib.dlr_train_layout(self._h)
+        self._c(min(rc, 0))
+        return rc
 
     def memory_info(self) -> Tuple[int, int]:
         a, b = i64(), i64()

@@ -194,6 +194,16 @@ int dlr_sync(dlr_ctx *ctx);
 int dlr_timing(dlr_ctx *ctx, int enable);
 int dlr_kernel_time(dlr_ctx *ctx, int which, double *total_ms, int64_t *launches);
 
+/* Column-major layout the loaded training shard uses for the gradient
+ * (chosen by dlr_load_train; DLR_GRAD_KERNEL=classic|lds|touched forces
+ * one): the LDS-resident-residual layout for batches of <= 65,536 rows,
+ * the touched-column layout when batches touch few of the D columns
+ * (huge D), else the classic layout.  Returns a DLR_LAYOUT_* value or < 0. */
+#define DLR_LAYOUT_CLASSIC 0
+#define DLR_LAYOUT_LDS 1
+#define DLR_LAYOUT_TOUCHED 2
+int dlr_train_layout(dlr_ctx *ctx);
+
 /* Device bytes resident for the loaded shards (for reporting). */
 int dlr_memory_info(dlr_ctx *ctx, int64_t *train_bytes, int64_t *test_bytes);
 
