@@ -42,28 +42,58 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# BASELINE.json configs measured here.  c2 is the default
+# (configs[1], the headline single-GPU workload); the others are run with
+# --config for their own bench lines.
+CONFIGS = {
+    "c2": dict(rows=10_000_000, features=1_000_000, nnz=50, batch=65536, value_mode=1, steps=1000, warmup=50,
+               label="C2 sparse LR"),
+    # C3: per-GPU shard of the 100M-row Criteo-shaped set (8 GPUs); one step
+    # = the full shard (B = -1, local.sh's batching), hashed Zipf fields
+    "c3": dict(rows=12_500_000, features=1 << 24, nnz=39, batch=-1, value_mode=0, steps=10, warmup=2,
+               label="C3 Criteo-shaped hashed LR", kind="hashed"),
+    "c5": dict(rows=1_024_000, features=1 << 28, nnz=10, batch=1024, value_mode=0, steps=200, warmup=10,
+               label="C5 high-dim ultra-sparse LR"),
+}
+
+
+def make_shard(args, n_rows: int, stream: int) -> "dlr.Dataset":
+    if args.kind == "hashed":
+        return dlr.Dataset.generate_hashed(n_rows, args.features, args.nnz, seed=10, stream=stream)
+    return dlr.Dataset.generate(n_rows, args.features, args.nnz, value_mode=args.value_mode, seed=10, stream=stream)
+
+
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--rows", type=int, default=10_000_000, help="training rows per GPU shard")
-    ap.add_argument("--features", type=int, default=1_000_000)
-    ap.add_argument("--nnz", type=int, default=50)
-    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--rows", type=int, default=None, help="training rows per GPU shard")
+    ap.add_argument("--features", type=int, default=None)
+    ap.add_argument("--nnz", type=int, default=None)
+    ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--lr", type=float, default=0.2)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per step (written by tools/pmc_traffic.py)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    for k in ("rows", "features", "nnz", "batch", "steps", "warmup"):
+        if getattr(args, k) is None:
+            setattr(args, k, cfg[k])
+    args.value_mode = cfg["value_mode"]
+    args.label = cfg["label"]
+    args.kind = cfg.get("kind", "uniform")
+    return args
 
 
-def alg_bytes_per_step(B: int, nnz: int, D: int) -> int:
+def alg_bytes_per_step(B: int, nnz: float, D: int) -> int:
     """8*nnz + 8 bytes per sample (int32 col + fp32 val per
     nnz; row offset + label per row) + 8*D/B per sample (dense-L2 weight
     read + write), times the B samples of one step."""
-    return B * (8 * nnz + 8) + 8 * D
+    return int(round(B * (8 * nnz + 8) + 8 * D))
 
 
 def cpu_baseline(args, D: int) -> dict:
@@ -72,12 +102,13 @@ def cpu_baseline(args, D: int) -> dict:
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # checker only: timed as the CPU baseline, never as the product
 
-    B = args.batch
-    n_rows = 4 * B
-    ds = dlr.Dataset.generate(n_rows, D, args.nnz, value_mode=1, seed=10, stream=1)
+    B = args.batch if args.batch > 0 else 200_000   # full-shard configs: a 200k-row shard, B = -1
+    n_rows = 4 * B if args.batch > 0 else B
+    ds = make_shard(args, n_rows, 1)
     rp, col, val, lab = ds.csr()
     w = dlr.init_weight(D)
-    rows = [oracle.batch_rows(n_rows, B, b) for b in range(4)]
+    bb = args.batch if args.batch > 0 else -1
+    rows = [oracle.batch_rows(n_rows, bb, b % oracle.num_batches(n_rows, bb)) for b in range(4)]
     done, t0 = 0, time.perf_counter()
     while True:
         g = oracle.grad_csr((rp, col, val), lab, rows[done % 4], w)
@@ -111,7 +142,8 @@ def main():
         uid = obj[0]
 
     t_setup = time.perf_counter()
-    ds = dlr.Dataset.generate(args.rows, D, args.nnz, value_mode=1, seed=10, stream=rank + 1)
+    ds = make_shard(args, args.rows, rank + 1)
+    nnz_avg = ds.info()[1] / max(1, args.rows)        # hashed rows lose a few duplicate fields
     t_gen = time.perf_counter() - t_setup
     eng = dlr.Engine(D, device=local, rank=rank, world=world, unique_id=uid)
     eng.set_weights(dlr.init_weight(D))
@@ -119,8 +151,9 @@ def main():
     train_bytes, _ = eng.memory_info()
     ds.free()
     t_load = time.perf_counter() - t_setup - t_gen
+    layout = {dlr.LAYOUT_CLASSIC: "classic", dlr.LAYOUT_LDS: "lds", dlr.LAYOUT_TOUCHED: "touched"}[eng.train_layout()]
     log(f"[rank {rank}] shard {args.rows} x {D}, nnz/row {args.nnz}: generated {t_gen:.1f}s, resident "
-        f"{train_bytes / 2**30:.2f} GiB in {t_load:.1f}s, {nb} batches/epoch")
+        f"{train_bytes / 2**30:.2f} GiB in {t_load:.1f}s, {nb} batches/epoch, gradient layout {layout}")
 
     def run(k0, k):
         for i in range(k0, k0 + k):
@@ -163,18 +196,19 @@ def main():
           [("margin", dlr.TIMER_MARGIN), ("grad_update", dlr.TIMER_GRAD), ("merge", dlr.TIMER_UPDATE),
            ("exchange", dlr.TIMER_EXCHANGE), ("step", dlr.TIMER_STEP)]}
     eng.timing(False)
-    samples = world * args.steps * B
+    B_eff = B if B > 0 else args.rows                 # B = -1: the full shard per step
+    samples = world * args.steps * B_eff
     value = samples / el
     avg_us = {k: (ms / n * 1000.0 if n else 0.0) for k, (ms, n) in kt.items()}
     kern_us = avg_us["margin"] + avg_us["grad_update"] + avg_us["merge"]
-    step_bytes = alg_bytes_per_step(B, args.nnz, D)
+    step_bytes = alg_bytes_per_step(B_eff, nnz_avg, D)
     achieved = step_bytes / (kern_us * 1e-6) / 1e9 if kern_us > 0 else 0.0
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("workload_key") == f"D{D}_nnz{args.nnz}_B{B}":
+            if tj.get("workload_key") == f"D{D}_nnz{args.nnz}_B{B}" and tj.get("layout", layout) == layout:
                 traffic = tj.get("hbm_bytes_per_step")
         except Exception:
             traffic = None
@@ -200,14 +234,17 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded gen_data.py-shaped sparse rows, 4-decimal values; resident in HBM)",
-            "config": {"workload": f"C2 sparse LR: {args.rows} rows/GPU x {D} features, {args.nnz} nnz/row, "
+            "data": "synthetic (seeded gen_data.py-shaped sparse rows, "
+                    f"{'4-decimal' if args.value_mode else 'binary'} values; resident in HBM)",
+            "config": {"workload": f"{args.label}: {args.rows} rows/GPU x {D} features, {args.nnz} nnz/row, "
                                    f"batch {B}, sync SGD lr {args.lr}, C=1",
+                       "name": args.config, "gradient_layout": layout,
                        "rows_per_gpu": args.rows, "num_feature_dim": D, "nnz_per_row": args.nnz,
                        "batch_size": B, "parallelism": f"dp{world}"},
             "roofline": {
                 "bound": "hbm",
-                "kernel": "train step = k_margin_residual + k_grad (+ k_merge_update when N>1)",
+                "kernel": "train step = margin (K2) + gradient (K3, + fused update) + update/merge (K4: dense L2 "
+                          "pass for the touched layout, key-range merge when N>1)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -18,6 +18,7 @@
 #include <memory>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "dlr_internal.h"
@@ -65,6 +66,13 @@ struct TrainShard {
     uint32_t *tcols = nullptr;
     std::vector<int64_t> tcoff, tncols, tpoff;
     int64_t tcap = 0;           // max touched columns of a batch (all ranks)
+    // long columns of the classic layout (per batch: lcoff cols, lsoff
+    // segments, leoff entries; cseg/sptr have one extra entry per batch)
+    bool any_long = false;
+    uint32_t *lcols = nullptr, *lcseg = nullptr, *lsptr = nullptr;
+    void *lrow = nullptr;
+    float *lval = nullptr, *lpart = nullptr;
+    std::vector<int64_t> lcoff, lsoff, leoff;
     bool row16 = false;
     uint32_t *cptr = nullptr;   // n_batches x (D+1)
     void *crow = nullptr;
@@ -180,7 +188,8 @@ void free_train(dlr_ctx *c) {
     TrainShard &t = c->train;
     for (void *p : {(void *)t.row_ptr, (void *)t.col, (void *)t.val, (void *)t.label, (void *)t.w_row_ptr,
                     (void *)t.w_col, (void *)t.w_val, (void *)t.w_label, (void *)t.cptr, t.crow, (void *)t.cval,
-                    (void *)t.pbase, (void *)t.pends, (void *)t.prow, (void *)t.pval, (void *)t.tcols})
+                    (void *)t.pbase, (void *)t.pends, (void *)t.prow, (void *)t.pval, (void *)t.tcols,
+                    (void *)t.lcols, (void *)t.lcseg, (void *)t.lsptr, t.lrow, (void *)t.lval, (void *)t.lpart})
         dev_free(c, p);
     t = TrainShard();
 }
@@ -271,42 +280,100 @@ int coll_gather_f32(dlr_ctx *c, float v, std::vector<float> &out) {
     return DLR_OK;
 }
 
+// Long columns of one batch, built beside the classic copy (see
+// dlr_kernels.hip "Long columns").
+template <typename RowT>
+struct LongBatch {
+    std::vector<uint32_t> cols, cseg, sptr;
+    std::vector<RowT> row;
+    std::vector<float> val;
+};
+
 // Builds the column-major copy of every batch: a stable counting sort by
 // column of the batch's entries taken in batch-row order, so each column's
-// segment lists its rows in the order lr.cc:37 visits them.
+// segment lists its rows in the order lr.cc:37 visits them.  Columns with
+// more than long_min entries (0: none) go to `lb` in chunks of kLongChunk
+// (4-aligned starts); their pointer entry carries kLongFlag and their
+// segment in the classic copy is empty.
 template <typename RowT>
 void build_csc(const dlr_dataset &ds, const std::vector<dlr::BatchSpan> &plan, int64_t D,
                const std::vector<int64_t> &coff, std::vector<uint32_t> &cptr, std::vector<RowT> &crow,
-               std::vector<float> &cval, int nthreads) {
+               std::vector<float> &cval, int64_t long_min, std::vector<LongBatch<RowT>> &lb, int nthreads) {
     const int64_t nb = (int64_t)plan.size();
     const int64_t N = ds.n_rows;
+    lb.assign((size_t)nb, LongBatch<RowT>());
     std::vector<std::thread> th;
     nthreads = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, nb));
     for (int t = 0; t < nthreads; ++t) {
         th.emplace_back([&, t] {
             std::vector<uint32_t> cnt((size_t)D + 1);
+            std::vector<uint8_t> is_long;
             for (int64_t b = t; b < nb; b += nthreads) {
                 const dlr::BatchSpan &sp = plan[(size_t)b];
+                LongBatch<RowT> &L = lb[(size_t)b];
                 std::fill(cnt.begin(), cnt.end(), 0u);
                 for (int64_t i = 0; i < sp.rows; ++i) {
                     const int64_t r = (sp.first_row + i) % N;
                     for (int64_t k = ds.row_ptr[(size_t)r]; k < ds.row_ptr[(size_t)r + 1]; ++k)
                         ++cnt[(size_t)ds.col[(size_t)k] + 1];
                 }
+                bool any_long = false;
+                if (long_min > 0) {
+                    is_long.assign((size_t)D, 0);
+                    for (int64_t j = 0; j < D; ++j)
+                        if ((int64_t)cnt[(size_t)j + 1] > long_min) {
+                            is_long[(size_t)j] = 1;
+                            any_long = true;
+                        }
+                }
                 uint32_t *ptr = cptr.data() + (size_t)b * (size_t)(D + 1);
                 ptr[0] = 0;
-                for (int64_t j = 0; j < D; ++j) ptr[j + 1] = ptr[j] + cnt[(size_t)j + 1];
-                std::copy(ptr, ptr + D, cnt.begin());  // cursors
+                uint32_t lat = 0;  // long-array cursor
+                for (int64_t j = 0; j < D; ++j) {
+                    const uint32_t c = cnt[(size_t)j + 1];
+                    if (any_long && is_long[(size_t)j]) {
+                        ptr[j + 1] = ptr[j];
+                        L.cols.push_back((uint32_t)j);
+                        L.cseg.push_back((uint32_t)L.sptr.size());
+                        for (uint32_t o = 0; o < c; o += dlr::kLongChunk) L.sptr.push_back(lat + o);
+                        cnt[(size_t)j + 1] = lat;  // long cursor
+                        lat += (c + 3) & ~3u;
+                    } else {
+                        ptr[j + 1] = ptr[j] + c;
+                    }
+                }
+                // every batch ends its cseg / sptr lists with one terminal
+                // entry (the per-batch offsets rely on it).  A chunk ends
+                // where the next begins: a column's last chunk also covers
+                // its <= 3 padding entries (row 0, value 0), whose products
+                // are +-0 and leave a sum unchanged.
+                L.cseg.push_back((uint32_t)L.sptr.size());
+                L.sptr.push_back(lat);
+                if (any_long) {
+                    L.row.assign((size_t)lat + 16, 0);
+                    L.val.assign((size_t)lat + 16, 0.0f);
+                }
+                // cursors: short columns in the classic copy, long ones in L
+                for (int64_t j = 0; j < D; ++j)
+                    if (!(any_long && is_long[(size_t)j])) cnt[(size_t)j + 1] = ptr[j];
                 RowT *rr = crow.data() + coff[(size_t)b];
                 float *vv = cval.data() + coff[(size_t)b];
                 for (int64_t i = 0; i < sp.rows; ++i) {
                     const int64_t r = (sp.first_row + i) % N;
                     for (int64_t k = ds.row_ptr[(size_t)r]; k < ds.row_ptr[(size_t)r + 1]; ++k) {
-                        const uint32_t pos = cnt[(size_t)ds.col[(size_t)k]]++;
-                        rr[pos] = (RowT)i;
-                        vv[pos] = ds.val[(size_t)k];
+                        const int32_t cj = ds.col[(size_t)k];
+                        const uint32_t pos = cnt[(size_t)cj + 1]++;
+                        if (any_long && is_long[(size_t)cj]) {
+                            L.row[pos] = (RowT)i;
+                            L.val[pos] = ds.val[(size_t)k];
+                        } else {
+                            rr[pos] = (RowT)i;
+                            vv[pos] = ds.val[(size_t)k];
+                        }
                     }
                 }
+                for (int64_t j = 0; j < D; ++j)
+                    if (any_long && is_long[(size_t)j]) ptr[j] |= 0x80000000u;
             }
         });
     }
@@ -480,7 +547,16 @@ dlr::DevCsc csc_view(const dlr_ctx *c, int64_t b) {
 hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float lr, float C, bool fused) {
     const TrainShard &t = c->train;
     if (t.pcsc) return dlr::launch_grad_lds(pcsc_view(c, b), c->D, B, c->resid, c->w, gout, lr, C, fused, c->stream);
-    return dlr::launch_grad(csc_view(c, b), c->D, c->resid, c->w, gout, B, lr, C, fused, c->stream);
+    hipError_t e = dlr::launch_grad(csc_view(c, b), c->D, c->resid, c->w, gout, B, lr, C, fused, c->stream);
+    if (e != hipSuccess || !t.any_long) return e;
+    const size_t bb = (size_t)b;
+    const int64_t nl = t.lcoff[bb + 1] - t.lcoff[bb];
+    if (nl == 0) return hipSuccess;
+    const size_t esz = t.row16 ? 2 : 4;
+    const dlr::DevLong lg{t.lcols + t.lcoff[bb], t.lcseg + (t.lcoff[bb] + (int64_t)b), t.lsptr + t.lsoff[bb],
+                          (const char *)t.lrow + esz * (size_t)t.leoff[bb], t.lval + t.leoff[bb], nl,
+                          t.lsoff[bb + 1] - t.lsoff[bb] - 1, t.row16};
+    return dlr::launch_grad_long(lg, B, c->resid, c->w, gout, t.lpart, lr, C, fused, c->stream);
 }
 
 }  // namespace
@@ -754,20 +830,65 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
     } else {
         t.row16 = t.B <= 65536;
         const int64_t total = t.coff[(size_t)nb];
+        if (total >= (int64_t)1 << 31) return fail(c, DLR_E_ARG, "dlr_load_train: a batch has >= 2^31 entries");
+        const char *lm = getenv("DLR_LONG_COLUMN");
+        const int64_t long_min = lm ? atoll(lm) : 4096;
         std::vector<uint32_t> cptr((size_t)nb * (size_t)(D + 1));
         std::vector<float> cval((size_t)total);
+        int64_t lbytes = 0;
+        auto finish_long = [&](auto &lb) -> int {
+            // concatenate the batches' long columns
+            using RowT = typename std::decay_t<decltype(lb[0].row)>::value_type;
+            t.lcoff.assign((size_t)nb + 1, 0);
+            t.lsoff.assign((size_t)nb + 1, 0);
+            t.leoff.assign((size_t)nb + 1, 0);
+            int64_t maxseg = 0;
+            for (int64_t b = 0; b < nb; ++b) {
+                t.lcoff[(size_t)b + 1] = t.lcoff[(size_t)b] + (int64_t)lb[(size_t)b].cols.size();
+                t.lsoff[(size_t)b + 1] = t.lsoff[(size_t)b] + (int64_t)lb[(size_t)b].sptr.size();
+                t.leoff[(size_t)b + 1] = t.leoff[(size_t)b] + (int64_t)lb[(size_t)b].row.size();
+                maxseg = std::max<int64_t>(maxseg, (int64_t)lb[(size_t)b].sptr.size());
+            }
+            t.any_long = t.lcoff[(size_t)nb] > 0;
+            if (!t.any_long) return DLR_OK;
+            std::vector<uint32_t> cols, cseg, sptr;
+            std::vector<RowT> row;
+            std::vector<float> val;
+            for (auto &L : lb) {
+                cols.insert(cols.end(), L.cols.begin(), L.cols.end());
+                cseg.insert(cseg.end(), L.cseg.begin(), L.cseg.end());
+                sptr.insert(sptr.end(), L.sptr.begin(), L.sptr.end());
+                row.insert(row.end(), L.row.begin(), L.row.end());
+                val.insert(val.end(), L.val.begin(), L.val.end());
+                L = {};
+            }
+            int r;
+            if ((r = upload(c, &t.lcols, cols.data(), cols.size()))) return r;
+            if ((r = upload(c, &t.lcseg, cseg.data(), cseg.size()))) return r;
+            if ((r = upload(c, &t.lsptr, sptr.data(), sptr.size()))) return r;
+            if ((r = upload(c, (RowT **)&t.lrow, row.data(), row.size(), 16))) return r;
+            if ((r = upload(c, &t.lval, val.data(), val.size(), 16))) return r;
+            if ((r = dev_alloc(c, (void **)&t.lpart, (size_t)maxseg * 4))) return r;
+            lbytes = (int64_t)(cols.size() * 4 + cseg.size() * 4 + sptr.size() * 4 + row.size() * sizeof(RowT) +
+                               val.size() * 4);
+            return DLR_OK;
+        };
         if (t.row16) {
             std::vector<uint16_t> crow((size_t)total);
-            build_csc(*ds, t.plan, D, t.coff, cptr, crow, cval, nthreads);
+            std::vector<LongBatch<uint16_t>> lb;
+            build_csc(*ds, t.plan, D, t.coff, cptr, crow, cval, long_min, lb, nthreads);
             if ((rc = upload(c, (uint16_t **)&t.crow, crow.data(), crow.size(), kPad))) return rc;
+            if ((rc = finish_long(lb))) return rc;
         } else {
             std::vector<uint32_t> crow((size_t)total);
-            build_csc(*ds, t.plan, D, t.coff, cptr, crow, cval, nthreads);
+            std::vector<LongBatch<uint32_t>> lb;
+            build_csc(*ds, t.plan, D, t.coff, cptr, crow, cval, long_min, lb, nthreads);
             if ((rc = upload(c, (uint32_t **)&t.crow, crow.data(), crow.size(), kPad))) return rc;
+            if ((rc = finish_long(lb))) return rc;
         }
         if ((rc = upload(c, &t.cptr, cptr.data(), cptr.size()))) return rc;
         if ((rc = upload(c, &t.cval, cval.data(), cval.size(), kPad))) return rc;
-        csc_bytes = (int64_t)(cptr.size() * 4 + (total + kPad) * ((t.row16 ? 2 : 4) + 4));
+        csc_bytes = (int64_t)(cptr.size() * 4 + (total + kPad) * ((t.row16 ? 2 : 4) + 4)) + lbytes;
     }
     // Residual buffer (padded to whole LDS phases for the LDS kernel).
     if (c->resid_cap < resid_need) {

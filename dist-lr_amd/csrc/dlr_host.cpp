@@ -547,6 +547,24 @@ void draw_columns(Rng &g, int64_t D, int k, std::vector<int32_t> &cols) {
 
 }  // namespace
 
+// Planted model w*_j ~ N(0,1), one generator per column (so it is the same
+// for every stream and thread count).
+std::vector<float> planted_model(uint64_t seed, int64_t D, int nthreads) {
+    std::vector<float> wstar((size_t)D);
+    int nt = nthreads > 0 ? nthreads : dlr::default_threads();
+    nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, D / 65536 + 1));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            for (int64_t j = D * t / nt; j < D * (t + 1) / nt; ++j) {
+                Rng g(mix64(seed * 0x9E3779B97F4A7C15ull ^ (uint64_t)j) ^ 0xA5A5A5A5ull);
+                wstar[(size_t)j] = (float)g.gauss();
+            }
+        });
+    for (auto &x : th) x.join();
+    return wstar;
+}
+
 extern "C" int dlr_dataset_generate(const dlr_gen_spec *spec, dlr_dataset **out) {
     if (!spec || !out || spec->n_rows < 0 || spec->num_feature_dim <= 0 || spec->nnz_per_row < 0 ||
         spec->num_feature_dim > INT32_MAX) {
@@ -570,11 +588,7 @@ extern "C" int dlr_dataset_generate(const dlr_gen_spec *spec, dlr_dataset **out)
     }
     for (int64_t i = 0; i <= N; ++i) ds->row_ptr[(size_t)i] = i * k;
     // Planted model w* ~ N(0,1) per column (shared by every stream of a seed).
-    std::vector<float> wstar((size_t)D);
-    for (int64_t j = 0; j < D; ++j) {
-        Rng g(mix64(spec->seed * 0x9E3779B97F4A7C15ull ^ (uint64_t)j) ^ 0xA5A5A5A5ull);
-        wstar[(size_t)j] = (float)g.gauss();
-    }
+    std::vector<float> wstar = planted_model(spec->seed, D, spec->nthreads);
     // Four-decimal values q/10000, q in [1, 10000], as ToFloat of the text.
     std::vector<float> lut(10001);
     for (int q = 1; q <= 10000; ++q) {
@@ -615,3 +629,94 @@ extern "C" int dlr_dataset_generate(const dlr_gen_spec *spec, dlr_dataset **out)
     *out = ds.release();
     return DLR_OK;
 }
+
+// Criteo-shaped hashed rows (BASELINE.json configs[2]):
+// each of `fields` categorical fields draws a value v ~ Zipf(s) over
+// [1, cardinality] (inverse CDF); the feature is splitmix64(field, v) mod D;
+// duplicates within a row collapse; columns ascending; value 1.  Labels come
+// from a planted model as in dlr_dataset_generate.
+extern "C" int dlr_dataset_generate_hashed(const dlr_hashed_spec *spec, dlr_dataset **out) {
+    if (!spec || !out || spec->n_rows < 0 || spec->num_feature_dim <= 0 || spec->num_feature_dim > INT32_MAX ||
+        spec->fields <= 0 || spec->fields > 1024 || spec->cardinality <= 0 || spec->zipf_s <= 0.0) {
+        set_error("dlr_dataset_generate_hashed: bad spec");
+        return DLR_E_ARG;
+    }
+    *out = nullptr;
+    const int64_t N = spec->n_rows, D = spec->num_feature_dim;
+    const int F = spec->fields;
+    auto ds = std::make_unique<dlr_dataset>();
+    ds->n_rows = N;
+    ds->D = D;
+    // Zipf(s) CDF over [1, cardinality]
+    std::vector<double> cdf((size_t)spec->cardinality);
+    double acc = 0.0;
+    for (int64_t v = 1; v <= spec->cardinality; ++v) {
+        acc += std::pow((double)v, -spec->zipf_s);
+        cdf[(size_t)v - 1] = acc;
+    }
+    for (double &c : cdf) c /= acc;
+    std::vector<float> wstar = planted_model(spec->seed, D, spec->nthreads);
+    const double thr = normal_quantile(1.0 - std::min(std::max(spec->positive_frac, 1e-6), 1.0 - 1e-6));
+    const uint64_t stream_key = mix64(spec->seed ^ mix64(0xC4173ull + spec->stream));
+    int nt = spec->nthreads > 0 ? spec->nthreads : dlr::default_threads();
+    nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, N / 4096 + 1));
+    // rows are generated per thread block, then concatenated
+    std::vector<std::vector<int32_t>> tcol((size_t)nt);
+    std::vector<std::vector<int64_t>> tlen((size_t)nt);
+    try {
+        ds->label.resize((size_t)N);
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t) {
+            th.emplace_back([&, t] {
+                const int64_t r0 = N * t / nt, r1 = N * (t + 1) / nt;
+                std::vector<int32_t> &cc = tcol[(size_t)t];
+                std::vector<int64_t> &ll = tlen[(size_t)t];
+                cc.reserve((size_t)((r1 - r0) * F));
+                ll.reserve((size_t)(r1 - r0));
+                std::vector<int32_t> row;
+                for (int64_t i = r0; i < r1; ++i) {
+                    Rng g(mix64(stream_key ^ (uint64_t)i * 0xD1342543DE82EF95ull));
+                    row.clear();
+                    for (int f = 0; f < F; ++f) {
+                        const double u = g.unit();
+                        const int64_t v = 1 + (int64_t)(std::lower_bound(cdf.begin(), cdf.end(), u) - cdf.begin());
+                        const uint64_t h = mix64(((uint64_t)f << 40) ^ (uint64_t)v ^ 0x51ED2701ull);
+                        row.push_back((int32_t)(h % (uint64_t)D));
+                    }
+                    std::sort(row.begin(), row.end());
+                    row.erase(std::unique(row.begin(), row.end()), row.end());
+                    double m = 0;
+                    for (int32_t c : row) m += (double)wstar[(size_t)c];
+                    bool pos = !row.empty() ? (m / std::sqrt((double)row.size())) > thr : g.unit() < spec->positive_frac;
+                    if (g.unit() < spec->label_noise) pos = !pos;
+                    ds->label[(size_t)i] = pos ? 1 : 0;
+                    cc.insert(cc.end(), row.begin(), row.end());
+                    ll.push_back((int64_t)row.size());
+                }
+            });
+        }
+        for (auto &x : th) x.join();
+        int64_t total = 0;
+        for (auto &v : tcol) total += (int64_t)v.size();
+        ds->row_ptr.resize((size_t)N + 1);
+        ds->col.resize((size_t)total);
+        ds->val.assign((size_t)total, 1.0f);
+        int64_t at = 0, i = 0;
+        ds->row_ptr[0] = 0;
+        for (int t = 0; t < nt; ++t) {
+            std::copy(tcol[(size_t)t].begin(), tcol[(size_t)t].end(), ds->col.begin() + at);
+            at += (int64_t)tcol[(size_t)t].size();
+            std::vector<int32_t>().swap(tcol[(size_t)t]);
+            for (int64_t len : tlen[(size_t)t]) {
+                ds->row_ptr[(size_t)i + 1] = ds->row_ptr[(size_t)i] + len;
+                ++i;
+            }
+        }
+    } catch (...) {
+        set_error("dlr_dataset_generate_hashed: out of host memory");
+        return DLR_E_NOMEM;
+    }
+    *out = ds.release();
+    return DLR_OK;
+}
+

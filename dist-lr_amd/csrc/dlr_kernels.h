@@ -28,6 +28,21 @@ struct DevCsc {
     bool row16;
 };
 
+// Long columns of one batch (classic layout): ncols columns cols[] (their
+// ptr entries in DevCsc carry bit 31), column l's chunks are segments
+// [cseg[l], cseg[l+1]); segment s spans entries [sptr[s], sptr[s+1]) of
+// row/val (4-aligned starts; at most kLongChunk entries).
+constexpr int kLongChunk = 512;
+struct DevLong {
+    const uint32_t *cols;
+    const uint32_t *cseg;
+    const uint32_t *sptr;
+    const void *row;
+    const float *val;
+    int64_t ncols, nseg;
+    bool row16;
+};
+
 // One batch column-major, PHASE-SPLIT for the LDS-resident gradient
 // kernel: rows fall in phases of R = grad_lds_fill(B)*4,096 (1 or 2 phases).
 // For 64-column group g and phase p, block (g*phases + p) holds the entries
@@ -58,6 +73,10 @@ hipError_t launch_predict(const DevBatch &bt, const float *w, unsigned long long
                           double *ll_out, hipStream_t s);
 hipError_t launch_grad(const DevCsc &cs, int64_t D, const float *resid, float *w, float *gout, int64_t B, float lr,
                        float C, bool fused, hipStream_t s);
+// Long columns: chunk sums (part[nseg] scratch), then the ordered combine
+// and the update (fused) / pushed gradient (gout).
+hipError_t launch_grad_long(const DevLong &lg, int64_t B, const float *resid, float *w, float *gout, float *part,
+                            float lr, float C, bool fused, hipStream_t s);
 int grad_lds_fill(int64_t B);  // float4 fills per thread = rows per phase / 4,096
 hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float *resid, float *w, float *gout,
                            float lr, float C, bool fused, hipStream_t s);

@@ -43,6 +43,8 @@ constexpr int kWave = 64;
 constexpr int kWaves = 4;      // waves per workgroup (independent)
 constexpr int kWin = 1024;     // entries per wave per window
 constexpr int kVec = 4;        // entries per lane per load
+constexpr uint32_t kLongFlag = 0x80000000u;  // DevCsc::ptr bit 31: long column
+constexpr uint32_t kPtrMask = 0x7FFFFFFFu;
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -263,10 +265,77 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad(DevCsc cs, const RowT *_
     const bool valid = j < D;
     const float wj = valid ? w[j] : 0.0f;
     const int64_t jl = min(j0 + kWave, D);
-    const int64_t e0 = cs.ptr[j0], e1 = cs.ptr[jl];
-    const int64_t a = valid ? (int64_t)cs.ptr[j] : e1, b = valid ? (int64_t)cs.ptr[j + 1] : e1;
+    // bit 31 of ptr[j] marks a LONG column: its entries live in the long
+    // arrays (k_long_segments / k_long_combine update it), its segment here
+    // is empty
+    const int64_t e0 = cs.ptr[j0] & kPtrMask, e1 = cs.ptr[jl] & kPtrMask;
+    const uint32_t pj = valid ? cs.ptr[j] : 0u;
+    const int64_t a = valid ? (int64_t)(pj & kPtrMask) : e1, b = valid ? (int64_t)(cs.ptr[j + 1] & kPtrMask) : e1;
     const float G = ordered_segment_dot<RowT>(e0, e1, a, b, lane, crow, cs.val, resid, s_p[wv]);
-    if (!valid) return;
+    if (!valid || (pj & kLongFlag)) return;
+    const float cw = C * wj;
+    const float l2 = cw / Bf;
+    const float g = (float)((double)G / Bd + (double)l2);
+    if (FUSED) {
+        const float step = lr * g;
+        w[j] = wj - step;
+    } else {
+        gout[j] = g;
+    }
+}
+
+// Long columns (classic layout, e.g. Zipf-hot features of a full-shard
+// Criteo batch, BASELINE C3): a column with more than DLR_LONG_COLUMN
+// entries (default 4,096) would be one lane's serial chain of millions of
+// adds.  Its entries are cut into chunks of kLongChunk: each chunk is summed
+// sequentially in batch-row order (lane per chunk, direct 16-byte loads),
+// then k_long_combine adds the chunk partials in chunk order.  Deterministic
+// (fixed chunking), but for these columns not the reference's single
+// sequential sum -- DLR_LONG_COLUMN=0 keeps every column bitwise.
+constexpr int kLongU = 16;  // entries in flight per lane
+
+template <typename RowT>
+__global__ __launch_bounds__(256) void k_long_segments(const uint32_t *__restrict__ sptr, int64_t nseg,
+                                                       const RowT *__restrict__ row, const float *__restrict__ val,
+                                                       const float *__restrict__ resid, float *__restrict__ part) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nseg) return;
+    const uint32_t a = sptr[s], b = sptr[s + 1];  // a is 4-aligned
+    float acc = 0.0f;
+    for (uint32_t k = a; k < b; k += kLongU) {
+        RowT r[kLongU];
+        float v[kLongU];
+#pragma unroll
+        for (int u = 0; u < kLongU; u += 4) {
+            const typename Vec4<RowT>::type r4 = *reinterpret_cast<const typename Vec4<RowT>::type *>(row + k + u);
+            const float4 v4 = *reinterpret_cast<const float4 *>(val + k + u);
+            r[u] = r4.x, r[u + 1] = r4.y, r[u + 2] = r4.z, r[u + 3] = r4.w;
+            v[u] = v4.x, v[u + 1] = v4.y, v[u + 2] = v4.z, v[u + 3] = v4.w;
+        }
+        float x[kLongU];
+#pragma unroll
+        for (int u = 0; u < kLongU; ++u) x[u] = (k + u < b) ? resid[r[u]] * v[u] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < kLongU; ++u)
+            if (k + u < b) acc = acc + x[u];
+    }
+    part[s] = acc;
+}
+
+// One long column per thread: G = chunk partials summed in chunk order,
+// then lr.cc:40 and the update (FUSED) or the pushed gradient.
+template <bool FUSED>
+__global__ __launch_bounds__(256) void k_long_combine(const uint32_t *__restrict__ cols,
+                                                      const uint32_t *__restrict__ cseg, int64_t ncols,
+                                                      const float *__restrict__ part, float *__restrict__ w,
+                                                      float *__restrict__ gout, float Bf, double Bd, float lr,
+                                                      float C) {
+    const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= ncols) return;
+    float G = 0.0f;
+    for (uint32_t s = cseg[l]; s < cseg[l + 1]; ++s) G = G + part[s];
+    const uint32_t j = cols[l];
+    const float wj = w[j];
     const float cw = C * wj;
     const float l2 = cw / Bf;
     const float g = (float)((double)G / Bd + (double)l2);
@@ -826,6 +895,26 @@ hipError_t launch_sparse_merge(const uint32_t *lists, int64_t cap, int64_t strid
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_sparse_merge, dim3(grid_for(n, 256)), dim3(256), 0, s, lists, cap, stride, w, rs, lr, C,
                        mode, out_cols, out_newv);
+    return hipGetLastError();
+}
+
+hipError_t launch_grad_long(const DevLong &lg, int64_t B, const float *resid, float *w, float *gout, float *part,
+                            float lr, float C, bool fused, hipStream_t s) {
+    if (lg.ncols <= 0) return hipSuccess;
+    if (lg.row16)
+        hipLaunchKernelGGL(k_long_segments<uint16_t>, dim3(grid_for(lg.nseg, 256)), dim3(256), 0, s, lg.sptr, lg.nseg,
+                           static_cast<const uint16_t *>(lg.row), lg.val, resid, part);
+    else
+        hipLaunchKernelGGL(k_long_segments<uint32_t>, dim3(grid_for(lg.nseg, 256)), dim3(256), 0, s, lg.sptr, lg.nseg,
+                           static_cast<const uint32_t *>(lg.row), lg.val, resid, part);
+    const float Bf = (float)B;
+    const double Bd = (double)B;
+    if (fused)
+        hipLaunchKernelGGL(k_long_combine<true>, dim3(grid_for(lg.ncols, 256)), dim3(256), 0, s, lg.cols, lg.cseg,
+                           lg.ncols, part, w, gout, Bf, Bd, lr, C);
+    else
+        hipLaunchKernelGGL(k_long_combine<false>, dim3(grid_for(lg.ncols, 256)), dim3(256), 0, s, lg.cols, lg.cseg,
+                           lg.ncols, part, w, gout, Bf, Bd, lr, C);
     return hipGetLastError();
 }
 

@@ -28,7 +28,7 @@ LAYOUT_CLASSIC, LAYOUT_LDS, LAYOUT_TOUCHED = 0, 1, 2
 # exports every one of them).
 SYMBOLS = [
     "dlr_to_int", "dlr_to_float", "dlr_split",
-    "dlr_dataset_load_libsvm", "dlr_dataset_from_csr", "dlr_dataset_generate",
+    "dlr_dataset_load_libsvm", "dlr_dataset_from_csr", "dlr_dataset_generate", "dlr_dataset_generate_hashed",
     "dlr_dataset_write_libsvm", "dlr_dataset_info", "dlr_dataset_view", "dlr_dataset_free",
     "dlr_num_batches", "dlr_batch_rows",
     "dlr_init_weight", "dlr_format_model", "dlr_key_range",
@@ -61,6 +61,21 @@ class GenSpec(C.Structure):
     ]
 
 
+class HashedSpec(C.Structure):
+    _fields_ = [
+        ("n_rows", C.c_int64),
+        ("num_feature_dim", C.c_int64),
+        ("fields", C.c_int32),
+        ("nthreads", C.c_int32),
+        ("cardinality", C.c_int64),
+        ("zipf_s", C.c_double),
+        ("seed", C.c_uint64),
+        ("stream", C.c_uint64),
+        ("positive_frac", C.c_double),
+        ("label_noise", C.c_double),
+    ]
+
+
 def _sig(name, res, *args):
     f = getattr(lib, name)
     f.restype = res
@@ -74,6 +89,7 @@ _sig("dlr_split", C.c_int, C.c_char_p, C.c_char, C.c_char_p, C.c_int)
 _sig("dlr_dataset_load_libsvm", C.c_int, C.c_char_p, i64, C.c_int, C.POINTER(P))
 _sig("dlr_dataset_from_csr", C.c_int, i64, i64, P, P, P, P, C.POINTER(P))
 _sig("dlr_dataset_generate", C.c_int, C.POINTER(GenSpec), C.POINTER(P))
+_sig("dlr_dataset_generate_hashed", C.c_int, C.POINTER(HashedSpec), C.POINTER(P))
 _sig("dlr_dataset_write_libsvm", C.c_int, P, C.c_char_p, C.c_int)
 _sig("dlr_dataset_info", C.c_int, P, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64))
 _sig("dlr_dataset_view", C.c_int, P, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P))
@@ -183,6 +199,17 @@ class Dataset:
                        label_noise, nthreads)
         h = P()
         _check(lib.dlr_dataset_generate(C.byref(spec), C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def generate_hashed(cls, n_rows: int, num_feature_dim: int = 1 << 24, fields: int = 39, *,
+                        cardinality: int = 1_000_000, zipf_s: float = 1.1, seed: int = 10, stream: int = 0,
+                        positive_frac: float = 0.25, label_noise: float = 0.05, nthreads: int = 0) -> "Dataset":
+        """Criteo-shaped hashed rows (BASELINE C3; dlr_dataset_generate_hashed)."""
+        spec = HashedSpec(n_rows, num_feature_dim, fields, nthreads, cardinality, zipf_s, seed, stream,
+                          positive_frac, label_noise)
+        h = P()
+        _check(lib.dlr_dataset_generate_hashed(C.byref(spec), C.byref(h)))
         return cls(h)
 
     def write_libsvm(self, path: str, value_mode: int = 0) -> None:

@@ -91,6 +91,24 @@ typedef struct dlr_gen_spec {
 } dlr_gen_spec;
 int dlr_dataset_generate(const dlr_gen_spec *spec, dlr_dataset **out);
 
+/* Criteo-shaped hashed categorical rows (BASELINE C3): `fields` fields, each
+ * drawing a value from Zipf(zipf_s) over [1, cardinality], hashed with
+ * splitmix64(field, value) mod num_feature_dim; duplicates within a row
+ * collapse, columns ascending, values 1.  Labels from a planted model. */
+typedef struct dlr_hashed_spec {
+    int64_t n_rows;
+    int64_t num_feature_dim;
+    int32_t fields;
+    int32_t nthreads;       /* <= 0: default                             */
+    int64_t cardinality;    /* values per field                          */
+    double zipf_s;
+    uint64_t seed;
+    uint64_t stream;
+    double positive_frac;
+    double label_noise;
+} dlr_hashed_spec;
+int dlr_dataset_generate_hashed(const dlr_hashed_spec *spec, dlr_dataset **out);
+
 /* Writes a dataset as libsvm text ("+1 idx:val ...", 1-based indices). */
 int dlr_dataset_write_libsvm(const dlr_dataset *ds, const char *path, int value_mode);
 

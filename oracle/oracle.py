@@ -192,6 +192,9 @@ def run_worker(shards: Sequence[Tuple[np.ndarray, np.ndarray]], D: int, num_iter
                mode: int = MODE_MEAN, C_: float = 1.0, random_state: int = 0, sparse: bool = True) -> RunResult:
     """main.cc:124-170 + lr.cc:28-63 with W = len(shards) workers.
 
+    A shard is (X, y) with X dense (N x D) or, for huge D, the CSR tuple
+    (row_ptr, col, val) that dense_to_csr would produce.
+
     Sync (modes MEAN/LAST): every worker pulls the same weights at step t
     (the server holds all pushes of a step until all W arrived), pushes
     arrive in rank order.  ASYNC: all workers pull the step's weights, the
@@ -208,7 +211,12 @@ def run_worker(shards: Sequence[Tuple[np.ndarray, np.ndarray]], D: int, num_iter
         raise ValueError(f"workers have different batch counts {nbs}: the reference's sync merge mixes epochs")
     data = []
     for X, y in shards:
-        data.append((dense_to_csr(X) if sparse else X, y))
+        if isinstance(X, tuple):        # already CSR (row_ptr, col, val): huge-D shards
+            if not sparse:
+                raise ValueError("CSR shards need sparse=True")
+            data.append((X, y))
+        else:
+            data.append((dense_to_csr(X) if sparse else X, y))
     test_csr = (dense_to_csr(test[0]), test[1]) if (test is not None and sparse) else test
     res = RunResult(w=w, pulled=pulled)
     for it in range(num_iteration):

@@ -146,3 +146,84 @@ def test_c5_shape_touched_steps():
         assert_same_weights(eng.get_weights(), w)
     finally:
         eng.close()
+
+
+# ---- C3: Criteo-shaped hashed rows, full-shard batches, Zipf-hot columns
+# (BASELINE configs[2]; rows reduced so the oracle finishes in seconds).
+
+def _c3_shards(W, rows=60_000):
+    return [dlr.Dataset.generate_hashed(rows, 1 << 24, 39, seed=10, stream=r + 1) for r in range(W)]
+
+
+def _csr_shard(ds):
+    # CSR straight to the oracle: a dense 60,000 x 2^24 shard would be 4 TB
+    rp, col, val, lab = ds.csr()
+    return (rp, col, val), lab
+
+
+def _hot_count(ds):
+    rp, col, val, lab = ds.csr()
+    return int(np.bincount(col).max())
+
+
+def test_c3_hot_columns_bitwise_without_chunking(monkeypatch):
+    # DLR_LONG_COLUMN=0: every column is one sequential sum -> bitwise
+    monkeypatch.setenv("DLR_LONG_COLUMN", "0")
+    D = 1 << 24
+    shards = _c3_shards(1)
+    assert _hot_count(shards[0]) > 4096
+    eng = run_engine(shards, D, 3, -1, 0.2)
+    orc = oracle.run_worker([_csr_shard(s) for s in shards], D, 3, -1, 0.2)
+    compare_runs(eng, orc)
+
+
+@pytest.mark.parametrize("W", [1, 2])
+def test_c3_long_column_chunking_within_tolerance(W):
+    # default: columns with > 4,096 entries are summed in 512-entry chunks
+    # (deterministic); weights stay within the north-star bar of the
+    # reference's single sequential sum: |a-b| <= 1e-5*|b| + 1e-7
+    D = 1 << 24
+    shards = _c3_shards(W)
+    eng = run_engine(shards, D, 3, -1, 0.2)
+    orc = oracle.run_worker([_csr_shard(s) for s in shards], D, 3, -1, 0.2)
+    a, b = eng.w.astype(np.float64), orc.w.astype(np.float64)
+    err = np.abs(a - b) - (1e-5 * np.abs(b) + 1e-7)
+    assert err.max() <= 0, f"max excess {err.max():.3g}"
+    # run twice: deterministic
+    eng2 = run_engine(shards, D, 3, -1, 0.2)
+    assert_same_weights(eng2.w, eng.w)
+
+
+def test_c3_long_columns_forced_collectives(monkeypatch):
+    # long columns through the key-range all-to-all exchange (1-rank comm)
+    monkeypatch.setenv("DLR_FORCE_COLLECTIVES", "1")
+    D = 1 << 24
+    shards = _c3_shards(1)
+    monkeypatch.delenv("DLR_FORCE_COLLECTIVES")
+    ref = run_engine(shards, D, 2, -1, 0.2)
+    monkeypatch.setenv("DLR_FORCE_COLLECTIVES", "1")
+    got = run_engine(shards, D, 2, -1, 0.2)
+    assert_same_weights(got.w, ref.w)
+
+
+def test_c3_long_column_gradient_tolerance():
+    # the pushed gradient itself (lr.cc:40's g): hot columns summed in
+    # chunks differ from the single sequential sum by rounding only
+    D = 1 << 24
+    ds = _c3_shards(1, rows=120_000)[0]
+    rp, col, val, lab = ds.csr()
+    hot = np.bincount(col, minlength=D) > 4096
+    assert hot.sum() >= 30
+    w0 = dlr.init_weight(D)
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(w0)
+        eng.load_train(ds, -1)
+        g = eng.worker_gradient(0, 1.0)
+    finally:
+        eng.close()
+    go = oracle.grad_csr((rp, col, val), lab, oracle.batch_rows(len(lab), -1, 0), w0)
+    # untouched-by-chunking columns: bitwise
+    assert_same_weights(g[~hot], go[~hot], "short-column gradient")
+    a, b = g[hot].astype(np.float64), go[hot].astype(np.float64)
+    assert np.all(np.abs(a - b) <= 1e-5 * np.abs(b) + 1e-9), np.max(np.abs(a - b) / np.abs(b))
