@@ -52,12 +52,18 @@ CONFIGS = {
     # = the full shard (B = -1, local.sh's batching), hashed Zipf fields
     "c3": dict(rows=12_500_000, features=1 << 24, nnz=39, batch=-1, value_mode=0, steps=10, warmup=2,
                label="C3 Criteo-shaped hashed LR", kind="hashed"),
+    # C4: dense 4,096 fp32 features; 20M rows over 8 GPUs = 2.5M rows/GPU
+    # (41 GB resident; a single GPU cannot hold all 20M rows: 328 GB)
+    "c4": dict(rows=2_500_000, features=4096, nnz=4096, batch=65536, value_mode=1, steps=100, warmup=5,
+               label="C4 dense LR", kind="dense"),
     "c5": dict(rows=1_024_000, features=1 << 28, nnz=10, batch=1024, value_mode=0, steps=200, warmup=10,
                label="C5 high-dim ultra-sparse LR"),
 }
 
 
-def make_shard(args, n_rows: int, stream: int) -> "dlr.Dataset":
+def make_shard(args, n_rows: int, stream: int):
+    if args.kind == "dense":
+        return dlr.DenseDataset.generate(n_rows, args.features, seed=10, stream=stream)
     if args.kind == "hashed":
         return dlr.Dataset.generate_hashed(n_rows, args.features, args.nnz, seed=10, stream=stream)
     return dlr.Dataset.generate(n_rows, args.features, args.nnz, value_mode=args.value_mode, seed=10, stream=stream)
@@ -89,11 +95,13 @@ def parse_args():
     return args
 
 
-def alg_bytes_per_step(B: int, nnz: float, D: int) -> int:
-    """8*nnz + 8 bytes per sample (int32 col + fp32 val per
-    nnz; row offset + label per row) + 8*D/B per sample (dense-L2 weight
-    read + write), times the B samples of one step."""
-    return int(round(B * (8 * nnz + 8) + 8 * D))
+def alg_bytes_per_step(B: int, nnz: float, D: int, dense: bool = False) -> int:
+    """sparse 8*nnz + 8 bytes per sample (int32 col + fp32
+    val per nnz; row offset + label per row), dense 4*D + 4 (the row + its
+    label), + 8*D/B per sample (dense-L2 weight read + write), times the B
+    samples of one step."""
+    per = 4 * D + 4 if dense else 8 * nnz + 8
+    return int(round(B * per + 8 * D))
 
 
 def cpu_baseline(args, D: int) -> dict:
@@ -105,20 +113,26 @@ def cpu_baseline(args, D: int) -> dict:
     B = args.batch if args.batch > 0 else 200_000   # full-shard configs: a 200k-row shard, B = -1
     n_rows = 4 * B if args.batch > 0 else B
     ds = make_shard(args, n_rows, 1)
-    rp, col, val, lab = ds.csr()
+    if args.kind == "dense":
+        X, lab = ds.arrays()
+        grad = lambda rr, ww: oracle.grad_dense(X, lab, rr, ww)       # noqa: E731
+    else:
+        rp, col, val, lab = ds.csr()
+        grad = lambda rr, ww: oracle.grad_csr((rp, col, val), lab, rr, ww)  # noqa: E731
     w = dlr.init_weight(D)
     bb = args.batch if args.batch > 0 else -1
     rows = [oracle.batch_rows(n_rows, bb, b % oracle.num_batches(n_rows, bb)) for b in range(4)]
     done, t0 = 0, time.perf_counter()
     while True:
-        g = oracle.grad_csr((rp, col, val), lab, rows[done % 4], w)
+        g = grad(rows[done % 4], w)
         oracle.server_update(w, [g], args.lr)
         done += 1
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds or done >= 5000:
             break
     return {"value": round(done * B / el, 1), "unit": "samples/s", "cores": 1, "kind": "port",
-            "sample": f"{done} steps of B={B}, D={D}, {args.nnz} nnz/row (oracle sparse port, 1 thread) in "
+            "sample": f"{done} steps of B={B}, D={D}, {args.nnz} nnz/row (oracle "
+                      f"{'dense' if args.kind == 'dense' else 'sparse'} port, 1 thread) in "
                       f"{el:.1f} s"}
 
 
@@ -143,15 +157,19 @@ def main():
 
     t_setup = time.perf_counter()
     ds = make_shard(args, args.rows, rank + 1)
-    nnz_avg = ds.info()[1] / max(1, args.rows)        # hashed rows lose a few duplicate fields
+    if args.kind == "dense":
+        nnz_avg = float(D)
+    else:
+        nnz_avg = ds.info()[1] / max(1, args.rows)    # hashed rows lose a few duplicate fields
     t_gen = time.perf_counter() - t_setup
     eng = dlr.Engine(D, device=local, rank=rank, world=world, unique_id=uid)
     eng.set_weights(dlr.init_weight(D))
-    nb = eng.load_train(ds, B)
+    nb = eng.load_train_dense(ds, B) if args.kind == "dense" else eng.load_train(ds, B)
     train_bytes, _ = eng.memory_info()
     ds.free()
     t_load = time.perf_counter() - t_setup - t_gen
-    layout = {dlr.LAYOUT_CLASSIC: "classic", dlr.LAYOUT_LDS: "lds", dlr.LAYOUT_TOUCHED: "touched"}[eng.train_layout()]
+    layout = "dense" if args.kind == "dense" else \
+        {dlr.LAYOUT_CLASSIC: "classic", dlr.LAYOUT_LDS: "lds", dlr.LAYOUT_TOUCHED: "touched"}[eng.train_layout()]
     log(f"[rank {rank}] shard {args.rows} x {D}, nnz/row {args.nnz}: generated {t_gen:.1f}s, resident "
         f"{train_bytes / 2**30:.2f} GiB in {t_load:.1f}s, {nb} batches/epoch, gradient layout {layout}")
 
@@ -201,7 +219,7 @@ def main():
     value = samples / el
     avg_us = {k: (ms / n * 1000.0 if n else 0.0) for k, (ms, n) in kt.items()}
     kern_us = avg_us["margin"] + avg_us["grad_update"] + avg_us["merge"]
-    step_bytes = alg_bytes_per_step(B_eff, nnz_avg, D)
+    step_bytes = alg_bytes_per_step(B_eff, nnz_avg, D, args.kind == "dense")
     achieved = step_bytes / (kern_us * 1e-6) / 1e9 if kern_us > 0 else 0.0
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -234,7 +252,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded gen_data.py-shaped sparse rows, "
+            "data": f"synthetic (seeded gen_data.py-shaped {'dense' if args.kind == 'dense' else 'sparse'} rows, "
                     f"{'4-decimal' if args.value_mode else 'binary'} values; resident in HBM)",
             "config": {"workload": f"{args.label}: {args.rows} rows/GPU x {D} features, {args.nnz} nnz/row, "
                                    f"batch {B}, sync SGD lr {args.lr}, C=1",

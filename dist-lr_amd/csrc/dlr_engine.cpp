@@ -73,6 +73,9 @@ struct TrainShard {
     void *lrow = nullptr;
     float *lval = nullptr, *lpart = nullptr;
     std::vector<int64_t> lcoff, lsoff, leoff;
+    // dense shard (dlr_load_train_dense): X row-major n_rows x D
+    bool dense = false, dblocked = false;
+    float *dX = nullptr, *dpart = nullptr;
     bool row16 = false;
     uint32_t *cptr = nullptr;   // n_batches x (D+1)
     void *crow = nullptr;
@@ -83,6 +86,8 @@ struct TrainShard {
 
 struct TestShard {
     bool loaded = false;
+    bool dense = false;
+    float *dX = nullptr;
     int64_t n_rows = 0, nnz = 0;
     int64_t *row_ptr = nullptr;
     int32_t *col = nullptr;
@@ -189,7 +194,8 @@ void free_train(dlr_ctx *c) {
     for (void *p : {(void *)t.row_ptr, (void *)t.col, (void *)t.val, (void *)t.label, (void *)t.w_row_ptr,
                     (void *)t.w_col, (void *)t.w_val, (void *)t.w_label, (void *)t.cptr, t.crow, (void *)t.cval,
                     (void *)t.pbase, (void *)t.pends, (void *)t.prow, (void *)t.pval, (void *)t.tcols,
-                    (void *)t.lcols, (void *)t.lcseg, (void *)t.lsptr, t.lrow, (void *)t.lval, (void *)t.lpart})
+                    (void *)t.lcols, (void *)t.lcseg, (void *)t.lsptr, t.lrow, (void *)t.lval, (void *)t.lpart,
+                    (void *)t.dX, (void *)t.dpart})
         dev_free(c, p);
     t = TrainShard();
 }
@@ -204,7 +210,7 @@ void free_touched_bufs(dlr_ctx *c) {
 
 void free_test(dlr_ctx *c) {
     TestShard &t = c->test;
-    for (void *p : {(void *)t.row_ptr, (void *)t.col, (void *)t.val, (void *)t.label}) dev_free(c, p);
+    for (void *p : {(void *)t.row_ptr, (void *)t.col, (void *)t.val, (void *)t.label, (void *)t.dX}) dev_free(c, p);
     t = TestShard();
 }
 
@@ -530,6 +536,14 @@ dlr::DevBatch batch_view(const dlr_ctx *c, int64_t b) {
     return {t.row_ptr + sp.first_row, t.col, t.val, t.label + sp.first_row, sp.rows, nnz};
 }
 
+hipError_t launch_margin(dlr_ctx *c, int64_t b) {
+    const TrainShard &t = c->train;
+    if (t.dense)
+        return dlr::launch_dense_margin({t.dX, t.label, t.n_rows, c->D}, t.plan[(size_t)b].first_row,
+                                        t.plan[(size_t)b].rows, c->w, c->resid, c->stream);
+    return dlr::launch_margin_residual(batch_view(c, b), c->w, c->resid, c->stream);
+}
+
 dlr::DevPcsc pcsc_view(const dlr_ctx *c, int64_t b) {
     const TrainShard &t = c->train;
     return {t.pbase + (size_t)b * (size_t)(t.pblocks + 1), t.pends + (size_t)b * (size_t)t.pblocks * 64,
@@ -544,8 +558,13 @@ dlr::DevCsc csc_view(const dlr_ctx *c, int64_t b) {
             t.row16};
 }
 
+dlr::DevDense dense_view(const TrainShard &t, int64_t D) { return {t.dX, t.label, t.n_rows, D}; }
+
 hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float lr, float C, bool fused) {
     const TrainShard &t = c->train;
+    if (t.dense)
+        return dlr::launch_dense_grad(dense_view(t, c->D), t.plan[(size_t)b].first_row, B, c->resid, c->w, gout,
+                                      t.dpart, t.dblocked, lr, C, fused, c->stream);
     if (t.pcsc) return dlr::launch_grad_lds(pcsc_view(c, b), c->D, B, c->resid, c->w, gout, lr, C, fused, c->stream);
     hipError_t e = dlr::launch_grad(csc_view(c, b), c->D, c->resid, c->w, gout, B, lr, C, fused, c->stream);
     if (e != hipSuccess || !t.any_long) return e;
@@ -932,18 +951,83 @@ int dlr_load_test(dlr_ctx *c, const dlr_dataset *ds) {
     return DLR_OK;
 }
 
+int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, int64_t *n_batches) {
+    if (!c || !ds) return fail(c, DLR_E_ARG, "dlr_load_train_dense: bad argument");
+    if (ds->D != c->D) return fail(c, DLR_E_ARG, "dlr_load_train_dense: dataset D != context D");
+    if (batch_size == 0) return fail(c, DLR_E_ARG, "dlr_load_train_dense: batch_size 0 (reference never terminates)");
+    if (ds->n_rows <= 0) return fail(c, DLR_E_ARG, "dlr_load_train_dense: empty shard (reference never terminates)");
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    free_train(c);
+    free_touched_bufs(c);
+    TrainShard &t = c->train;
+    t.dense = true;
+    t.n_rows = ds->n_rows;
+    t.B = batch_size < 0 ? ds->n_rows : batch_size;
+    t.plan = dlr::plan_batches(ds->n_rows, batch_size);
+    const int64_t D = c->D;
+    const char *dg = getenv("DLR_DENSE_GRAD");
+    t.dblocked = dg ? strcmp(dg, "blocked") == 0 : (t.B * D > ((int64_t)1 << 24));
+    int rc;
+    if ((rc = upload(c, &t.dX, ds->X.data(), ds->X.size(), 64))) return rc;
+    {
+        std::vector<float> lab(ds->label.begin(), ds->label.end());
+        if ((rc = upload(c, &t.label, lab.data(), lab.size()))) return rc;
+    }
+    if (t.dblocked &&
+        (rc = dev_alloc(c, (void **)&t.dpart, (size_t)dlr::dense_chunks(t.B) * (size_t)((D + 3) & ~int64_t(3)) * 4)))
+        return rc;
+    if (c->resid_cap < t.B) {
+        dev_free(c, c->resid);
+        c->resid = nullptr;
+        if ((rc = dev_alloc(c, (void **)&c->resid, (size_t)t.B * 4))) return rc;
+        c->resid_cap = t.B;
+    }
+    t.bytes = (int64_t)(ds->X.size() * 4 + ds->label.size() * 4);
+    t.loaded = true;
+    if (n_batches) *n_batches = (int64_t)t.plan.size();
+    return DLR_OK;
+}
+
+int dlr_load_test_dense(dlr_ctx *c, const dlr_dense *ds) {
+    if (!c || !ds) return fail(c, DLR_E_ARG, "dlr_load_test_dense: bad argument");
+    if (ds->D != c->D) return fail(c, DLR_E_ARG, "dlr_load_test_dense: dataset D != context D");
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    free_test(c);
+    TestShard &t = c->test;
+    t.dense = true;
+    t.n_rows = ds->n_rows;
+    int rc;
+    if ((rc = upload(c, &t.dX, ds->X.data(), ds->X.size(), 64))) return rc;
+    std::vector<float> lab(ds->label.begin(), ds->label.end());
+    if ((rc = upload(c, &t.label, lab.data(), lab.size()))) return rc;
+    t.grid = dlr::predict_dense_grid(t.n_rows);
+    if (c->ll_cap < t.grid + 1) {
+        dev_free(c, c->ll);
+        c->ll = nullptr;
+        if ((rc = dev_alloc(c, (void **)&c->ll, (size_t)(t.grid + 1) * 8))) return rc;
+        c->ll_cap = t.grid + 1;
+    }
+    t.bytes = (int64_t)(ds->X.size() * 4 + ds->label.size() * 4);
+    t.loaded = true;
+    return DLR_OK;
+}
+
 int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
     if (!c) return fail(c, DLR_E_ARG, "dlr_train_step: null context");
     if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_step: no training shard loaded");
     if (b < 0 || b >= (int64_t)c->train.plan.size()) return fail(c, DLR_E_ARG, "dlr_train_step: batch out of range");
     if (mode < 0 || mode > 2) return fail(c, DLR_E_ARG, "dlr_train_step: bad mode");
     HIPC(c, hipSetDevice(c->device));
-    const dlr::DevBatch bt = batch_view(c, b);
+    struct {
+        int64_t rows;
+    } const bt{c->train.plan[(size_t)b].rows};
     if (bt.rows > c->resid_cap) return fail(c, DLR_E_STATE, "dlr_train_step: residual buffer too small");
     hipEvent_t t_step, t0;
     time_begin(c, &t_step);
     time_begin(c, &t0);
-    HIPC(c, dlr::launch_margin_residual(bt, c->w, c->resid, c->stream));
+    HIPC(c, launch_margin(c, b));
     time_end(c, 0, t0);
     if (c->train.touched) {
         // touched columns (ordered gradient), then the dense L2 pass over
@@ -1021,8 +1105,10 @@ int dlr_worker_gradient(dlr_ctx *c, int64_t b, float C, float *grad_out, int64_t
     if (b < 0 || b >= (int64_t)c->train.plan.size())
         return fail(c, DLR_E_ARG, "dlr_worker_gradient: batch out of range");
     HIPC(c, hipSetDevice(c->device));
-    const dlr::DevBatch bt = batch_view(c, b);
-    HIPC(c, dlr::launch_margin_residual(bt, c->w, c->resid, c->stream));
+    struct {
+        int64_t rows;
+    } const bt{c->train.plan[(size_t)b].rows};
+    HIPC(c, launch_margin(c, b));
     if (c->train.touched) {
         // full pushed vector: the L2 term everywhere, the touched columns' g
         const TrainShard &t = c->train;
@@ -1061,8 +1147,13 @@ int dlr_predict(dlr_ctx *c, int64_t *correct, int64_t *n_rows, double *logloss) 
     HIPC(c, hipSetDevice(c->device));
     const TestShard &t = c->test;
     HIPC(c, hipMemsetAsync(c->correct, 0, 8, c->stream));
-    const dlr::DevBatch bt{t.row_ptr, t.col, t.val, t.label, t.n_rows, t.nnz};
-    HIPC(c, dlr::launch_predict(bt, c->w, c->correct, c->ll + 1, c->ll, c->stream));
+    if (t.dense) {
+        HIPC(c, dlr::launch_dense_predict({t.dX, t.label, t.n_rows, c->D}, c->w, c->correct, c->ll + 1, c->ll,
+                                          c->stream));
+    } else {
+        const dlr::DevBatch bt{t.row_ptr, t.col, t.val, t.label, t.n_rows, t.nnz};
+        HIPC(c, dlr::launch_predict(bt, c->w, c->correct, c->ll + 1, c->ll, c->stream));
+    }
     HIPC(c, hipMemcpyAsync(c->h_correct, c->correct, 8, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipMemcpyAsync(c->h_ll, c->ll, 8, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));

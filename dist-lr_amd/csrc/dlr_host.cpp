@@ -375,6 +375,73 @@ extern "C" int dlr_dataset_view(const dlr_dataset *ds, const int64_t **row_ptr, 
 
 extern "C" void dlr_dataset_free(dlr_dataset *ds) { delete ds; }
 
+// ------------------------------------------------------------------ dense
+
+extern "C" int dlr_dense_from_dataset(const dlr_dataset *ds, dlr_dense **out) {
+    if (!ds || !out) {
+        set_error("dlr_dense_from_dataset: bad argument");
+        return DLR_E_ARG;
+    }
+    *out = nullptr;
+    auto d = std::make_unique<dlr_dense>();
+    d->n_rows = ds->n_rows;
+    d->D = ds->D;
+    try {
+        d->X.assign((size_t)(ds->n_rows * ds->D), 0.0f);
+    } catch (...) {
+        set_error("dlr_dense_from_dataset: out of host memory");
+        return DLR_E_NOMEM;
+    }
+    for (int64_t i = 0; i < ds->n_rows; ++i)
+        for (int64_t k = ds->row_ptr[(size_t)i]; k < ds->row_ptr[(size_t)i + 1]; ++k)
+            d->X[(size_t)(i * ds->D + ds->col[(size_t)k])] = ds->val[(size_t)k];
+    d->label = ds->label;
+    *out = d.release();
+    return DLR_OK;
+}
+
+extern "C" int dlr_dense_from_array(int64_t n_rows, int64_t num_feature_dim, const float *X, const int32_t *label,
+                                    dlr_dense **out) {
+    if (!out || n_rows < 0 || num_feature_dim <= 0 || (n_rows > 0 && (!X || !label))) {
+        set_error("dlr_dense_from_array: bad argument");
+        return DLR_E_ARG;
+    }
+    *out = nullptr;
+    for (int64_t i = 0; i < n_rows; ++i)
+        if (label[i] != 0 && label[i] != 1) {
+            set_error("dlr_dense_from_array: labels must be 0/1");
+            return DLR_E_ARG;
+        }
+    auto d = std::make_unique<dlr_dense>();
+    d->n_rows = n_rows;
+    d->D = num_feature_dim;
+    try {
+        d->X.assign(X, X + n_rows * num_feature_dim);
+        d->label.assign(label, label + n_rows);
+    } catch (...) {
+        set_error("dlr_dense_from_array: out of host memory");
+        return DLR_E_NOMEM;
+    }
+    *out = d.release();
+    return DLR_OK;
+}
+
+extern "C" int dlr_dense_info(const dlr_dense *ds, int64_t *n_rows, int64_t *D) {
+    if (!ds) return DLR_E_ARG;
+    if (n_rows) *n_rows = ds->n_rows;
+    if (D) *D = ds->D;
+    return DLR_OK;
+}
+
+extern "C" int dlr_dense_view(const dlr_dense *ds, const float **X, const int32_t **label) {
+    if (!ds) return DLR_E_ARG;
+    if (X) *X = ds->X.data();
+    if (label) *label = ds->label.data();
+    return DLR_OK;
+}
+
+extern "C" void dlr_dense_free(dlr_dense *ds) { delete ds; }
+
 extern "C" int dlr_dataset_write_libsvm(const dlr_dataset *ds, const char *path, int value_mode) {
     if (!ds || !path) return DLR_E_ARG;
     FILE *f = fopen(path, "wb");
@@ -717,6 +784,62 @@ extern "C" int dlr_dataset_generate_hashed(const dlr_hashed_spec *spec, dlr_data
         return DLR_E_NOMEM;
     }
     *out = ds.release();
+    return DLR_OK;
+}
+
+// Dense rows for C4 (4,096 features x 20M samples fp32): every feature a
+// 4-decimal value in (0,1] held as ToFloat of its text; planted labels.
+extern "C" int dlr_dense_generate(const dlr_dense_spec *spec, dlr_dense **out) {
+    if (!spec || !out || spec->n_rows < 0 || spec->num_feature_dim <= 0) {
+        set_error("dlr_dense_generate: bad spec");
+        return DLR_E_ARG;
+    }
+    *out = nullptr;
+    const int64_t N = spec->n_rows, D = spec->num_feature_dim;
+    auto d = std::make_unique<dlr_dense>();
+    d->n_rows = N;
+    d->D = D;
+    try {
+        d->X.resize((size_t)(N * D));
+        d->label.resize((size_t)N);
+    } catch (...) {
+        set_error("dlr_dense_generate: out of host memory");
+        return DLR_E_NOMEM;
+    }
+    std::vector<float> wstar = planted_model(spec->seed, D, spec->nthreads);
+    std::vector<float> lut(10001);
+    for (int q = 1; q <= 10000; ++q) {
+        char t[16];
+        if (q == 10000)
+            snprintf(t, sizeof t, "1.0000");
+        else
+            snprintf(t, sizeof t, "0.%04d", q);
+        lut[(size_t)q] = dlr_to_float(t);
+    }
+    // centre the planted margin: E[x] = 0.50005 per feature
+    const double thr = normal_quantile(1.0 - std::min(std::max(spec->positive_frac, 1e-6), 1.0 - 1e-6));
+    const uint64_t stream_key = mix64(spec->seed ^ mix64(0xDE45Eull + spec->stream));
+    int nt = spec->nthreads > 0 ? spec->nthreads : dlr::default_threads();
+    nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, N / 256 + 1));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            for (int64_t i = N * t / nt; i < N * (t + 1) / nt; ++i) {
+                Rng g(mix64(stream_key ^ (uint64_t)i * 0xD1342543DE82EF95ull));
+                float *x = d->X.data() + (size_t)(i * D);
+                double m = 0;
+                for (int64_t j = 0; j < D; ++j) {
+                    const uint64_t q = 1 + g.below(10000);
+                    x[j] = lut[(size_t)q];
+                    m += (double)wstar[(size_t)j] * ((double)q * 1e-4 - 0.50005);
+                }
+                bool pos = (m / std::sqrt((double)D / 12.0)) > thr;
+                if (g.unit() < spec->label_noise) pos = !pos;
+                d->label[(size_t)i] = pos ? 1 : 0;
+            }
+        });
+    for (auto &x : th) x.join();
+    *out = d.release();
     return DLR_OK;
 }
 

@@ -18,6 +18,15 @@ struct dlr_dataset {
     std::vector<int32_t> label;    // 0 / 1
 };
 
+// Dense shard: what distlr::DataIter itself holds (data_iter.h:28: every
+// Sample is a D-float vector), row-major N x D fp32.
+struct dlr_dense {
+    int64_t n_rows = 0;
+    int64_t D = 0;
+    std::vector<float> X;        // n_rows * D
+    std::vector<int32_t> label;  // 0 / 1
+};
+
 namespace dlr {
 
 // Thread-local "last error" for calls that have no context (and mirror of

@@ -59,6 +59,13 @@ struct DevPcsc {
     int phases;
 };
 
+// Dense rows (row-major N x D fp32) and 0/1 labels as floats.
+struct DevDense {
+    const float *X;
+    const float *label;
+    int64_t N, D;
+};
+
 // Batch size of every rank (the L2 term of rank r's push is
 // fl32(C*w)/(float)B_r); at most kMaxRanks ranks.
 constexpr int kMaxRanks = 16;
@@ -90,6 +97,15 @@ hipError_t launch_scatter(float *w, const uint32_t *cols, const float *newv, int
 hipError_t launch_sparse_merge(const uint32_t *lists, int64_t cap, int64_t stride, const float *w,
                                const RankSizes &rs, float lr, float C, int mode, uint32_t *out_cols, float *out_newv,
                                hipStream_t s);
+// K6 dense (dlr_kernels.hip "K6: dense rows"): batch rows (first+i) mod N.
+hipError_t launch_dense_margin(const DevDense &dd, int64_t first, int64_t B, const float *w, float *resid,
+                               hipStream_t s);
+int64_t dense_chunks(int64_t B);  // row chunks of the blocked gradient (part: chunks x roundup4(D) floats)
+hipError_t launch_dense_grad(const DevDense &dd, int64_t first, int64_t B, const float *resid, float *w, float *gout,
+                             float *part, bool blocked, float lr, float C, bool fused, hipStream_t s);
+int predict_dense_grid(int64_t rows);
+hipError_t launch_dense_predict(const DevDense &dd, const float *w, unsigned long long *correct, double *ll_part,
+                                double *ll_out, hipStream_t s);
 hipError_t launch_merge_update(const float *recv, int W, int64_t chunk, int64_t n, float *w_own, float lr, int mode,
                                hipStream_t s);
 

@@ -693,6 +693,194 @@ __global__ __launch_bounds__(256) void k_sparse_merge(const uint32_t *__restrict
     out_newv[idx] = server_apply(wj, g, W, lr, mode, false);
 }
 
+// ---------------------------------------------------------------------------
+// K6: dense rows (BASELINE C4, 4,096 features; and the reference's own dense
+// representation).  GEMV-shaped and HBM-bound (0.5 flop/byte): no MFMA --
+// its f32 MFMA would also reorder the sums.  Batch row i is shard row
+// (first + i) mod N (NextBatch's wrap, data_iter.h:49-52).
+
+// Shard row of batch row i: (first + i) mod N without a 64-bit division
+// (first < N; a batch wraps ceil(B/N) times at most).
+__device__ __forceinline__ int64_t wrap_row(int64_t r, int64_t N) {
+    while (r >= N) r -= N;
+    return r;
+}
+
+// K6a: lane per batch row; z = sum_j w_j*x_ij sequential fp32, j ascending
+// (lr.cc:108-112), then sigma - y.  VEC4 (D % 4 == 0): 16-byte loads along
+// the row, 8 in flight; w is wave-uniform (scalar loads).
+template <bool VEC4>
+__global__ __launch_bounds__(256) void k_dense_margin(DevDense dd, int64_t first, int64_t B,
+                                                      const float *__restrict__ w, float *__restrict__ resid) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    const int64_t row = wrap_row(first + i, dd.N);
+    const float *__restrict__ x = dd.X + row * dd.D;
+    float acc = 0.0f;
+    int64_t j = 0;
+    if (VEC4) {
+        constexpr int U = 8;
+        for (; j + 4 * U <= dd.D; j += 4 * U) {
+            float4 xv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) xv[u] = *reinterpret_cast<const float4 *>(x + j + 4 * u);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const float4 wv = *reinterpret_cast<const float4 *>(w + j + 4 * u);
+                acc = acc + wv.x * xv[u].x;
+                acc = acc + wv.y * xv[u].y;
+                acc = acc + wv.z * xv[u].z;
+                acc = acc + wv.w * xv[u].w;
+            }
+        }
+    }
+    for (; j < dd.D; ++j) acc = acc + w[j] * x[j];
+    resid[i] = sigmoid_ref(acc) - dd.label[row];
+}
+
+// K6b, reference order: lane per column, G_j = sum over the batch rows in
+// order of fl32(r_i*x_ij) (lr.cc:35-39); 8 rows' loads in flight.  Only
+// D/64 waves: for parity-scale batches (DLR_DENSE_GRAD).
+template <bool FUSED>
+__global__ __launch_bounds__(256) void k_dense_grad_seq(DevDense dd, int64_t first, int64_t B,
+                                                        const float *__restrict__ resid, float *__restrict__ w,
+                                                        float *__restrict__ gout, float Bf, double Bd, float lr,
+                                                        float C) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= dd.D) return;
+    constexpr int U = 8;
+    float acc = 0.0f;
+    for (int64_t i = 0; i < B; i += U) {
+        float xv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t ii = i + u < B ? i + u : B - 1;
+            xv[u] = dd.X[wrap_row(first + ii, dd.N) * dd.D + j];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i + u < B) acc = acc + resid[i + u] * xv[u];
+    }
+    const float wj = w[j];
+    const float cw = C * wj;
+    const float l2 = cw / Bf;
+    const float g = (float)((double)acc / Bd + (double)l2);
+    if (FUSED) {
+        const float step = lr * g;
+        w[j] = wj - step;
+    } else {
+        gout[j] = g;
+    }
+}
+
+// K6b, blocked: workgroup (k, c) sums batch rows [k*R, (k+1)*R) of columns
+// [c*1024, (c+1)*1024) -- per column sequential in row order, 4 columns per
+// lane (16-byte loads along the row: every row read once, coalesced) --
+// into part[k][j]; k_dense_combine then adds the chunk partials in chunk
+// order.  Deterministic; a different (blocked) order than lr.cc:37.
+constexpr int kDenseChunk = 256;
+template <bool VEC4>
+__global__ __launch_bounds__(256) void k_dense_grad_blocked(DevDense dd, int64_t first, int64_t B,
+                                                            const float *__restrict__ resid, int64_t Dp,
+                                                            float *__restrict__ part) {
+    const int64_t k = blockIdx.x;
+    const int64_t i0 = k * kDenseChunk, i1 = min(i0 + kDenseChunk, B);
+    constexpr int U = 8;
+    if (VEC4) {
+        const int64_t j = ((int64_t)blockIdx.y * blockDim.x + threadIdx.x) * 4;
+        if (j >= dd.D) return;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int64_t i = i0; i < i1; i += U) {
+            float4 xv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t ii = i + u < i1 ? i + u : i1 - 1;
+                xv[u] = *reinterpret_cast<const float4 *>(dd.X + wrap_row(first + ii, dd.N) * dd.D + j);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (i + u < i1) {
+                    const float r = resid[i + u];
+                    acc.x = acc.x + r * xv[u].x;
+                    acc.y = acc.y + r * xv[u].y;
+                    acc.z = acc.z + r * xv[u].z;
+                    acc.w = acc.w + r * xv[u].w;
+                }
+            }
+        }
+        *reinterpret_cast<float4 *>(part + k * Dp + j) = acc;
+    } else {
+        const int64_t j = (int64_t)blockIdx.y * blockDim.x + threadIdx.x;
+        if (j >= dd.D) return;
+        float acc = 0.0f;
+        for (int64_t i = i0; i < i1; ++i) acc = acc + resid[i] * dd.X[wrap_row(first + i, dd.N) * dd.D + j];
+        part[k * Dp + j] = acc;
+    }
+}
+
+template <bool FUSED>
+__global__ __launch_bounds__(256) void k_dense_combine(const float *__restrict__ part, int64_t nchunks, int64_t Dp,
+                                                       int64_t D, float *__restrict__ w, float *__restrict__ gout,
+                                                       float Bf, double Bd, float lr, float C) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= D) return;
+    float G = 0.0f;
+    for (int64_t k = 0; k < nchunks; ++k) G = G + part[k * Dp + j];
+    const float wj = w[j];
+    const float cw = C * wj;
+    const float l2 = cw / Bf;
+    const float g = (float)((double)G / Bd + (double)l2);
+    if (FUSED) {
+        const float step = lr * g;
+        w[j] = wj - step;
+    } else {
+        gout[j] = g;
+    }
+}
+
+// K5 dense: LR::Test on dense rows (lr.cc:47-63, 100-106); counts and
+// log-loss partials as k_predict.
+template <bool VEC4>
+__global__ __launch_bounds__(kWaves *kWave) void k_dense_predict(DevDense dd, const float *__restrict__ w,
+                                                                 unsigned long long *__restrict__ correct,
+                                                                 double *__restrict__ ll_part) {
+    __shared__ double s_ll[kWaves];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double ll = 0.0;
+    bool hit = false;
+    if (i < dd.N) {
+        const float *__restrict__ x = dd.X + i * dd.D;
+        float z = 0.0f;
+        int64_t j = 0;
+        if (VEC4)
+            for (; j + 4 <= dd.D; j += 4) {
+                const float4 xv = *reinterpret_cast<const float4 *>(x + j);
+                const float4 wv4 = *reinterpret_cast<const float4 *>(w + j);
+                z = z + wv4.x * xv.x;
+                z = z + wv4.y * xv.y;
+                z = z + wv4.z * xv.z;
+                z = z + wv4.w * xv.w;
+            }
+        for (; j < dd.D; ++j) z = z + w[j] * x[j];
+        const float y = dd.label[i];
+        hit = (z > 0.0f ? 1 : 0) == (int)y;
+        ll = y != 0.0f ? softplus(-(double)z) : softplus((double)z);
+    }
+    const unsigned long long m = __ballot(hit);
+    if (lane == 0 && m) atomicAdd(correct, (unsigned long long)__popcll(m));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) ll += __shfl_xor(ll, off);
+    if (lane == 0) s_ll[wv] = ll;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int q = 0; q < kWaves; ++q) t += s_ll[q];
+        ll_part[blockIdx.x] = t;
+    }
+}
+
 // K4 for world > 1: this rank owns keys [kb, kb+n) ("serves" them, the
 // role of KVStoreDistServer::DataHandle, main.cc:57-84).  recv holds the W
 // ranks' pushed gradients for the owned range, rank-major.
@@ -917,6 +1105,66 @@ hipError_t launch_grad_long(const DevLong &lg, int64_t B, const float *resid, fl
                            lg.ncols, part, w, gout, Bf, Bd, lr, C);
     return hipGetLastError();
 }
+
+hipError_t launch_dense_margin(const DevDense &dd, int64_t first, int64_t B, const float *w, float *resid,
+                               hipStream_t s) {
+    if (B <= 0) return hipSuccess;
+    if (dd.D % 4 == 0)
+        hipLaunchKernelGGL(k_dense_margin<true>, dim3(grid_for(B, 256)), dim3(256), 0, s, dd, first, B, w, resid);
+    else
+        hipLaunchKernelGGL(k_dense_margin<false>, dim3(grid_for(B, 256)), dim3(256), 0, s, dd, first, B, w, resid);
+    return hipGetLastError();
+}
+
+int64_t dense_chunks(int64_t B) { return (B + kDenseChunk - 1) / kDenseChunk; }
+
+hipError_t launch_dense_grad(const DevDense &dd, int64_t first, int64_t B, const float *resid, float *w, float *gout,
+                             float *part, bool blocked, float lr, float C, bool fused, hipStream_t s) {
+    if (B <= 0) return hipSuccess;
+    const float Bf = (float)B;
+    const double Bd = (double)B;
+    if (!blocked) {
+        if (fused)
+            hipLaunchKernelGGL(k_dense_grad_seq<true>, dim3(grid_for(dd.D, 256)), dim3(256), 0, s, dd, first, B, resid,
+                               w, gout, Bf, Bd, lr, C);
+        else
+            hipLaunchKernelGGL(k_dense_grad_seq<false>, dim3(grid_for(dd.D, 256)), dim3(256), 0, s, dd, first, B,
+                               resid, w, gout, Bf, Bd, lr, C);
+        return hipGetLastError();
+    }
+    const int64_t nch = dense_chunks(B);
+    const int64_t Dp = (dd.D + 3) & ~int64_t(3);
+    if (dd.D % 4 == 0)
+        hipLaunchKernelGGL(k_dense_grad_blocked<true>, dim3((unsigned)nch, grid_for(dd.D / 4, 256)), dim3(256), 0, s,
+                           dd, first, B, resid, Dp, part);
+    else
+        hipLaunchKernelGGL(k_dense_grad_blocked<false>, dim3((unsigned)nch, grid_for(dd.D, 256)), dim3(256), 0, s,
+                           dd, first, B, resid, Dp, part);
+    if (fused)
+        hipLaunchKernelGGL(k_dense_combine<true>, dim3(grid_for(dd.D, 256)), dim3(256), 0, s, part, nch, Dp, dd.D, w,
+                           gout, Bf, Bd, lr, C);
+    else
+        hipLaunchKernelGGL(k_dense_combine<false>, dim3(grid_for(dd.D, 256)), dim3(256), 0, s, part, nch, Dp, dd.D,
+                           w, gout, Bf, Bd, lr, C);
+    return hipGetLastError();
+}
+
+hipError_t launch_dense_predict(const DevDense &dd, const float *w, unsigned long long *correct, double *ll_part,
+                                double *ll_out, hipStream_t s) {
+    const int grid = predict_dense_grid(dd.N);
+    if (grid > 0) {
+        if (dd.D % 4 == 0)
+            hipLaunchKernelGGL(k_dense_predict<true>, dim3(grid), dim3(kWaves * kWave), 0, s, dd, w, correct,
+                               ll_part);
+        else
+            hipLaunchKernelGGL(k_dense_predict<false>, dim3(grid), dim3(kWaves * kWave), 0, s, dd, w, correct,
+                               ll_part);
+    }
+    hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(64), 0, s, ll_part, grid, ll_out);
+    return hipGetLastError();
+}
+
+int predict_dense_grid(int64_t rows) { return rows <= 0 ? 0 : (int)grid_for(rows, kWaves * kWave); }
 
 hipError_t launch_merge_update(const float *recv, int W, int64_t chunk, int64_t n, float *w_own, float lr, int mode,
                                hipStream_t s) {

@@ -30,10 +30,13 @@ SYMBOLS = [
     "dlr_to_int", "dlr_to_float", "dlr_split",
     "dlr_dataset_load_libsvm", "dlr_dataset_from_csr", "dlr_dataset_generate", "dlr_dataset_generate_hashed",
     "dlr_dataset_write_libsvm", "dlr_dataset_info", "dlr_dataset_view", "dlr_dataset_free",
+    "dlr_dense_from_dataset", "dlr_dense_from_array", "dlr_dense_generate", "dlr_dense_info", "dlr_dense_view",
+    "dlr_dense_free",
     "dlr_num_batches", "dlr_batch_rows",
     "dlr_init_weight", "dlr_format_model", "dlr_key_range",
     "dlr_get_unique_id", "dlr_create", "dlr_destroy", "dlr_last_error",
-    "dlr_set_weights", "dlr_get_weights", "dlr_load_train", "dlr_load_test",
+    "dlr_set_weights", "dlr_get_weights", "dlr_load_train", "dlr_load_test", "dlr_load_train_dense",
+    "dlr_load_test_dense",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
     "dlr_timing", "dlr_kernel_time", "dlr_train_layout", "dlr_memory_info",
 ]
@@ -76,6 +79,19 @@ class HashedSpec(C.Structure):
     ]
 
 
+class DenseSpec(C.Structure):
+    _fields_ = [
+        ("n_rows", C.c_int64),
+        ("num_feature_dim", C.c_int64),
+        ("seed", C.c_uint64),
+        ("stream", C.c_uint64),
+        ("positive_frac", C.c_double),
+        ("label_noise", C.c_double),
+        ("nthreads", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+
 def _sig(name, res, *args):
     f = getattr(lib, name)
     f.restype = res
@@ -90,6 +106,14 @@ _sig("dlr_dataset_load_libsvm", C.c_int, C.c_char_p, i64, C.c_int, C.POINTER(P))
 _sig("dlr_dataset_from_csr", C.c_int, i64, i64, P, P, P, P, C.POINTER(P))
 _sig("dlr_dataset_generate", C.c_int, C.POINTER(GenSpec), C.POINTER(P))
 _sig("dlr_dataset_generate_hashed", C.c_int, C.POINTER(HashedSpec), C.POINTER(P))
+_sig("dlr_dense_from_dataset", C.c_int, P, C.POINTER(P))
+_sig("dlr_dense_from_array", C.c_int, i64, i64, P, P, C.POINTER(P))
+_sig("dlr_dense_generate", C.c_int, C.POINTER(DenseSpec), C.POINTER(P))
+_sig("dlr_dense_info", C.c_int, P, C.POINTER(i64), C.POINTER(i64))
+_sig("dlr_dense_view", C.c_int, P, C.POINTER(P), C.POINTER(P))
+_sig("dlr_dense_free", None, P)
+_sig("dlr_load_train_dense", C.c_int, P, P, i64, C.POINTER(i64))
+_sig("dlr_load_test_dense", C.c_int, P, P)
 _sig("dlr_dataset_write_libsvm", C.c_int, P, C.c_char_p, C.c_int)
 _sig("dlr_dataset_info", C.c_int, P, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64))
 _sig("dlr_dataset_view", C.c_int, P, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P))
@@ -250,6 +274,65 @@ class Dataset:
             pass
 
 
+class DenseDataset:
+    """Host dense shard (dlr_dense): row-major N x D fp32 + 0/1 labels."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @property
+    def handle(self):
+        return self._h
+
+    @classmethod
+    def from_dataset(cls, ds: "Dataset") -> "DenseDataset":
+        h = P()
+        _check(lib.dlr_dense_from_dataset(ds.handle, C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def from_array(cls, X: np.ndarray, label) -> "DenseDataset":
+        X = np.ascontiguousarray(X, dtype=np.float32)
+        y = np.ascontiguousarray(label, dtype=np.int32)
+        h = P()
+        _check(lib.dlr_dense_from_array(X.shape[0], X.shape[1], _ptr(X), _ptr(y), C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def generate(cls, n_rows: int, num_feature_dim: int, *, seed: int = 10, stream: int = 0,
+                 positive_frac: float = 0.3, label_noise: float = 0.05, nthreads: int = 0) -> "DenseDataset":
+        spec = DenseSpec(n_rows, num_feature_dim, seed, stream, positive_frac, label_noise, nthreads, 0)
+        h = P()
+        _check(lib.dlr_dense_generate(C.byref(spec), C.byref(h)))
+        return cls(h)
+
+    def info(self) -> Tuple[int, int]:
+        n, d = i64(), i64()
+        _check(lib.dlr_dense_info(self._h, C.byref(n), C.byref(d)))
+        return n.value, d.value
+
+    def arrays(self):
+        """(X, label) numpy views (valid while this object lives)."""
+        n, d = self.info()
+        xp, yp = P(), P()
+        _check(lib.dlr_dense_view(self._h, C.byref(xp), C.byref(yp)))
+        X = np.ctypeslib.as_array(C.cast(xp, C.POINTER(C.c_float)), shape=(n * d,)).reshape(n, d) if n else \
+            np.zeros((0, d), np.float32)
+        y = np.ctypeslib.as_array(C.cast(yp, C.POINTER(C.c_int32)), shape=(n,)) if n else np.zeros(0, np.int32)
+        return X, y
+
+    def free(self):
+        if self._h:
+            lib.dlr_dense_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 def num_batches(n_rows: int, batch_size: int) -> int:
     return lib.dlr_num_batches(n_rows, batch_size)
 
@@ -325,6 +408,14 @@ class Engine:
 
     def load_test(self, ds: Dataset) -> None:
         self._c(lib.dlr_load_test(self._h, ds.handle))
+
+    def load_train_dense(self, ds: DenseDataset, batch_size: int) -> int:
+        nb = i64()
+        self._c(lib.dlr_load_train_dense(self._h, ds.handle, batch_size, C.byref(nb)))
+        return nb.value
+
+    def load_test_dense(self, ds: DenseDataset) -> None:
+        self._c(lib.dlr_load_test_dense(self._h, ds.handle))
 
     def train_step(self, batch: int, lr: float, C_: float = 1.0, mode: int = MODE_SYNC_MEAN) -> None:
         self._c(lib.dlr_train_step(self._h, batch, lr, C_, mode))

@@ -41,6 +41,7 @@ extern "C" {
 #define DLR_MODE_ASYNC 2      /* main.cc:79-84 per push, pushes applied in rank order           */
 
 typedef struct dlr_dataset dlr_dataset; /* host CSR shard (DataIter's storage) */
+typedef struct dlr_dense dlr_dense;     /* host dense shard (DataIter's own N x D layout) */
 typedef struct dlr_ctx dlr_ctx;         /* one GPU engine context (one rank)   */
 
 /* ------------------------------------------------------------------ */
@@ -118,6 +119,30 @@ int dlr_dataset_view(const dlr_dataset *ds, const int64_t **row_ptr, const int32
                      const int32_t **label);
 void dlr_dataset_free(dlr_dataset *ds);
 
+/* Dense shards (BASELINE C4: wide dense inputs; also the reference's own
+ * representation, data_iter.h:28).  Row-major N x D fp32 + 0/1 labels. */
+/* Densifies a CSR dataset (what DataIter does per line, data_iter.h:28-31). */
+int dlr_dense_from_dataset(const dlr_dataset *ds, dlr_dense **out);
+/* Copies caller arrays X[n_rows * D] (row-major) and label[n_rows]. */
+int dlr_dense_from_array(int64_t n_rows, int64_t num_feature_dim, const float *X, const int32_t *label,
+                         dlr_dense **out);
+/* Seeded dense rows: every feature a 4-decimal value in (0,1] (ToFloat of
+ * its text, like dlr_dataset_generate's value_mode 1), planted-model labels. */
+typedef struct dlr_dense_spec {
+    int64_t n_rows;
+    int64_t num_feature_dim;
+    uint64_t seed;
+    uint64_t stream;
+    double positive_frac;
+    double label_noise;
+    int32_t nthreads;       /* <= 0: default */
+    int32_t reserved;
+} dlr_dense_spec;
+int dlr_dense_generate(const dlr_dense_spec *spec, dlr_dense **out);
+int dlr_dense_info(const dlr_dense *ds, int64_t *n_rows, int64_t *num_feature_dim);
+int dlr_dense_view(const dlr_dense *ds, const float **X, const int32_t **label);
+void dlr_dense_free(dlr_dense *ds);
+
 /* replaces DataIter::NextBatch/HasNext batching -- include/data_iter.h:40-59:
  * ceil(N/B) batches per epoch (B < 0 means N); batch b holds rows
  * (b*B + i) mod N, i in [0,B) (the last batch wraps to row 0). */
@@ -175,6 +200,14 @@ int dlr_get_weights(dlr_ctx *ctx, float *w, int64_t num_feature_dim);
 int dlr_load_train(dlr_ctx *ctx, const dlr_dataset *ds, int64_t batch_size, int64_t *n_batches);
 /* Test shard (LR::Test's NextBatch(-1), lr.cc:49). */
 int dlr_load_test(dlr_ctx *ctx, const dlr_dataset *ds);
+/* The dense counterparts (K6: GEMV-shaped margin and gradient kernels,
+ * HBM-bound, off MFMA).  The gradient is the reference's per-column
+ * sequential sum when batch rows x D <= 2^24, else a blocked sum (per-column
+ * sequential over 256-row chunks, chunk partials added in order:
+ * deterministic, within the north-star tolerance); DLR_DENSE_GRAD=seq|blocked
+ * forces one. */
+int dlr_load_train_dense(dlr_ctx *ctx, const dlr_dense *ds, int64_t batch_size, int64_t *n_batches);
+int dlr_load_test_dense(dlr_ctx *ctx, const dlr_dense *ds);
 
 /* One step of LR::Train's loop body (lr.cc:30-43) plus the server update
  * (main.cc:57-84) for batch `batch` of the loaded shard: margin + sigmoid +

@@ -27,16 +27,29 @@ class EngineRun:
 
 def run_engine(shards: Sequence[dlr.Dataset], D: int, num_iteration: int, batch_size: int, learning_rate: float,
                test: Optional[dlr.Dataset] = None, test_interval: int = 10, mode: int = dlr.MODE_SYNC_MEAN,
-               C_: float = 1.0, random_state: int = 0) -> EngineRun:
+               C_: float = 1.0, random_state: int = 0, dense: bool = False) -> EngineRun:
+    """dense=True: the shards go through the dense path (K6, DataIter's own
+    N x D layout) instead of the sparse one."""
     W = len(shards)
     w0 = dlr.init_weight(D, random_state)
+    if dense:
+        shards = [s if isinstance(s, dlr.DenseDataset) else dlr.DenseDataset.from_dataset(s) for s in shards]
+        if test is not None and not isinstance(test, dlr.DenseDataset):
+            test = dlr.DenseDataset.from_dataset(test)
+
+    def load_train(eng, ds):
+        return eng.load_train_dense(ds, batch_size) if dense else eng.load_train(ds, batch_size)
+
+    def load_test(eng, ds):
+        return eng.load_test_dense(ds) if dense else eng.load_test(ds)
+
     if W == 1:
         eng = dlr.Engine(D)
         try:
             eng.set_weights(w0)
-            nb = eng.load_train(shards[0], batch_size)
+            nb = load_train(eng, shards[0])
             if test is not None:
-                eng.load_test(test)
+                load_test(eng, test)
             pulled = w0.copy()
             res = EngineRun(w=w0, pulled=[pulled])
             for it in range(num_iteration):
@@ -58,10 +71,10 @@ def run_engine(shards: Sequence[dlr.Dataset], D: int, num_iteration: int, batch_
     server = dlr.Engine(D)
     try:
         server.set_weights(w0)
-        nbs = [wk.load_train(s, batch_size) for wk, s in zip(workers, shards)]
+        nbs = [load_train(wk, s) for wk, s in zip(workers, shards)]
         assert len(set(nbs)) == 1
         if test is not None:
-            server.load_test(test)
+            load_test(server, test)
         pulled = [w0.copy() for _ in range(W)]
         res = EngineRun(w=w0, pulled=pulled)
         for it in range(num_iteration):

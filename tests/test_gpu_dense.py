@@ -1,0 +1,137 @@
+"""GPU parity of the dense path (K6; BASELINE C4, and the reference's own
+dense DataIter layout).  The per-column sequential gradient is the
+reference's order -> bitwise; the blocked gradient (default for big
+batches) is deterministic and within the north-star bar
+|a-b| <= 1e-5*|b| + 1e-7 of the oracle."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+import distlr_amd as dlr
+import oracle
+from conftest import GOLDEN, read_golden_json
+from engine_driver import run_engine
+from test_gpu_parity import assert_same_weights, compare_runs
+
+pytestmark = pytest.mark.gpu
+
+
+def dense_shard(dd: dlr.DenseDataset):
+    X, y = dd.arrays()
+    return X, y
+
+
+def within_bar(got, want):
+    a, b = np.asarray(got, np.float64), np.asarray(want, np.float64)
+    excess = np.abs(a - b) - (1e-5 * np.abs(b) + 1e-7)
+    assert excess.max() <= 0, f"max excess {excess.max():.3g}"
+
+
+@pytest.mark.parametrize("name", ["c1_W1_Bfull_mean", "c1_W1_B7_mean", "c1_W2_Bfull_mean", "c1_W2_B64_async",
+                                  "real_W2_B50_mean", "real_W1_B33_mean"])
+def test_golden_trajectories_dense(name):
+    # the golden C1 shards densified (data_iter.h:28) -> the same bits
+    meta = read_golden_json("trajectories.json")[name]
+    base = os.path.join(GOLDEN, meta["dataset"])
+    D = meta["D"]
+    shards = [dlr.Dataset.load_libsvm(os.path.join(base, "train", f"part-00{p + 1}"), D)
+              for p in range(meta["workers"])]
+    test = dlr.Dataset.load_libsvm(os.path.join(base, "test", "part-001"), D)
+    res = run_engine(shards, D, meta["num_iteration"], meta["batch_size"], meta["learning_rate"], test=test,
+                     test_interval=meta["test_interval"], mode=meta["mode"], dense=True)
+    assert res.w.astype("<f4").tobytes().hex() == meta["w"]
+    assert [p.astype("<f4").tobytes().hex() for p in res.pulled] == meta["pulled"]
+    lines = [f"Iteration {it}, accuracy: {oracle.format_g(oracle.accuracy(c, n))}" for it, c, n, _ in res.tests]
+    assert lines == meta["accuracy_lines"]
+
+
+@pytest.mark.parametrize("D", [123, 256])
+@pytest.mark.parametrize("B", [1, 7, 1001, 2500, -1])
+def test_dense_batch_sizes_bitwise(D, B):
+    # D=123: scalar loads; D=256: 16-byte loads.  B=2500 > N wraps twice.
+    dd = dlr.DenseDataset.generate(1000, D, seed=5, stream=1)
+    test = dlr.DenseDataset.generate(777, D, seed=5, stream=2)
+    eng = run_engine([dd], D, 2, B, 0.05, test=test, test_interval=1, dense=True)
+    orc = oracle.run_worker([dense_shard(dd)], D, 2, B, 0.05, test=dense_shard(test), test_interval=1, sparse=False)
+    compare_runs(eng, orc)
+
+
+def test_dense_forced_collectives(monkeypatch):
+    monkeypatch.setenv("DLR_FORCE_COLLECTIVES", "1")
+    D = 256
+    dd = dlr.DenseDataset.generate(600, D, seed=6, stream=1)
+    eng = run_engine([dd], D, 2, 100, 0.05, dense=True)
+    orc = oracle.run_worker([dense_shard(dd)], D, 2, 100, 0.05, sparse=False)
+    compare_runs(eng, orc)
+
+
+@pytest.mark.parametrize("W", [1, 2])
+def test_dense_blocked_gradient_within_bar(monkeypatch, W):
+    monkeypatch.setenv("DLR_DENSE_GRAD", "blocked")
+    D = 512
+    shards = [dlr.DenseDataset.generate(3000, D, seed=7, stream=r + 1) for r in range(W)]
+    eng = run_engine(shards, D, 3, 1500, 0.05, dense=True)
+    orc = oracle.run_worker([dense_shard(s) for s in shards], D, 3, 1500, 0.05, sparse=False)
+    within_bar(eng.w, orc.w)
+    eng2 = run_engine(shards, D, 3, 1500, 0.05, dense=True)
+    assert_same_weights(eng2.w, eng.w)
+
+
+def test_c4_shape_dense_steps():
+    # BASELINE C4: 4,096 dense features, B = 65,536 (blocked gradient by
+    # default at this size); rows reduced to two batches.
+    # At this size the reference's own sequential fp32 gradient is ~1.4e-5
+    # (relative) from exact arithmetic and moves a weight by ~3e-7 per step
+    # (measured: see DESIGN.md "Dense"), so no reordered sum can match it to
+    # a 1e-7 absolute floor.  The bar here: the engine's pushed gradient is at
+    # least as close to the fp64-exact gradient as the reference's, and the
+    # weights stay within 1e-5 relative + 1e-6 absolute of the reference.
+    D, B = 4096, 65536
+    dd = dlr.DenseDataset.generate(2 * B, D, seed=10, stream=1)
+    X, y = dd.arrays()
+    w0 = dlr.init_weight(D)
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(w0)
+        assert eng.load_train_dense(dd, B) == 2
+        rows = oracle.batch_rows(len(y), B, 0)
+        g_eng = eng.worker_gradient(0, 1.0).astype(np.float64)
+        g_ref = oracle.grad_dense(X, y, rows, w0).astype(np.float64)
+        # fp64-exact gradient from the reference's own fp32 residuals
+        z = np.zeros(B, np.float32)
+        Xb = X[rows]
+        for j in range(D):
+            z = (z + (w0[j] * Xb[:, j]).astype(np.float32)).astype(np.float32)
+        r = ((1.0 / (1.0 + np.exp(-z.astype(np.float64)))).astype(np.float32) - y[rows].astype(np.float32))
+        G64 = (r[:, None].astype(np.float32) * Xb).astype(np.float32).astype(np.float64).sum(0)
+        g64 = G64 / B + ((np.float32(1.0) * w0) / np.float32(B)).astype(np.float64)
+        assert np.max(np.abs(g_eng - g64)) <= np.max(np.abs(g_ref - g64))
+        w = w0.copy()
+        for b in range(3):
+            eng.train_step(b % 2, 0.05, 1.0)
+            g = oracle.grad_dense(X, y, oracle.batch_rows(len(y), B, b % 2), w)
+            oracle.server_update(w, [g], 0.05)
+        a, bb = eng.get_weights().astype(np.float64), w.astype(np.float64)
+        assert np.all(np.abs(a - bb) <= 1e-5 * np.abs(bb) + 1e-6)
+    finally:
+        eng.close()
+
+
+def test_dense_predict_counts_and_logloss():
+    D = 1024
+    test = dlr.DenseDataset.generate(20001, D, seed=9, stream=3)
+    eng = dlr.Engine(D)
+    try:
+        w = (dlr.init_weight(D) - np.float32(0.5)).astype(np.float32)
+        eng.set_weights(w)
+        eng.load_test_dense(test)
+        c, n, ll = eng.predict()
+        X, y = test.arrays()
+        c2, ll2 = oracle.predict_dense(X, y, w)
+        assert (c, n) == (c2, 20001)
+        assert abs(ll - ll2) <= 1e-9 * abs(ll2)
+    finally:
+        eng.close()
