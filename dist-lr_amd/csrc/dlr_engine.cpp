@@ -356,8 +356,8 @@ void build_csc(const dlr_dataset &ds, const std::vector<dlr::BatchSpan> &plan, i
                 L.cseg.push_back((uint32_t)L.sptr.size());
                 L.sptr.push_back(lat);
                 if (any_long) {
-                    L.row.assign((size_t)lat + 16, 0);
-                    L.val.assign((size_t)lat + 16, 0.0f);
+                    L.row.assign((size_t)lat + dlr::kLongChunk, 0);
+                    L.val.assign((size_t)lat + dlr::kLongChunk, 0.0f);
                 }
                 // cursors: short columns in the classic copy, long ones in L
                 for (int64_t j = 0; j < D; ++j)
@@ -885,8 +885,8 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             if ((r = upload(c, &t.lcols, cols.data(), cols.size()))) return r;
             if ((r = upload(c, &t.lcseg, cseg.data(), cseg.size()))) return r;
             if ((r = upload(c, &t.lsptr, sptr.data(), sptr.size()))) return r;
-            if ((r = upload(c, (RowT **)&t.lrow, row.data(), row.size(), 16))) return r;
-            if ((r = upload(c, &t.lval, val.data(), val.size(), 16))) return r;
+            if ((r = upload(c, (RowT **)&t.lrow, row.data(), row.size(), dlr::kLongChunk))) return r;
+            if ((r = upload(c, &t.lval, val.data(), val.size(), dlr::kLongChunk))) return r;
             if ((r = dev_alloc(c, (void **)&t.lpart, (size_t)maxseg * 4))) return r;
             lbytes = (int64_t)(cols.size() * 4 + cseg.size() * 4 + sptr.size() * 4 + row.size() * sizeof(RowT) +
                                val.size() * 4);

@@ -31,8 +31,9 @@ struct DevCsc {
 // Long columns of one batch (classic layout): ncols columns cols[] (their
 // ptr entries in DevCsc carry bit 31), column l's chunks are segments
 // [cseg[l], cseg[l+1]); segment s spans entries [sptr[s], sptr[s+1]) of
-// row/val (4-aligned starts; at most kLongChunk entries).
-constexpr int kLongChunk = 512;
+// row/val (4-aligned starts; at most kLongChunk entries + 3 padding; the
+// arrays are padded by kLongChunk entries).
+constexpr int kLongChunk = 256;
 struct DevLong {
     const uint32_t *cols;
     const uint32_t *cseg;

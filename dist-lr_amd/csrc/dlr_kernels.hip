@@ -67,9 +67,6 @@ struct Vec4<uint16_t> {
     using type = ushort4;
 };
 
-// Sum over this lane's segment [a, b) of fl32(table[idx[k]] * val[k]), in
-// k order.  The wave's entries are [e0, e1).  lds: kWin floats of this wave.
-// Only lanes < SEG own a segment; all 64 lanes load and gather.
 // Non-temporal 16-byte loads for once-read streams: the streamed lines do
 // not displace the gathered table (w) from L2 (tools/kbench, cold 10M-row
 // shard: margin 22.9 -> 20.8 us).
@@ -89,6 +86,9 @@ __device__ __forceinline__ V load_stream(const V *p) {
     return out;
 }
 
+// Sum over this lane's segment [a, b) of fl32(table[idx[k]] * val[k]), in
+// k order.  The wave's entries are [e0, e1).  lds: kWin floats of this wave.
+// Only lanes < SEG own a segment; all 64 lanes load and gather.
 template <typename IdxT>
 __device__ __forceinline__ float ordered_segment_dot(int64_t e0, int64_t e1, int64_t a, int64_t b, int lane,
                                                      const IdxT *__restrict__ idx, const float *__restrict__ val,
@@ -292,48 +292,62 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad(DevCsc cs, const RowT *_
 // then k_long_combine adds the chunk partials in chunk order.  Deterministic
 // (fixed chunking), but for these columns not the reference's single
 // sequential sum -- DLR_LONG_COLUMN=0 keeps every column bitwise.
-constexpr int kLongU = 16;  // entries in flight per lane
+//
+// One wave per chunk of kLongChunk = 256 entries: entry-parallel 16-byte
+// loads (a hot column's rows ascend, so neighbouring lanes' residual
+// gathers hit neighbouring lines), each lane adds its 4 products in order,
+// the wave adds the 64 lane sums with a fixed xor-shuffle tree (fp add is
+// commutative: every lane gets the same bits).  Fixed chunks + fixed tree:
+// deterministic, more accurate than one fp32 chain.  (A lane-per-chunk
+// sequential version took 5.35 ms on the C3 shard: each lane streamed its
+// own region and the rows' locality was lost.)
 
 template <typename RowT>
 __global__ __launch_bounds__(256) void k_long_segments(const uint32_t *__restrict__ sptr, int64_t nseg,
                                                        const RowT *__restrict__ row, const float *__restrict__ val,
                                                        const float *__restrict__ resid, float *__restrict__ part) {
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nseg) return;
-    const uint32_t a = sptr[s], b = sptr[s + 1];  // a is 4-aligned
-    float acc = 0.0f;
-    for (uint32_t k = a; k < b; k += kLongU) {
-        RowT r[kLongU];
-        float v[kLongU];
+    using RV = typename Vec4<RowT>::type;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t wpb = blockDim.x / kWave;
+    const int64_t nw = (int64_t)gridDim.x * wpb;
+    for (int64_t s = (int64_t)blockIdx.x * wpb + threadIdx.x / kWave; s < nseg; s += nw) {  // wave-uniform
+        const uint32_t a = sptr[s], b = sptr[s + 1];  // a 4-aligned; b - a <= kLongChunk (+3 padding)
+        const uint32_t e = a + (uint32_t)lane * 4;      // arrays padded by kLongChunk entries
+        const RV r4 = *reinterpret_cast<const RV *>(row + e);
+        const float4 v4 = *reinterpret_cast<const float4 *>(val + e);
+        float x0 = 0.0f, x1 = 0.0f, x2 = 0.0f, x3 = 0.0f;
+        if (e < b) x0 = resid[r4.x] * v4.x;
+        if (e + 1 < b) x1 = resid[r4.y] * v4.y;
+        if (e + 2 < b) x2 = resid[r4.z] * v4.z;
+        if (e + 3 < b) x3 = resid[r4.w] * v4.w;
+        float t = x0 + x1;
+        t = t + x2;
+        t = t + x3;
 #pragma unroll
-        for (int u = 0; u < kLongU; u += 4) {
-            const typename Vec4<RowT>::type r4 = *reinterpret_cast<const typename Vec4<RowT>::type *>(row + k + u);
-            const float4 v4 = *reinterpret_cast<const float4 *>(val + k + u);
-            r[u] = r4.x, r[u + 1] = r4.y, r[u + 2] = r4.z, r[u + 3] = r4.w;
-            v[u] = v4.x, v[u + 1] = v4.y, v[u + 2] = v4.z, v[u + 3] = v4.w;
-        }
-        float x[kLongU];
-#pragma unroll
-        for (int u = 0; u < kLongU; ++u) x[u] = (k + u < b) ? resid[r[u]] * v[u] : 0.0f;
-#pragma unroll
-        for (int u = 0; u < kLongU; ++u)
-            if (k + u < b) acc = acc + x[u];
+        for (int off = 32; off > 0; off >>= 1) t = t + __shfl_xor(t, off);
+        if (lane == 0) part[s] = t;
     }
-    part[s] = acc;
 }
 
-// One long column per thread: G = chunk partials summed in chunk order,
-// then lr.cc:40 and the update (FUSED) or the pushed gradient.
+// One long column per wave: lane l adds chunk partials l, l+64, ... in
+// order, the wave adds the 64 lane sums with the fixed xor-shuffle tree
+// (deterministic); then lr.cc:40 and the update (FUSED) or the pushed
+// gradient.
 template <bool FUSED>
 __global__ __launch_bounds__(256) void k_long_combine(const uint32_t *__restrict__ cols,
                                                       const uint32_t *__restrict__ cseg, int64_t ncols,
                                                       const float *__restrict__ part, float *__restrict__ w,
                                                       float *__restrict__ gout, float Bf, double Bd, float lr,
                                                       float C) {
-    const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (l >= ncols) return;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t l = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+    if (l >= ncols) return;  // wave-uniform
+    const uint32_t s0 = cseg[l], s1 = cseg[l + 1];
     float G = 0.0f;
-    for (uint32_t s = cseg[l]; s < cseg[l + 1]; ++s) G = G + part[s];
+    for (uint32_t s = s0 + (uint32_t)lane; s < s1; s += kWave) G = G + part[s];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) G = G + __shfl_xor(G, off);
+    if (lane != 0) return;
     const uint32_t j = cols[l];
     const float wj = w[j];
     const float cw = C * wj;
@@ -1089,20 +1103,22 @@ hipError_t launch_sparse_merge(const uint32_t *lists, int64_t cap, int64_t strid
 hipError_t launch_grad_long(const DevLong &lg, int64_t B, const float *resid, float *w, float *gout, float *part,
                             float lr, float C, bool fused, hipStream_t s) {
     if (lg.ncols <= 0) return hipSuccess;
+    const unsigned sgrid = (unsigned)std::min<int64_t>((lg.nseg + 3) / 4, 256 * 16);  // a wave per chunk
     if (lg.row16)
-        hipLaunchKernelGGL(k_long_segments<uint16_t>, dim3(grid_for(lg.nseg, 256)), dim3(256), 0, s, lg.sptr, lg.nseg,
+        hipLaunchKernelGGL(k_long_segments<uint16_t>, dim3(sgrid), dim3(256), 0, s, lg.sptr, lg.nseg,
                            static_cast<const uint16_t *>(lg.row), lg.val, resid, part);
     else
-        hipLaunchKernelGGL(k_long_segments<uint32_t>, dim3(grid_for(lg.nseg, 256)), dim3(256), 0, s, lg.sptr, lg.nseg,
+        hipLaunchKernelGGL(k_long_segments<uint32_t>, dim3(sgrid), dim3(256), 0, s, lg.sptr, lg.nseg,
                            static_cast<const uint32_t *>(lg.row), lg.val, resid, part);
     const float Bf = (float)B;
     const double Bd = (double)B;
+    const unsigned cgrid = grid_for(lg.ncols, 4);  // a wave per long column
     if (fused)
-        hipLaunchKernelGGL(k_long_combine<true>, dim3(grid_for(lg.ncols, 256)), dim3(256), 0, s, lg.cols, lg.cseg,
-                           lg.ncols, part, w, gout, Bf, Bd, lr, C);
+        hipLaunchKernelGGL(k_long_combine<true>, dim3(cgrid), dim3(256), 0, s, lg.cols, lg.cseg, lg.ncols, part, w,
+                           gout, Bf, Bd, lr, C);
     else
-        hipLaunchKernelGGL(k_long_combine<false>, dim3(grid_for(lg.ncols, 256)), dim3(256), 0, s, lg.cols, lg.cseg,
-                           lg.ncols, part, w, gout, Bf, Bd, lr, C);
+        hipLaunchKernelGGL(k_long_combine<false>, dim3(cgrid), dim3(256), 0, s, lg.cols, lg.cseg, lg.ncols, part, w,
+                           gout, Bf, Bd, lr, C);
     return hipGetLastError();
 }
 

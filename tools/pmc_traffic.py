@@ -47,6 +47,7 @@ def main() -> int:
     ap.add_argument("pmc_dir")
     ap.add_argument("--out", default=None)
     ap.add_argument("--workload-key", default="D1000000_nnz50_B65536")
+    ap.add_argument("--layout", default="lds", help="gradient layout the passes ran with (bench.py reports it)")
     args = ap.parse_args()
     d = args.pmc_dir
     # calibration: mb_stream reads 25 MiB and writes n4*4 bytes per launch
@@ -56,7 +57,9 @@ def main() -> int:
     cw = pick(per_kernel(os.path.join(d, "calib_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE"), "mb_stream")
     read_factor = win / (statistics.median(cf) * 1024.0)
     write_factor = (n4 * 4) / (statistics.median(cw) * 1024.0)
-    res = {"workload_key": args.workload_key,
+    res = {"workload_key": args.workload_key, "layout": args.layout,
+           "note": "L2-to-fabric bytes (FETCH_SIZE corrected by the calibration factor, WRITE_SIZE); Infinity-Cache "
+                   "hits are counted, so gathered tables resident in MALL show here",
            "calibration": {"kernel": "kbench mb_stream, cold 25 MiB windows, 16-B loads per lane",
                            "read_bytes_true": win, "FETCH_SIZE_kB_median": statistics.median(cf),
                            "read_factor": round(read_factor, 4), "write_bytes_true": n4 * 4,

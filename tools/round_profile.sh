@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round measurement session (one GPU box): GPU parity suite, smoke, C2 bench,
+# rocprofv3 kernel-trace summaries of every config, PMC traffic passes for C2.
+# Every GPU step has its own time limit; steps are chained with &&.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$(pwd); export TMPDIR=/tmp; mkdir -p gpurun_out/rp
+echo "== pytest -m gpu"
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
+    > gpurun_out/rp/pytest_gpu.log 2>&1 && tail -2 gpurun_out/rp/pytest_gpu.log && \
+echo "== smoke" && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" && \
+echo "== bench c2" && timeout -k 10 400 python -u bench.py > gpurun_out/rp/bench_c2.json 2> gpurun_out/rp/bench_c2.err && \
+tail -c 400 gpurun_out/rp/bench_c2.json && echo && \
+for cfg in c2 c3 c4 c5; do
+  echo "== rocprofv3 $cfg" && ( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
+      -d "$R/gpurun_out/rp/prof_$cfg" -o run -- python3 "$R/bench.py" --config $cfg --no-cpu-baseline \
+      > "$R/gpurun_out/rp/prof_$cfg.json" 2> "$R/gpurun_out/rp/prof_$cfg.err" ) || exit 1
+done && \
+echo "== pmc" && bash tools/pmc_pass.sh > gpurun_out/rp/pmc_pass.log 2>&1 && echo "round profile done"
