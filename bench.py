@@ -207,18 +207,28 @@ def main():
 
     # Pass 1 (the throughput): no per-kernel events in the launch stream.
     el = timed(args.warmup, False)
-    # Pass 2: the same K steps with a HIP-event pair around every kernel on
-    # the engine's stream -> per-kernel average durations for the roofline.
+    # Pass 2: the same K steps with a HIP-event pair around every launch on
+    # the engine's stream -> the step breakdown (exchange included, N>1).
     el_instr = timed(args.warmup + args.steps, True)
     kt = {name: eng.kernel_time(i) for name, i in
           [("margin", dlr.TIMER_MARGIN), ("grad_update", dlr.TIMER_GRAD), ("merge", dlr.TIMER_UPDATE),
            ("exchange", dlr.TIMER_EXCHANGE), ("step", dlr.TIMER_STEP)]}
     eng.timing(False)
+    # Pass 3 (the roofline): each kernel stage over K consecutive batches
+    # between ONE event pair (no per-launch event overhead, comparable with
+    # rocprofv3's kernel durations).  Runs after the measured passes: the
+    # stages run without their partners and change the weights.
+    k0 = args.warmup + 2 * args.steps
+    stage_us = {"margin": eng.stage_time(dlr.STAGE_MARGIN, k0 % nb, args.steps, args.lr) * 1000.0,
+                "gradient": eng.stage_time(dlr.STAGE_GRADIENT, k0 % nb, args.steps, args.lr) * 1000.0}
+    if layout == "touched":
+        stage_us["update"] = eng.stage_time(dlr.STAGE_UPDATE, k0 % nb, args.steps, args.lr) * 1000.0
     B_eff = B if B > 0 else args.rows                 # B = -1: the full shard per step
     samples = world * args.steps * B_eff
     value = samples / el
     avg_us = {k: (ms / n * 1000.0 if n else 0.0) for k, (ms, n) in kt.items()}
-    kern_us = avg_us["margin"] + avg_us["grad_update"] + avg_us["merge"]
+    # the step's kernels: stage averages, plus the key-range merge (N>1)
+    kern_us = sum(stage_us.values()) + (avg_us["merge"] if world > 1 and layout != "touched" else 0.0)
     step_bytes = alg_bytes_per_step(B_eff, nnz_avg, D, args.kind == "dense")
     achieved = step_bytes / (kern_us * 1e-6) / 1e9 if kern_us > 0 else 0.0
     traffic = None
@@ -269,9 +279,12 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "alg_bytes_per_step": step_bytes,
-                "kernel_avg_us": {k: round(v, 3) for k, v in avg_us.items()},
-                "timing": "kernel averages from a second pass of the same K steps with HIP events on the "
-                          "engine stream; value from the first, un-instrumented pass",
+                "kernel_avg_us": {k: round(v, 3) for k, v in stage_us.items()},
+                "step_breakdown_us": {k: round(v, 3) for k, v in avg_us.items()},
+                "timing": "value: K un-instrumented steps; kernel_avg_us: each kernel stage over K consecutive "
+                          "batches between one HIP-event pair on the engine stream (achieved = alg bytes / their "
+                          "sum); step_breakdown_us: a pass of K steps with an event pair around every launch "
+                          "(includes the exchange when N>1; event overhead ~2 us per launch)",
                 "instrumented_ms_per_step": round(el_instr / args.steps * 1000.0, 5),
             },
             "cpu_baseline": cpu,

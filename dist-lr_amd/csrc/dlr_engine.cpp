@@ -1197,6 +1197,52 @@ int dlr_kernel_time(dlr_ctx *c, int which, double *total_ms, int64_t *launches) 
     return DLR_OK;
 }
 
+int dlr_stage_time(dlr_ctx *c, int stage, int64_t first, int64_t count, float lr, float C, double *avg_ms) {
+    if (!c || count <= 0 || stage < 0 || stage > 2) return fail(c, DLR_E_ARG, "dlr_stage_time: bad argument");
+    if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_stage_time: no training shard loaded");
+    const TrainShard &t = c->train;
+    if (stage == DLR_STAGE_UPDATE && !t.touched)
+        return fail(c, DLR_E_ARG, "dlr_stage_time: the update stage is separate only in the touched layout");
+    HIPC(c, hipSetDevice(c->device));
+    harvest(c);
+    const bool was = c->timing;
+    c->timing = false;
+    hipEvent_t a, b;
+    HIPC(c, hipEventCreate(&a));
+    HIPC(c, hipEventCreate(&b));
+    const int64_t nb = (int64_t)t.plan.size();
+    hipError_t e = hipEventRecord(a, c->stream);
+    for (int64_t k = 0; k < count && e == hipSuccess; ++k) {
+        const int64_t bb = (first + k) % nb;
+        const int64_t rows = t.plan[(size_t)bb].rows;
+        if (stage == DLR_STAGE_MARGIN) {
+            e = launch_margin(c, bb);
+        } else if (t.touched) {
+            const int64_t n = t.tncols[(size_t)bb];
+            const uint32_t *cols = t.tcols + t.tcoff[(size_t)bb];
+            if (stage == DLR_STAGE_GRADIENT)
+                e = dlr::launch_grad_touched(csc_view(c, bb), cols, n, c->resid, c->w, c->newv, rows, lr, C, true,
+                                             c->stream);
+            else {
+                e = dlr::launch_dense_l2(c->w, c->D, c->rs, lr, C, 0, c->stream);
+                if (e == hipSuccess) e = dlr::launch_scatter(c->w, cols, c->newv, n, c->stream);
+            }
+        } else {
+            e = launch_gradient(c, bb, rows, c->comm ? c->g : nullptr, lr, C, !c->comm);
+        }
+    }
+    if (e == hipSuccess) e = hipEventRecord(b, c->stream);
+    if (e == hipSuccess) e = hipEventSynchronize(b);
+    float ms = 0;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, a, b);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    c->timing = was;
+    if (e != hipSuccess) return fail(c, DLR_E_HIP, std::string("dlr_stage_time: ") + hipGetErrorString(e));
+    if (avg_ms) *avg_ms = (double)ms / (double)count;
+    return DLR_OK;
+}
+
 int dlr_train_layout(dlr_ctx *c) {
     if (!c) return DLR_E_ARG;
     if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_layout: no training shard loaded");

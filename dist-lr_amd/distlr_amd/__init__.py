@@ -23,6 +23,7 @@ MODE_SYNC_LAST = 1
 MODE_ASYNC = 2
 UNIQUE_ID_BYTES = 128
 LAYOUT_CLASSIC, LAYOUT_LDS, LAYOUT_TOUCHED = 0, 1, 2
+STAGE_MARGIN, STAGE_GRADIENT, STAGE_UPDATE = 0, 1, 2
 
 # Exported symbols, in include/distlr_amd.h order (tests check the .so
 # exports every one of them).
@@ -38,7 +39,7 @@ SYMBOLS = [
     "dlr_set_weights", "dlr_get_weights", "dlr_load_train", "dlr_load_test", "dlr_load_train_dense",
     "dlr_load_test_dense",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
-    "dlr_timing", "dlr_kernel_time", "dlr_train_layout", "dlr_memory_info",
+    "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_memory_info",
 ]
 
 if not os.path.exists(LIB_PATH):
@@ -139,6 +140,7 @@ _sig("dlr_predict", C.c_int, P, C.POINTER(i64), C.POINTER(i64), C.POINTER(C.c_do
 _sig("dlr_sync", C.c_int, P)
 _sig("dlr_timing", C.c_int, P, C.c_int)
 _sig("dlr_kernel_time", C.c_int, P, C.c_int, C.POINTER(C.c_double), C.POINTER(i64))
+_sig("dlr_stage_time", C.c_int, P, C.c_int, i64, i64, C.c_float, C.c_float, C.POINTER(C.c_double))
 _sig("dlr_train_layout", C.c_int, P)
 _sig("dlr_memory_info", C.c_int, P, C.POINTER(i64), C.POINTER(i64))
 
@@ -448,6 +450,13 @@ class Engine:
         ms, n = C.c_double(), i64()
         self._c(lib.dlr_kernel_time(self._h, which, C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+    def stage_time(self, stage: int, first_batch: int, count: int, lr: float = 0.2, C_: float = 1.0) -> float:
+        """Average ms of one kernel stage over `count` consecutive launches
+        between one event pair (dlr_stage_time)."""
+        ms = C.c_double()
+        self._c(lib.dlr_stage_time(self._h, stage, first_batch, count, lr, C_, C.byref(ms)))
+        return ms.value
 
     def train_layout(self) -> int:
         """LAYOUT_CLASSIC / LAYOUT_LDS / LAYOUT_TOUCHED of the loaded shard."""

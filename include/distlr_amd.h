@@ -244,6 +244,21 @@ int dlr_sync(dlr_ctx *ctx);
  * 2 update/merge, 3 exchange, 4 step total) since enabling; syncs first. */
 int dlr_timing(dlr_ctx *ctx, int enable);
 int dlr_kernel_time(dlr_ctx *ctx, int which, double *total_ms, int64_t *launches);
+/* Average duration of ONE kernel stage over `count` consecutive launches on
+ * batches first, first+1, ... (mod the epoch), between a single HIP-event
+ * pair on the context's stream -- the per-launch event overhead of
+ * dlr_timing is gone, so the figure is comparable with rocprofv3's kernel
+ * durations.  stage: DLR_STAGE_MARGIN (K2), DLR_STAGE_GRADIENT (K3 with the
+ * fused single-rank update, or the pushed gradient when world > 1; for the
+ * touched layout the touched-column gradient), DLR_STAGE_UPDATE (the
+ * touched layout's dense L2 pass + scatter).  The stages run without their
+ * partners, so the weights end up changed: use after the measured run.
+ * Blocks. */
+#define DLR_STAGE_MARGIN 0
+#define DLR_STAGE_GRADIENT 1
+#define DLR_STAGE_UPDATE 2
+int dlr_stage_time(dlr_ctx *ctx, int stage, int64_t first_batch, int64_t count, float learning_rate, float C,
+                   double *avg_ms);
 
 /* Column-major layout the loaded training shard uses for the gradient
  * (chosen by dlr_load_train; DLR_GRAD_KERNEL=classic|lds|touched forces

@@ -217,6 +217,92 @@ __global__ __launch_bounds__(256) void k2_lpr(dlr::DevBatch bt, const float *__r
     resid[i] = sig(acc) - y;
 }
 
+// Column-split margin pass: row i's entries in this half are [row_ptr[i],
+// row_ptr[i+1]); the sum continues from zin[i] (pass B) and either stores
+// the partial (pass A) or finishes sigma - y (pass B).
+template <int SEG, bool FIRST, bool LAST>
+__global__ __launch_bounds__(256) void k2_split(dlr::DevBatch bt, const float *__restrict__ w,
+                                                const float *__restrict__ zin, float *__restrict__ out) {
+    __shared__ float s_p[4][1024];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x / 64;
+    const int64_t row0 = ((int64_t)blockIdx.x * 4 + wv) * SEG;
+    if (row0 >= bt.rows) return;
+    const int64_t my = row0 + lane;
+    const bool valid = lane < SEG && my < bt.rows;
+    const int64_t rlast = min(row0 + SEG, bt.rows);
+    const int64_t e0 = bt.row_ptr[row0], e1 = bt.row_ptr[rlast];
+    const int64_t a = valid ? bt.row_ptr[my] : e1, b = valid ? bt.row_ptr[my + 1] : e1;
+    const float z0 = (!FIRST && valid) ? zin[my] : 0.0f;
+    float z = dlr::ordered_segment_dot<int32_t>(e0, e1, a, b, lane, bt.col, bt.val, w, s_p[wv]);
+    // ordered_segment_dot starts from 0: for pass B re-add in order is NOT
+    // the same as continuing -- so pass B below uses osd_from instead.
+    (void)z0;
+    if (valid) out[my] = LAST ? sig(z) - bt.label[my] : z;
+}
+
+// ordered segment dot continuing from acc0 (same as dlr::ordered_segment_dot
+// but with an initial value): the column-split pass B.
+template <int SEG>
+__global__ __launch_bounds__(256) void k2_splitB(dlr::DevBatch bt, const float *__restrict__ w,
+                                                 const float *__restrict__ zin, float *__restrict__ resid) {
+    __shared__ float s_p[4][1024];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x / 64;
+    const int64_t row0 = ((int64_t)blockIdx.x * 4 + wv) * SEG;
+    if (row0 >= bt.rows) return;
+    const int64_t my = row0 + lane;
+    const bool valid = lane < SEG && my < bt.rows;
+    const int64_t rlast = min(row0 + SEG, bt.rows);
+    const int64_t e0 = bt.row_ptr[row0], e1 = bt.row_ptr[rlast];
+    const int64_t a = valid ? bt.row_ptr[my] : e1, b = valid ? bt.row_ptr[my + 1] : e1;
+    float acc = valid ? zin[my] : 0.0f;
+    // same window loop as the production kernel, summing into acc
+    float *lds = s_p[wv];
+    const int64_t base = e0 & ~int64_t(3);
+    for (int64_t ws = base; ws < e1; ws += 1024) {
+        const int64_t left = e1 - ws;
+        int4 iv[4];
+        float4 v[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (t * 256 < left) {
+                const int64_t e = ws + t * 256 + lane * 4;
+                const int64_t ec = e < e1 ? e : ws + t * 256;
+                iv[t] = dlr::load_stream(reinterpret_cast<const int4 *>(bt.col + ec));
+                v[t] = dlr::load_stream(reinterpret_cast<const float4 *>(bt.val + ec));
+            }
+        float g[4][4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (t * 256 < left) {
+                const int64_t e = ws + t * 256 + lane * 4;
+                g[t][0] = w[(e >= e0 && e < e1) ? iv[t].x : 0];
+                g[t][1] = w[(e + 1 >= e0 && e + 1 < e1) ? iv[t].y : 0];
+                g[t][2] = w[(e + 2 >= e0 && e + 2 < e1) ? iv[t].z : 0];
+                g[t][3] = w[(e + 3 >= e0 && e + 3 < e1) ? iv[t].w : 0];
+            }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (t * 256 < left) {
+                const int o = t * 256 + lane * 4;
+                const int64_t e = ws + o;
+                float4 p;
+                p.x = (e >= e0 && e < e1) ? g[t][0] * v[t].x : 0.0f;
+                p.y = (e + 1 >= e0 && e + 1 < e1) ? g[t][1] * v[t].y : 0.0f;
+                p.z = (e + 2 >= e0 && e + 2 < e1) ? g[t][2] * v[t].z : 0.0f;
+                p.w = (e + 3 >= e0 && e + 3 < e1) ? g[t][3] * v[t].w : 0.0f;
+                *reinterpret_cast<float4 *>(lds + o) = p;
+            }
+        dlr::wave_sync();
+        const int64_t lo = a > ws ? a : ws;
+        const int64_t hi = b < ws + 1024 ? b : ws + 1024;
+        for (int o = (int)(lo - ws); o < (int)(hi - ws); ++o) acc = acc + lds[o];
+        dlr::wave_sync();
+    }
+    if (valid) resid[my] = sig(acc) - bt.label[my];
+}
+
 // ---------------- K3 candidates
 // Lane per column: the column's segment read straight (U entries at a time).
 template <int U, bool FUSED>
@@ -842,6 +928,73 @@ int main(int argc, char **argv) {
         printf("K2 ref SEG=%-2d               %8.2f us  %7.1f GB/s\n", seg, t, rate(mb_k2, t));
     }
     hipLaunchKernelGGL(dlr::k_margin_residual<16>, dim3((B + 63) / 64), dim3(256), 0, 0, bt, d_w, d_r);
+    {   // column-split margin (two passes over half-size w tables) vs one pass, cold shard
+        const int64_t NB = 40;
+        // host split of the batch: entries with col < D/2 (A) and >= D/2 (B)
+        std::vector<int64_t> rpA(B + 1), rpB(B + 1);
+        std::vector<int32_t> cA, cB;
+        std::vector<float> vA, vB;
+        for (int64_t i = 0; i < B; ++i) {
+            rpA[i] = (int64_t)cA.size();
+            rpB[i] = (int64_t)cB.size();
+            for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                if (col[k] < D / 2) {
+                    cA.push_back(col[k]);
+                    vA.push_back(val[k]);
+                } else {
+                    cB.push_back(col[k]);
+                    vB.push_back(val[k]);
+                }
+            }
+        }
+        rpA[B] = (int64_t)cA.size();
+        rpB[B] = (int64_t)cB.size();
+        const int64_t EA = (int64_t)cA.size(), EB = (int64_t)cB.size();
+        auto mk = [&](const std::vector<int64_t> &rph, const std::vector<int32_t> &ch, const std::vector<float> &vh,
+                      int64_t Eh, int64_t **drp, int32_t **dc, float **dv) {
+            CK(hipMalloc(dc, (Eh * NB + 1024) * 4));
+            CK(hipMalloc(dv, (Eh * NB + 1024) * 4));
+            CK(hipMalloc(drp, (B * NB + 1) * 8));
+            std::vector<int64_t> big(B * NB + 1);
+            for (int64_t q = 0; q < NB; ++q) {
+                CK(hipMemcpy(*dc + q * Eh, ch.data(), Eh * 4, hipMemcpyHostToDevice));
+                CK(hipMemcpy(*dv + q * Eh, vh.data(), Eh * 4, hipMemcpyHostToDevice));
+                for (int64_t i = 0; i < B; ++i) big[q * B + i] = q * Eh + rph[i];
+            }
+            big[B * NB] = Eh * NB;
+            CK(hipMemcpy(*drp, big.data(), big.size() * 8, hipMemcpyHostToDevice));
+        };
+        int64_t *drA, *drB;
+        int32_t *dcA, *dcB;
+        float *dvA, *dvB, *dz;
+        mk(rpA, cA, vA, EA, &drA, &dcA, &dvA);
+        mk(rpB, cB, vB, EB, &drB, &dcB, &dvB);
+        CK(hipMalloc(&dz, B * 4));
+        int q = 0;
+        t = time_us(reps, [&] {
+            const dlr::DevBatch ba{drA + (q % NB) * B, dcA, dvA, d_lab, B, EA};
+            const dlr::DevBatch bb{drB + (q % NB) * B, dcB, dvB, d_lab, B, EB};
+            ++q;
+            hipLaunchKernelGGL((k2_split<16, true, false>), dim3((B + 63) / 64), dim3(256), 0, 0, ba, d_w, nullptr, dz);
+            hipLaunchKernelGGL((k2_splitB<16>), dim3((B + 63) / 64), dim3(256), 0, 0, bb, d_w, dz, d_r2);
+        });
+        printf("K2 column-split 2 passes     %8.2f us  %7.1f GB/s\n", t, rate(mb_k2, t));
+        bad |= cmp_bits(d_r, d_r2, B, "K2 split vs ref");
+        for (int seg : {8, 16, 32}) {
+            q = 0;
+            t = time_us(reps, [&] {
+                const dlr::DevBatch ba{drA + (q % NB) * B, dcA, dvA, d_lab, B, EA};
+                ++q;
+                if (seg == 8)
+                    hipLaunchKernelGGL((k2_split<8, true, false>), dim3((B + 31) / 32), dim3(256), 0, 0, ba, d_w, nullptr, dz);
+                else if (seg == 16)
+                    hipLaunchKernelGGL((k2_split<16, true, false>), dim3((B + 63) / 64), dim3(256), 0, 0, ba, d_w, nullptr, dz);
+                else
+                    hipLaunchKernelGGL((k2_split<32, true, false>), dim3((B + 127) / 128), dim3(256), 0, 0, ba, d_w, nullptr, dz);
+            });
+            printf("K2 half pass A alone SEG=%-2d  %8.2f us\n", seg, t);
+        }
+    }
     {   // margin over a cold 10M-row shard (HBM-resident stream), plain vs nt
         const int64_t NB = 40;  // batches in the cold shard
         const int64_t EB = E * NB;
