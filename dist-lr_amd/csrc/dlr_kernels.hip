@@ -617,7 +617,9 @@ __device__ __forceinline__ float l2_only_update(float wj, const RankSizes &rs, f
 
 // K4d: every weight gets the L2-only update of the W ranks; touched columns
 // are overwritten afterwards by K4s.  16-byte non-temporal loads and stores
-// (every byte is touched once).
+// (every byte is touched once), one float4 per thread: a one-shot grid
+// streams at 6.0 TB/s where a 2048-block grid-stride loop reached 4.9
+// (profiles/r01_kbench_l2.txt).
 __global__ __launch_bounds__(256) void k_dense_l2(float *__restrict__ w, int64_t D, RankSizes rs, float lr,
                                                   float C, int mode) {
     typedef float f4 __attribute__((ext_vector_type(4)));
@@ -838,8 +840,18 @@ __global__ __launch_bounds__(256) void k_dense_combine(const float *__restrict__
                                                        float Bf, double Bd, float lr, float C) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= D) return;
+    // chunk order as before; the partials are loaded 16 at a time so the
+    // loads overlap (D threads only -- latency, not bandwidth, bounds this)
+    constexpr int U = 16;
     float G = 0.0f;
-    for (int64_t k = 0; k < nchunks; ++k) G = G + part[k * Dp + j];
+    for (int64_t k = 0; k < nchunks; k += U) {
+        float pv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) pv[u] = k + u < nchunks ? part[(k + u) * Dp + j] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (k + u < nchunks) G = G + pv[u];
+    }
     const float wj = w[j];
     const float cw = C * wj;
     const float l2 = cw / Bf;
@@ -1073,7 +1085,7 @@ hipError_t launch_grad_touched(const DevCsc &cs, const uint32_t *cols, int64_t n
 hipError_t launch_dense_l2(float *w, int64_t D, const RankSizes &rs, float lr, float C, int mode, hipStream_t s) {
     if (D <= 0) return hipSuccess;
     const int64_t work = std::max<int64_t>(D / 4, 4);
-    const unsigned grid = (unsigned)std::min<int64_t>((work + 255) / 256, 256 * 8);
+    const unsigned grid = (unsigned)std::min<int64_t>((work + 255) / 256, int64_t(1) << 30);
     hipLaunchKernelGGL(k_dense_l2, dim3(grid), dim3(256), 0, s, w, D, rs, lr, C, mode);
     return hipGetLastError();
 }

@@ -94,6 +94,38 @@ __global__ __launch_bounds__(256) void mb_gather_g(const int4 *idx, const float 
     out[t] = s;
 }
 
+// Dense L2-only update variants (C5's HBM-bound pass), W = 1 formula.
+template <bool NT, int U>
+__global__ __launch_bounds__(256) void mb_l2(float *__restrict__ w, int64_t n4, float Bf, float lr, float C) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q0 < n4; q0 += stride * U) {
+        f4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t q = q0 + u * stride;
+            if (q < n4) v[u] = NT ? __builtin_nontemporal_load(reinterpret_cast<const f4 *>(w) + q)
+                                  : reinterpret_cast<const f4 *>(w)[q];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t q = q0 + u * stride;
+            if (q >= n4) continue;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float cw = C * v[u][k];
+                const float l2 = cw / Bf;
+                const float st = lr * l2;
+                v[u][k] = v[u][k] - st;
+            }
+            if (NT)
+                __builtin_nontemporal_store(v[u], reinterpret_cast<f4 *>(w) + q);
+            else
+                reinterpret_cast<f4 *>(w)[q] = v[u];
+        }
+    }
+}
+
 // ---------------- K2 candidates
 // The production margin kernel with non-temporal loads of the col/val
 // stream (so the streamed lines do not evict w from L2).
@@ -928,6 +960,28 @@ int main(int argc, char **argv) {
         printf("K2 ref SEG=%-2d               %8.2f us  %7.1f GB/s\n", seg, t, rate(mb_k2, t));
     }
     hipLaunchKernelGGL(dlr::k_margin_residual<16>, dim3((B + 63) / 64), dim3(256), 0, 0, bt, d_w, d_r);
+    {   // C5 dense L2 pass variants on a 1 GiB weight vector (2^28 floats)
+        const int64_t DW = (int64_t)1 << 28;
+        float *wb = nullptr;
+        CK(hipMalloc(&wb, DW * 4));
+        CK(hipMemset(wb, 0, DW * 4));
+        const int64_t n4 = DW / 4;
+        const double bytes = 2.0 * DW * 4;
+        auto run = [&](const char *nm, auto kern, unsigned grid) {
+            const float tt = time_us(20, [&] { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, wb, n4, 1024.f, 0.2f, 1.0f); });
+            printf("L2 pass %-28s grid %6u %9.1f us  %7.1f GB/s\n", nm, grid, tt, bytes / (tt * 1e-6) / 1e9);
+        };
+        run("nt U1 (production)", mb_l2<true, 1>, 2048);
+        run("nt U1", mb_l2<true, 1>, 8192);
+        run("nt U4", mb_l2<true, 4>, 2048);
+        run("nt U4", mb_l2<true, 4>, 4096);
+        run("plain U1", mb_l2<false, 1>, 2048);
+        run("plain U4", mb_l2<false, 4>, 2048);
+        run("plain U4", mb_l2<false, 4>, 8192);
+        run("plain U1 one-shot", mb_l2<false, 1>, (unsigned)((n4 + 255) / 256));
+        run("nt U1 one-shot", mb_l2<true, 1>, (unsigned)((n4 + 255) / 256));
+        CK(hipFree(wb));
+    }
     {   // column-split margin (two passes over half-size w tables) vs one pass, cold shard
         const int64_t NB = 40;
         // host split of the batch: entries with col < D/2 (A) and >= D/2 (B)
