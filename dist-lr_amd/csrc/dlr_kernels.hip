@@ -392,6 +392,7 @@ __device__ unsigned long long *g_stamp = nullptr;
 constexpr int kGradWaves = 16;  // waves per workgroup
 constexpr int kGradNG = 4;      // 64-column groups per wave
 constexpr int kBlk = 256;       // window = one phase block (<= 255 entries)
+constexpr int kBlkPad = kBlk + 8;  // product slab per wave: lane reads at o + [0, 8) never leave it
 
 template <int FILL, bool FUSED, bool NTW>
 __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int64_t D, int64_t B,
@@ -403,8 +404,8 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float *s_r = smem;
     const int lane = threadIdx.x & (kWave - 1);
-    const int wv = threadIdx.x / kWave;
-    float *s_p = smem + R + wv * kBlk;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // uniform: scalar block loads
+    float *s_p = smem + R + wv * kBlkPad;
     const int P = pc.phases;
     const int64_t ng = (D + 63) / 64;
     const int64_t gfirst = (int64_t)blockIdx.x * (kGradWaves * NG) + wv;
@@ -431,10 +432,9 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
             cnt[gi][p] = (ok && p < P) ? hi - (lane ? lo : 0u) : 0u;
         }
     }
+    auto windows = [&](int p) {
 #pragma unroll
-    for (int gi = 0; gi < NG; ++gi) {
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
+        for (int gi = 0; gi < NG; ++gi) {
             const unsigned e = bs[gi][p] + lane * 4;  // entries are padded: always in bounds
             if (NTW) {
                 rq[gi][p] = load_stream(reinterpret_cast<const ushort4 *>(pc.row + e));
@@ -444,7 +444,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
                 vq[gi][p] = *reinterpret_cast<const float4 *>(pc.val + e);
             }
         }
-    }
+    };
     // Residual fills by LDS-DMA (no VGPRs): each wave-instruction copies
     // 1 KiB -- lane l's 16 bytes land at the wave-uniform base + 16*l.
     auto fill = [&](int64_t lo) {
@@ -456,7 +456,12 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
                 (__attribute__((address_space(3))) void *)(s_r + o), 16, 0, 0);
         }
     };
+    // Phase 0's windows and the first fill are issued up front; phase 1's
+    // windows only after phase 0's first group has consumed its data (the
+    // compiler drains every older load there), so they stream from HBM while
+    // the rest of phase 0 computes instead of delaying its start.
     DLR_STAMP(0);
+    windows(0);
     fill(0);
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
@@ -471,6 +476,11 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
         DLR_STAMP(1 + 3 * p);
 #pragma unroll
         for (int gi = 0; gi < NG; ++gi) {
+            if (p == 0 && gi == 1 && P > 1) {
+                asm volatile("" ::: "memory");
+                windows(1);
+                asm volatile("" ::: "memory");
+            }
             if (gfirst + kGradWaves * gi >= ng) break;  // wave-uniform
             const ushort4 r4 = rq[gi][p];
             const float4 v4 = vq[gi][p];
@@ -481,16 +491,33 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
             q.w = s_r[r4.w] * v4.w;
             *reinterpret_cast<float4 *>(s_p + lane * 4) = q;
             wave_sync();
-            // this lane's column: cnt products in order from off
+            // this lane's column: cnt products in order from off.  The first
+            // eight are read at immediate offsets from s_p + o (the slab is
+            // padded, so no clamping) and added while any lane still has one
+            // (a wave-uniform exit: the sum stops at the wave's largest count,
+            // ~5 at C2's 1.6 entries per column and phase); the rare longer
+            // runs continue in a general loop.  Per product: compare, add,
+            // select -- this loop is what bounds the kernel (VALU issue).
             const unsigned o = off[gi][p], c = cnt[gi][p];
+            const float *__restrict__ sp = s_p + o;
             float a = acc[gi];
-            for (unsigned k = 0; k < c; k += 8) {
-                float x[8];
+            float x[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) x[u] = s_p[min(o + k + u, (unsigned)kBlk - 1)];
+            for (int u = 0; u < 8; ++u) x[u] = sp[u];
+            // all eight reads issue together (one LDS round trip); without
+            // this the compiler sinks each read into its step of the loop
+            asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]),
+                         "v"(x[7]));
 #pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (k + u < c) a = a + x[u];
+            for (int u = 0; u < 8; ++u) {
+                const bool take = (unsigned)u < c;
+                if (__builtin_amdgcn_ballot_w64(take) == 0) break;  // wave-uniform
+                const float t = a + x[u];
+                a = take ? t : a;
+            }
+            for (unsigned k = 8; __builtin_amdgcn_ballot_w64(k < c) != 0; ++k) {
+                const float xv = s_p[min(o + k, (unsigned)kBlk - 1)];
+                if (k < c) a = a + xv;
             }
             acc[gi] = a;
             wave_sync();
@@ -1022,7 +1049,7 @@ hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float 
     const float Bf = (float)B;
     const double Bd = (double)B;
     const int fill = grad_lds_fill(B);
-    const size_t lds = (size_t)fill * 4096 * 4 + (size_t)kGradWaves * kBlk * 4;
+    const size_t lds = (size_t)fill * 4096 * 4 + (size_t)kGradWaves * kBlkPad * 4;
     // Non-temporal window loads measured slower here (tools/ab_bench.sh,
     // C2: 19.4 vs 16.6 us -- this kernel is latency-bound in its prologue);
     // DLR_GRAD_NT=1 turns them on.

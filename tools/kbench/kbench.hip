@@ -94,6 +94,143 @@ __global__ __launch_bounds__(256) void mb_gather_g(const int4 *idx, const float 
     out[t] = s;
 }
 
+// Ablation copy of dlr::k_grad_lds (FILL = 8, not fused): ABL bit 0 skips
+// the residual gathers (products = values), bit 1 skips the per-column read
+// loop (one product per lane), bit 2 runs phase 0 only, bit 3 skips the fill
+// waits (garbage residuals; timing only).
+template <int ABL>
+__global__ __launch_bounds__(1024) void mb_grad_abl(dlr::DevPcsc pc, int64_t D, const float *__restrict__ resid,
+                                                    float *__restrict__ w, float *__restrict__ gout, float Bf,
+                                                    double Bd, float C) {
+    constexpr int R = 8 * 4096, NG = 4, W = 16;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float *s_r = smem;
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x / 64;
+    float *s_p = smem + R + wv * (256 + 8);
+    const int P = (ABL & 4) ? 1 : pc.phases;
+    const int64_t ng = (D + 63) / 64;
+    const int64_t gfirst = (int64_t)blockIdx.x * (W * NG) + wv;
+    unsigned bs[NG][2], off[NG][2], cnt[NG][2];
+    float acc[NG], wj[NG];
+    ushort4 rq[NG][2];
+    float4 vq[NG][2];
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+        const int64_t g = gfirst + W * gi;
+        const bool gv = g < ng;
+        const int64_t gc = gv ? g : ng - 1;
+        const int64_t j = g * 64 + lane;
+        const bool ok = gv && j < D;
+        wj[gi] = w[j < D ? j : D - 1];
+        acc[gi] = 0.0f;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int64_t blk = gc * pc.phases + (p < pc.phases ? p : pc.phases - 1);
+            bs[gi][p] = pc.base[blk];
+            const unsigned hi = pc.ends[blk * 64 + lane];
+            const unsigned lo = pc.ends[blk * 64 + (lane ? lane - 1 : 0)];
+            off[gi][p] = lane ? lo : 0u;
+            cnt[gi][p] = (ok && p < P) ? hi - (lane ? lo : 0u) : 0u;
+        }
+    }
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const unsigned e = bs[gi][p] + lane * 4;
+            rq[gi][p] = *reinterpret_cast<const ushort4 *>(pc.row + e);
+            vq[gi][p] = *reinterpret_cast<const float4 *>(pc.val + e);
+        }
+    auto fill = [&](int64_t lo) {
+#pragma unroll
+        for (int f = 0; f < 8; ++f) {
+            const int o = (f * W + wv) * 64 * 4;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(resid + lo + o + lane * 4),
+                                             (__attribute__((address_space(3))) void *)(s_r + o), 16, 0, 0);
+        }
+    };
+    if (!(ABL & 8)) fill(0);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        if (p >= P) break;
+        if (p > 0) {
+            __syncthreads();
+            if (!(ABL & 8)) fill((int64_t)p * R);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) {
+            if (gfirst + W * gi >= ng) break;
+            const ushort4 r4 = rq[gi][p];
+            const float4 v4 = vq[gi][p];
+            float4 q;
+            if (ABL & 1) {
+                q = v4;
+                q.x += (float)r4.x;
+            } else {
+                q.x = s_r[r4.x] * v4.x;
+                q.y = s_r[r4.y] * v4.y;
+                q.z = s_r[r4.z] * v4.z;
+                q.w = s_r[r4.w] * v4.w;
+            }
+            *reinterpret_cast<float4 *>(s_p + lane * 4) = q;
+            __builtin_amdgcn_wave_barrier();
+            const unsigned o = off[gi][p], c = cnt[gi][p];
+            const float *sp = s_p + o;
+            float a = acc[gi];
+            if (ABL & 2) {
+                a = a + sp[0];
+            } else {
+                float x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = sp[u];
+                asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]));
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const bool take = (unsigned)u < c;
+                    if (__builtin_amdgcn_ballot_w64(take) == 0) break;
+                    const float t = a + x[u];
+                    a = take ? t : a;
+                }
+            }
+            acc[gi] = a;
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+        const int64_t j = (gfirst + W * gi) * 64 + lane;
+        if (gfirst + W * gi >= ng || j >= D) continue;
+        const float cw = C * wj[gi];
+        const float l2 = cw / Bf;
+        gout[j] = (float)((double)acc[gi] / Bd + (double)l2);
+    }
+}
+
+// LDS random 4-B gathers: 1,024 threads, each NR reads per round from a
+// 128 KiB table at LCG addresses.
+template <int NR>
+__global__ __launch_bounds__(1024) void mb_lds_gather(float *out, int rounds, unsigned mask) {
+    extern __shared__ float tab[];
+    for (int i = threadIdx.x; i < 32768; i += 1024) tab[i] = (float)i;
+    __syncthreads();
+    unsigned x = threadIdx.x * 2654435761u + blockIdx.x;
+    float acc = 0.f;
+    for (int r = 0; r < rounds; ++r) {
+        float v[NR];
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+            x = x * 1664525u + 1013904223u;
+            v[k] = tab[(x >> 8) & mask];
+        }
+#pragma unroll
+        for (int k = 0; k < NR; ++k) acc += v[k];
+    }
+    out[blockIdx.x * 1024 + threadIdx.x] = acc;
+}
+
 // Dense L2-only update variants (C5's HBM-bound pass), W = 1 formula.
 template <bool NT, int U>
 __global__ __launch_bounds__(256) void mb_l2(float *__restrict__ w, int64_t n4, float Bf, float lr, float C) {
@@ -1252,6 +1389,36 @@ int main(int argc, char **argv) {
         t = time_us(reps, [&] { CK(dlr::launch_grad_lds(pc, D, B, d_rp, d_w, d_g2, 0.2f, 1.0f, false, 0)); });
         printf("K3 production lds            %8.2f us  %7.1f GB/s\n", t, rate(mb_k3, t));
         bad |= cmp_bits(d_g, d_g2, D, "K3 production lds vs ref");
+        {
+            const size_t lds = (size_t)8 * 4096 * 4 + 16 * 264 * 4;
+            const unsigned grid = (unsigned)((ngr + 63) / 64);
+            auto abl = [&](const char *nm, auto kern) {
+                const float ta = time_us(reps, [&] {
+                    hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), lds, 0, pc, D, d_rp, d_w, d_g2, (float)B, (double)B, 1.0f);
+                });
+                printf("K3 ablation %-32s %8.2f us\n", nm, ta);
+            };
+            abl("none (copy)", mb_grad_abl<0>);
+            abl("no gathers", mb_grad_abl<1>);
+            abl("no read loop", mb_grad_abl<2>);
+            abl("no gathers, no read loop", mb_grad_abl<3>);
+            abl("phase 0 only", mb_grad_abl<4>);
+            abl("no fills", mb_grad_abl<8>);
+            abl("no fills, no gathers, no loop", mb_grad_abl<11>);
+            abl("phase 0 only, no fills/gathers/loop", mb_grad_abl<15>);
+            float *d_o = nullptr;
+            CK(hipMalloc(&d_o, 256 * 1024 * 4));
+            for (unsigned mask : {32767u, 0u}) {
+                const int rounds = 64;
+                const float tg = time_us(20, [&] {
+                    hipLaunchKernelGGL(mb_lds_gather<8>, dim3(256), dim3(1024), 131072, 0, d_o, rounds, mask);
+                });
+                const double n = 256.0 * 1024 * 8 * rounds;
+                printf("LDS gather mask %5u: %8.2f us  %7.1f G/s chip  %5.2f lanes/clk/CU @2.4GHz\n", mask, tg, n / tg * 1e-3,
+                       n / 256 / (tg * 1e-6) / 2.4e9);
+            }
+            CK(hipFree(d_o));
+        }
         for (int it = 0; it < 20; ++it) CK(dlr::launch_grad_lds(pc, D, B, d_rp, d_w, d_g2, 0.2f, 1.0f, false, 0));
         CK(hipDeviceSynchronize());
         std::vector<unsigned long long> st((size_t)G * 8);
