@@ -58,7 +58,14 @@ CONFIGS = {
                label="C4 dense LR", kind="dense"),
     "c5": dict(rows=1_024_000, features=1 << 28, nnz=10, batch=1024, value_mode=0, steps=200, warmup=10,
                label="C5 high-dim ultra-sparse LR"),
+    # C4 on ONE GPU as SURVEY 8(d) states it: the rows do not fit in HBM, so
+    # they stay in pinned host memory and each batch is staged over PCIe
+    # (streamed residency); a 2.5M-row host shard stands in for the 20M rows
+    # (the rate is per batch and does not depend on the shard's length)
+    "c4s": dict(rows=2_500_000, features=4096, nnz=4096, batch=65536, value_mode=1, steps=40, warmup=4,
+                label="C4 dense LR, streamed from host", kind="dense", residency="stream"),
 }
+PCIE_PEAK_GBS = 63.0  # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s (spec)
 
 
 def make_shard(args, n_rows: int, stream: int):
@@ -92,6 +99,7 @@ def parse_args():
     args.value_mode = cfg["value_mode"]
     args.label = cfg["label"]
     args.kind = cfg.get("kind", "uniform")
+    args.residency = cfg.get("residency", "auto")
     return args
 
 
@@ -164,14 +172,19 @@ def main():
     t_gen = time.perf_counter() - t_setup
     eng = dlr.Engine(D, device=local, rank=rank, world=world, unique_id=uid)
     eng.set_weights(dlr.init_weight(D))
+    if args.residency != "auto":
+        eng.set_residency({"device": dlr.RESIDENCY_DEVICE, "stream": dlr.RESIDENCY_STREAM}[args.residency])
     nb = eng.load_train_dense(ds, B) if args.kind == "dense" else eng.load_train(ds, B)
+    streamed = args.kind == "dense" and eng.train_residency() == dlr.RESIDENCY_STREAM
     train_bytes, _ = eng.memory_info()
-    ds.free()
+    if not streamed:
+        ds.free()   # a streamed shard reads these host rows every step
     t_load = time.perf_counter() - t_setup - t_gen
     layout = "dense" if args.kind == "dense" else \
         {dlr.LAYOUT_CLASSIC: "classic", dlr.LAYOUT_LDS: "lds", dlr.LAYOUT_TOUCHED: "touched"}[eng.train_layout()]
-    log(f"[rank {rank}] shard {args.rows} x {D}, nnz/row {args.nnz}: generated {t_gen:.1f}s, resident "
-        f"{train_bytes / 2**30:.2f} GiB in {t_load:.1f}s, {nb} batches/epoch, gradient layout {layout}")
+    log(f"[rank {rank}] shard {args.rows} x {D}, nnz/row {args.nnz}: generated {t_gen:.1f}s, "
+        f"{'streamed from host' if streamed else 'resident'} {train_bytes / 2**30:.2f} GiB in {t_load:.1f}s, "
+        f"{nb} batches/epoch, gradient layout {layout}")
 
     def run(k0, k):
         for i in range(k0, k0 + k):
@@ -218,9 +231,12 @@ def main():
     # between ONE event pair (no per-launch event overhead, comparable with
     # rocprofv3's kernel durations).  Runs after the measured passes: the
     # stages run without their partners and change the weights.
+    # (A streamed shard is bound by the batch copies instead: no stage pass.)
     k0 = args.warmup + 2 * args.steps
-    stage_us = {"margin": eng.stage_time(dlr.STAGE_MARGIN, k0 % nb, args.steps, args.lr) * 1000.0,
-                "gradient": eng.stage_time(dlr.STAGE_GRADIENT, k0 % nb, args.steps, args.lr) * 1000.0}
+    stage_us = {}
+    if not streamed:
+        stage_us = {"margin": eng.stage_time(dlr.STAGE_MARGIN, k0 % nb, args.steps, args.lr) * 1000.0,
+                    "gradient": eng.stage_time(dlr.STAGE_GRADIENT, k0 % nb, args.steps, args.lr) * 1000.0}
     if layout == "touched":
         stage_us["update"] = eng.stage_time(dlr.STAGE_UPDATE, k0 % nb, args.steps, args.lr) * 1000.0
     B_eff = B if B > 0 else args.rows                 # B = -1: the full shard per step
@@ -240,6 +256,35 @@ def main():
                 traffic = tj.get("hbm_bytes_per_step")
         except Exception:
             traffic = None
+
+    roofline = {
+        "bound": "hbm",
+        "kernel": "train step = margin (K2) + gradient (K3, + fused update) + update/merge (K4: dense L2 "
+                  "pass for the touched layout, key-range merge when N>1)",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": traffic,
+        "alg_bytes_per_step": step_bytes,
+        "kernel_avg_us": {k: round(v, 3) for k, v in stage_us.items()},
+        "step_breakdown_us": {k: round(v, 3) for k, v in avg_us.items()},
+        "timing": "value: K un-instrumented steps; kernel_avg_us: each kernel stage over K consecutive "
+                  "batches between one HIP-event pair on the engine stream (achieved = alg bytes / their "
+                  "sum); step_breakdown_us: a pass of K steps with an event pair around every launch "
+                  "(includes the exchange when N>1; event overhead ~2 us per launch)",
+        "instrumented_ms_per_step": round(el_instr / args.steps * 1000.0, 5),
+    }
+    if streamed:
+        # bound by the host->device batch copies (B rows x D fp32 + labels per step)
+        h2d = B_eff * (4 * D + 4)
+        pcie = h2d / (el / args.steps) / 1e9
+        roofline.update({"bound": "pcie", "kernel": "per-batch host->device staging (copy stream) overlapped "
+                                                      "with the margin/gradient kernels of the previous batch",
+                         "achieved": round(pcie, 2), "peak": PCIE_PEAK_GBS, "frac": round(pcie / PCIE_PEAK_GBS, 4),
+                         "h2d_bytes_per_step": h2d, "hbm_kernels_gbs": round(achieved, 1) if kern_us > 0 else None})
+        roofline["timing"] = "value and achieved: K un-instrumented steps (copy-bound); step_breakdown_us: " \
+                             "the event pass (the margin interval includes the wait for the batch copy)"
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -263,30 +308,14 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic (seeded gen_data.py-shaped {'dense' if args.kind == 'dense' else 'sparse'} rows, "
-                    f"{'4-decimal' if args.value_mode else 'binary'} values; resident in HBM)",
+                    f"{'4-decimal' if args.value_mode else 'binary'} values; "
+                    f"{'pinned host memory, staged per batch' if streamed else 'resident in HBM'})",
             "config": {"workload": f"{args.label}: {args.rows} rows/GPU x {D} features, {args.nnz} nnz/row, "
                                    f"batch {B}, sync SGD lr {args.lr}, C=1",
                        "name": args.config, "gradient_layout": layout,
                        "rows_per_gpu": args.rows, "num_feature_dim": D, "nnz_per_row": args.nnz,
                        "batch_size": B, "parallelism": f"dp{world}"},
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "train step = margin (K2) + gradient (K3, + fused update) + update/merge (K4: dense L2 "
-                          "pass for the touched layout, key-range merge when N>1)",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "alg_bytes_per_step": step_bytes,
-                "kernel_avg_us": {k: round(v, 3) for k, v in stage_us.items()},
-                "step_breakdown_us": {k: round(v, 3) for k, v in avg_us.items()},
-                "timing": "value: K un-instrumented steps; kernel_avg_us: each kernel stage over K consecutive "
-                          "batches between one HIP-event pair on the engine stream (achieved = alg bytes / their "
-                          "sum); step_breakdown_us: a pass of K steps with an event pair around every launch "
-                          "(includes the exchange when N>1; event overhead ~2 us per launch)",
-                "instrumented_ms_per_step": round(el_instr / args.steps * 1000.0, 5),
-            },
+            "roofline": roofline,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -76,6 +76,13 @@ struct TrainShard {
     // dense shard (dlr_load_train_dense): X row-major n_rows x D
     bool dense = false, dblocked = false;
     float *dX = nullptr, *dpart = nullptr;
+    // streamed dense shard (DLR_RESIDENCY_STREAM): X stays in the caller's
+    // host memory (registered, pinned in place); each batch's rows and labels
+    // are staged into one of two device slots on the copy stream
+    bool streamed = false, host_registered = false;
+    const float *hX = nullptr;
+    float *sx[2] = {nullptr, nullptr}, *sl[2] = {nullptr, nullptr};
+    int64_t sb[2] = {-1, -1};  // batch held by each slot
     bool row16 = false;
     uint32_t *cptr = nullptr;   // n_batches x (D+1)
     void *crow = nullptr;
@@ -124,6 +131,11 @@ struct dlr_ctx {
     float *xnewv = nullptr;
     int64_t xcap = 0;
     dlr::RankSizes rs{};
+    // residency of the next dense training shard, and the streamed shard's
+    // copy stream + slot events (created on first use)
+    int residency = DLR_RESIDENCY_AUTO;
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
     std::vector<void *> allocs;
     // timing
     bool timing = false;
@@ -191,6 +203,11 @@ int upload(dlr_ctx *c, T **dst, const T *src, size_t n, size_t pad = 0) {
 
 void free_train(dlr_ctx *c) {
     TrainShard &t = c->train;
+    if (t.streamed) {
+        if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+        if (t.host_registered) (void)hipHostUnregister(const_cast<float *>(t.hX));
+        for (void *p : {(void *)t.sx[0], (void *)t.sx[1], (void *)t.sl[0], (void *)t.sl[1]}) dev_free(c, p);
+    }
     for (void *p : {(void *)t.row_ptr, (void *)t.col, (void *)t.val, (void *)t.label, (void *)t.w_row_ptr,
                     (void *)t.w_col, (void *)t.w_val, (void *)t.w_label, (void *)t.cptr, t.crow, (void *)t.cval,
                     (void *)t.pbase, (void *)t.pends, (void *)t.prow, (void *)t.pval, (void *)t.tcols,
@@ -536,11 +553,72 @@ dlr::DevBatch batch_view(const dlr_ctx *c, int64_t b) {
     return {t.row_ptr + sp.first_row, t.col, t.val, t.label + sp.first_row, sp.rows, nnz};
 }
 
+// Streamed dense shard: copy batch b's rows (wrapping to row 0 as
+// data_iter.h:49-52 does) and labels into slot s, after the kernels that
+// last read the slot are done (ev_free[s]); ev_ready[s] marks the copy.
+hipError_t stage_dense(dlr_ctx *c, int64_t b, int s) {
+    TrainShard &t = c->train;
+    const int64_t D = c->D, N = t.n_rows;
+    hipError_t e = hipStreamWaitEvent(c->cstream, c->ev_free[s], 0);
+    int64_t row = t.plan[(size_t)b].first_row, off = 0, left = t.plan[(size_t)b].rows;
+    while (e == hipSuccess && left > 0) {
+        const int64_t n = std::min(left, N - row);
+        e = hipMemcpyAsync(t.sx[s] + off * D, t.hX + row * D, (size_t)(n * D) * 4, hipMemcpyHostToDevice, c->cstream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(t.sl[s] + off, t.label + row, (size_t)n * 4, hipMemcpyDeviceToDevice, c->cstream);
+        off += n;
+        left -= n;
+        row = 0;
+    }
+    if (e == hipSuccess) e = hipEventRecord(c->ev_ready[s], c->cstream);
+    t.sb[s] = e == hipSuccess ? b : -1;
+    return e;
+}
+
+// Batch b's rows as the dense kernels see them: the resident shard (rows
+// from plan.first_row, wrapping), or the slot b is staged in (rows 0..B-1;
+// the engine stream waits for its copy).
+hipError_t dense_batch(dlr_ctx *c, int64_t b, dlr::DevDense *dd, int64_t *first) {
+    TrainShard &t = c->train;
+    if (!t.streamed) {
+        *dd = {t.dX, t.label, t.n_rows, c->D};
+        *first = t.plan[(size_t)b].first_row;
+        return hipSuccess;
+    }
+    int s = t.sb[0] == b ? 0 : t.sb[1] == b ? 1 : -1;
+    hipError_t e = hipSuccess;
+    if (s < 0) {
+        s = (int)(b & 1);
+        e = stage_dense(c, b, s);
+    }
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_ready[s], 0);
+    *dd = {t.sx[s], t.sl[s], t.plan[(size_t)b].rows, c->D};
+    *first = 0;
+    return e;
+}
+
+// After the last kernel that reads batch b's slot: release the slot and
+// start copying the next batch into the other one (it overlaps this step's
+// remaining work and the next margin's wait is only for what is left).
+hipError_t dense_batch_done(dlr_ctx *c, int64_t b) {
+    TrainShard &t = c->train;
+    if (!t.streamed) return hipSuccess;
+    const int s = t.sb[0] == b ? 0 : 1;
+    hipError_t e = hipEventRecord(c->ev_free[s], c->stream);
+    const int64_t nx = (b + 1) % (int64_t)t.plan.size();
+    if (e == hipSuccess && t.sb[0] != nx && t.sb[1] != nx) e = stage_dense(c, nx, s ^ 1);
+    return e;
+}
+
 hipError_t launch_margin(dlr_ctx *c, int64_t b) {
     const TrainShard &t = c->train;
-    if (t.dense)
-        return dlr::launch_dense_margin({t.dX, t.label, t.n_rows, c->D}, t.plan[(size_t)b].first_row,
-                                        t.plan[(size_t)b].rows, c->w, c->resid, c->stream);
+    if (t.dense) {
+        dlr::DevDense dd;
+        int64_t first;
+        hipError_t e = dense_batch(c, b, &dd, &first);
+        if (e != hipSuccess) return e;
+        return dlr::launch_dense_margin(dd, first, t.plan[(size_t)b].rows, c->w, c->resid, c->stream);
+    }
     return dlr::launch_margin_residual(batch_view(c, b), c->w, c->resid, c->stream);
 }
 
@@ -558,13 +636,17 @@ dlr::DevCsc csc_view(const dlr_ctx *c, int64_t b) {
             t.row16};
 }
 
-dlr::DevDense dense_view(const TrainShard &t, int64_t D) { return {t.dX, t.label, t.n_rows, D}; }
-
 hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float lr, float C, bool fused) {
     const TrainShard &t = c->train;
-    if (t.dense)
-        return dlr::launch_dense_grad(dense_view(t, c->D), t.plan[(size_t)b].first_row, B, c->resid, c->w, gout,
-                                      t.dpart, t.dblocked, lr, C, fused, c->stream);
+    if (t.dense) {
+        dlr::DevDense dd;
+        int64_t first;
+        hipError_t e = dense_batch(c, b, &dd, &first);
+        if (e == hipSuccess)
+            e = dlr::launch_dense_grad(dd, first, B, c->resid, c->w, gout, t.dpart, t.dblocked, lr, C, fused, c->stream);
+        if (e == hipSuccess) e = dense_batch_done(c, b);
+        return e;
+    }
     if (t.pcsc) return dlr::launch_grad_lds(pcsc_view(c, b), c->D, B, c->resid, c->w, gout, lr, C, fused, c->stream);
     hipError_t e = dlr::launch_grad(csc_view(c, b), c->D, c->resid, c->w, gout, B, lr, C, fused, c->stream);
     if (e != hipSuccess || !t.any_long) return e;
@@ -604,6 +686,10 @@ int dlr_create(int device, int rank, int world, const void *unique_id, int64_t D
     c->D = D;
     c->chunk = (D + world - 1) / world;
     c->Dpad = c->chunk * world;
+    if (const char *r = getenv("DLR_RESIDENCY"))  // default for dlr_set_residency
+        c->residency = strcmp(r, "stream") == 0 ? DLR_RESIDENCY_STREAM
+                       : strcmp(r, "device") == 0 ? DLR_RESIDENCY_DEVICE
+                                                  : DLR_RESIDENCY_AUTO;
     HIPC(c.get(), hipSetDevice(device));
     HIPC(c.get(), hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     int rc;
@@ -636,11 +722,18 @@ void dlr_destroy(dlr_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->cstream) (void)hipStreamSynchronize(ctx->cstream);
+    free_train(ctx);  // unregisters a streamed shard's host rows
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     for (void *p : ctx->allocs) (void)hipFree(p);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->h_correct) (void)hipHostFree(ctx->h_correct);
     if (ctx->h_ll) (void)hipHostFree(ctx->h_ll);
+    for (int k = 0; k < 2; ++k) {
+        if (ctx->ev_ready[k]) (void)hipEventDestroy(ctx->ev_ready[k]);
+        if (ctx->ev_free[k]) (void)hipEventDestroy(ctx->ev_free[k]);
+    }
+    if (ctx->cstream) (void)hipStreamDestroy(ctx->cstream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -969,7 +1062,39 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
     const char *dg = getenv("DLR_DENSE_GRAD");
     t.dblocked = dg ? strcmp(dg, "blocked") == 0 : (t.B * D > ((int64_t)1 << 24));
     int rc;
-    if ((rc = upload(c, &t.dX, ds->X.data(), ds->X.size(), 64))) return rc;
+    // Residency: device-resident unless asked to stream, or (auto) the rows
+    // would not leave room in HBM (20M x 4096 fp32 = 328 GB
+    // on one 288 GB GPU).  Streamed rows are staged per batch over PCIe.
+    const size_t xbytes = ds->X.size() * 4;
+    const size_t slot_bytes = (size_t)(t.B * D) * 4;
+    bool stream = c->residency == DLR_RESIDENCY_STREAM;
+    if (c->residency == DLR_RESIDENCY_AUTO) {
+        size_t fr = 0, tot = 0;
+        HIPC(c, hipMemGetInfo(&fr, &tot));
+        const size_t reserve = ((size_t)8 << 30) + 4 * slot_bytes;
+        stream = xbytes + reserve > fr;
+    }
+    if (stream) {
+        t.streamed = true;
+        t.hX = ds->X.data();
+        hipError_t e = hipHostRegister(const_cast<float *>(t.hX), xbytes, hipHostRegisterDefault);
+        if (e == hipSuccess)
+            t.host_registered = true;
+        else if (e == hipErrorHostMemoryAlreadyRegistered)
+            (void)hipGetLastError();
+        else
+            return fail(c, DLR_E_HIP, std::string("dlr_load_train_dense: hipHostRegister: ") + hipGetErrorString(e));
+        if (!c->cstream) HIPC(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+        for (int k = 0; k < 2; ++k) {
+            if (!c->ev_ready[k]) HIPC(c, hipEventCreateWithFlags(&c->ev_ready[k], hipEventDisableTiming));
+            if (!c->ev_free[k]) HIPC(c, hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming));
+            if ((rc = dev_alloc(c, (void **)&t.sx[k], slot_bytes + 64))) return rc;
+            if ((rc = dev_alloc(c, (void **)&t.sl[k], (size_t)t.B * 4 + 64))) return rc;
+            HIPC(c, hipEventRecord(c->ev_free[k], c->stream));
+        }
+    } else if ((rc = upload(c, &t.dX, ds->X.data(), ds->X.size(), 64))) {
+        return rc;
+    }
     {
         std::vector<float> lab(ds->label.begin(), ds->label.end());
         if ((rc = upload(c, &t.label, lab.data(), lab.size()))) return rc;
@@ -1203,6 +1328,7 @@ int dlr_stage_time(dlr_ctx *c, int stage, int64_t first, int64_t count, float lr
     const TrainShard &t = c->train;
     if (stage == DLR_STAGE_UPDATE && !t.touched)
         return fail(c, DLR_E_ARG, "dlr_stage_time: the update stage is separate only in the touched layout");
+    if (t.streamed) return fail(c, DLR_E_STATE, "dlr_stage_time: streamed shard (kernel stages wait on batch copies)");
     HIPC(c, hipSetDevice(c->device));
     harvest(c);
     const bool was = c->timing;
@@ -1241,6 +1367,19 @@ int dlr_stage_time(dlr_ctx *c, int stage, int64_t first, int64_t count, float lr
     if (e != hipSuccess) return fail(c, DLR_E_HIP, std::string("dlr_stage_time: ") + hipGetErrorString(e));
     if (avg_ms) *avg_ms = (double)ms / (double)count;
     return DLR_OK;
+}
+
+int dlr_set_residency(dlr_ctx *c, int mode) {
+    if (!c || mode < DLR_RESIDENCY_AUTO || mode > DLR_RESIDENCY_STREAM)
+        return fail(c, DLR_E_ARG, "dlr_set_residency: bad mode");
+    c->residency = mode;
+    return DLR_OK;
+}
+
+int dlr_train_residency(dlr_ctx *c) {
+    if (!c) return DLR_E_ARG;
+    if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_residency: no training shard loaded");
+    return c->train.streamed ? DLR_RESIDENCY_STREAM : DLR_RESIDENCY_DEVICE;
 }
 
 int dlr_train_layout(dlr_ctx *c) {

@@ -23,6 +23,7 @@ MODE_SYNC_LAST = 1
 MODE_ASYNC = 2
 UNIQUE_ID_BYTES = 128
 LAYOUT_CLASSIC, LAYOUT_LDS, LAYOUT_TOUCHED = 0, 1, 2
+RESIDENCY_AUTO, RESIDENCY_DEVICE, RESIDENCY_STREAM = 0, 1, 2
 STAGE_MARGIN, STAGE_GRADIENT, STAGE_UPDATE = 0, 1, 2
 
 # Exported symbols, in include/distlr_amd.h order (tests check the .so
@@ -37,7 +38,7 @@ SYMBOLS = [
     "dlr_init_weight", "dlr_format_model", "dlr_key_range",
     "dlr_get_unique_id", "dlr_create", "dlr_destroy", "dlr_last_error",
     "dlr_set_weights", "dlr_get_weights", "dlr_load_train", "dlr_load_test", "dlr_load_train_dense",
-    "dlr_load_test_dense",
+    "dlr_load_test_dense", "dlr_set_residency", "dlr_train_residency",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
     "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_memory_info",
 ]
@@ -115,6 +116,8 @@ _sig("dlr_dense_view", C.c_int, P, C.POINTER(P), C.POINTER(P))
 _sig("dlr_dense_free", None, P)
 _sig("dlr_load_train_dense", C.c_int, P, P, i64, C.POINTER(i64))
 _sig("dlr_load_test_dense", C.c_int, P, P)
+_sig("dlr_set_residency", C.c_int, P, C.c_int)
+_sig("dlr_train_residency", C.c_int, P)
 _sig("dlr_dataset_write_libsvm", C.c_int, P, C.c_char_p, C.c_int)
 _sig("dlr_dataset_info", C.c_int, P, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64))
 _sig("dlr_dataset_view", C.c_int, P, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P))
@@ -414,7 +417,18 @@ class Engine:
     def load_train_dense(self, ds: DenseDataset, batch_size: int) -> int:
         nb = i64()
         self._c(lib.dlr_load_train_dense(self._h, ds.handle, batch_size, C.byref(nb)))
+        self._train_src = ds  # a streamed shard reads the host rows in place: keep them alive
         return nb.value
+
+    def set_residency(self, mode: int) -> None:
+        """RESIDENCY_AUTO / _DEVICE / _STREAM for the next dense training
+        shard (dlr_set_residency)."""
+        self._c(lib.dlr_set_residency(self._h, mode))
+
+    def train_residency(self) -> int:
+        rc = lib.dlr_train_residency(self._h)
+        self._c(min(rc, 0))
+        return rc
 
     def load_test_dense(self, ds: DenseDataset) -> None:
         self._c(lib.dlr_load_test_dense(self._h, ds.handle))

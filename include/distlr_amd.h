@@ -209,6 +209,20 @@ int dlr_load_test(dlr_ctx *ctx, const dlr_dataset *ds);
 int dlr_load_train_dense(dlr_ctx *ctx, const dlr_dense *ds, int64_t batch_size, int64_t *n_batches);
 int dlr_load_test_dense(dlr_ctx *ctx, const dlr_dense *ds);
 
+/* Residency of the next dense training shard (20M x 4096
+ * fp32 is 328 GB, more than one GPU's HBM).  DEVICE uploads the rows once;
+ * STREAM keeps them in the caller's host memory (registered in place, so
+ * the dlr_dense must outlive the loaded shard) and copies each batch into
+ * one of two device slots on a copy stream while the previous batch
+ * computes -- PCIe-bound; AUTO (default) streams only when the rows would
+ * not fit in free HBM.  Results are identical either way.
+ * dlr_train_residency reports what the loaded shard uses. */
+#define DLR_RESIDENCY_AUTO 0
+#define DLR_RESIDENCY_DEVICE 1
+#define DLR_RESIDENCY_STREAM 2
+int dlr_set_residency(dlr_ctx *ctx, int mode);
+int dlr_train_residency(dlr_ctx *ctx);
+
 /* One step of LR::Train's loop body (lr.cc:30-43) plus the server update
  * (main.cc:57-84) for batch `batch` of the loaded shard: margin + sigmoid +
  * residual (K2), segmented Xᵀr gradient + L2 (K3), key-range exchange over

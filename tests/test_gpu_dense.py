@@ -135,3 +135,60 @@ def test_dense_predict_counts_and_logloss():
         assert abs(ll - ll2) <= 1e-9 * abs(ll2)
     finally:
         eng.close()
+
+
+# Streamed residency (rows staged per batch from pinned host
+# memory into two device slots): the same kernels on the same rows, so the
+# trajectories are bitwise those of the device-resident shard -- through
+# wrapping batches, batches longer than the shard, one full-shard batch,
+# the blocked gradient and the collectives / worker entry points.
+@pytest.mark.parametrize("B", [7, 300, 1000, 2500, -1])
+def test_streamed_dense_bitwise(monkeypatch, B):
+    D = 256
+    dd = dlr.DenseDataset.generate(1000, D, seed=11, stream=1)
+    test = dlr.DenseDataset.generate(333, D, seed=11, stream=2)
+    monkeypatch.setenv("DLR_RESIDENCY", "device")
+    ref = run_engine([dd], D, 3, B, 0.05, test=test, test_interval=1, dense=True)
+    monkeypatch.setenv("DLR_RESIDENCY", "stream")
+    got = run_engine([dd], D, 3, B, 0.05, test=test, test_interval=1, dense=True)
+    assert_same_weights(got.w, ref.w)
+    assert [(c, n) for _, c, n, _ in got.tests] == [(c, n) for _, c, n, _ in ref.tests]
+    orc = oracle.run_worker([dense_shard(dd)], D, 3, B, 0.05, sparse=False)
+    assert_same_weights(got.w, orc.w)
+
+
+@pytest.mark.parametrize("W", [1, 2])
+def test_streamed_dense_blocked_and_collectives(monkeypatch, W):
+    monkeypatch.setenv("DLR_DENSE_GRAD", "blocked")
+    monkeypatch.setenv("DLR_FORCE_COLLECTIVES", "1")
+    D = 512
+    shards = [dlr.DenseDataset.generate(2000, D, seed=12, stream=r + 1) for r in range(W)]
+    monkeypatch.setenv("DLR_RESIDENCY", "device")
+    ref = run_engine(shards, D, 3, 700, 0.05, dense=True)
+    monkeypatch.setenv("DLR_RESIDENCY", "stream")
+    got = run_engine(shards, D, 3, 700, 0.05, dense=True)
+    assert_same_weights(got.w, ref.w)
+
+
+def test_residency_reporting():
+    D = 128
+    dd = dlr.DenseDataset.generate(500, D, seed=13, stream=1)
+    eng = dlr.Engine(D)
+    try:
+        eng.load_train_dense(dd, 100)
+        assert eng.train_residency() == dlr.RESIDENCY_DEVICE  # auto: fits in HBM
+        eng.set_residency(dlr.RESIDENCY_STREAM)
+        nb = eng.load_train_dense(dd, 100)
+        assert eng.train_residency() == dlr.RESIDENCY_STREAM
+        eng.set_weights(dlr.init_weight(D))
+        for b in range(nb):
+            eng.train_step(b, 0.05)
+        with pytest.raises(dlr.DLRError):
+            eng.stage_time(dlr.STAGE_MARGIN, 0, 2)
+        eng.set_residency(dlr.RESIDENCY_DEVICE)
+        eng.load_train_dense(dd, 100)  # the streamed shard is released (host rows unregistered)
+        assert eng.train_residency() == dlr.RESIDENCY_DEVICE
+        with pytest.raises(dlr.DLRError):
+            eng.set_residency(7)
+    finally:
+        eng.close()
