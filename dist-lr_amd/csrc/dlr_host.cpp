@@ -465,6 +465,135 @@ extern "C" int dlr_dataset_write_libsvm(const dlr_dataset *ds, const char *path,
     return ok ? DLR_OK : DLR_E_IO;
 }
 
+// ------------------------------------------------------------ binary CSR cache
+// A parsed shard saved as its four CSR arrays (SURVEY 8(f) ingest: C2's
+// 500M-entry text parse is paid once).  Layout, little-endian:
+//   "DLRCSR" 0 1 | n_rows D nnz (int64) | checksum (uint64) |
+//   row_ptr[n_rows+1] (int64) | col[nnz] (int32) | val[nnz] (fp32) | label[n_rows] (int32)
+// The checksum mixes every 8-byte word of the arrays; a load verifies it and
+// the CSR invariants before handing the shard out.
+
+namespace {
+
+constexpr char kBinMagic[8] = {'D', 'L', 'R', 'C', 'S', 'R', 0, 1};
+
+uint64_t mix_words(uint64_t h, const void *p, size_t bytes) {
+    const unsigned char *b = static_cast<const unsigned char *>(p);
+    size_t i = 0;
+    for (; i + 8 <= bytes; i += 8) {
+        uint64_t w;
+        memcpy(&w, b + i, 8);
+        h = (h ^ w) * 0x100000001B3ull;
+        h ^= h >> 29;
+    }
+    uint64_t w = 0;
+    memcpy(&w, b + i, bytes - i);
+    return ((h ^ w ^ (uint64_t)bytes) * 0x100000001B3ull) ^ (h >> 31);
+}
+
+uint64_t csr_checksum(const dlr_dataset &d) {
+    uint64_t h = 0xCBF29CE484222325ull;
+    h = mix_words(h, d.row_ptr.data(), d.row_ptr.size() * 8);
+    h = mix_words(h, d.col.data(), d.col.size() * 4);
+    h = mix_words(h, d.val.data(), d.val.size() * 4);
+    return mix_words(h, d.label.data(), d.label.size() * 4);
+}
+
+}  // namespace
+
+extern "C" int dlr_dataset_save_binary(const dlr_dataset *ds, const char *path) {
+    if (!ds || !path) {
+        set_error("dlr_dataset_save_binary: bad argument");
+        return DLR_E_ARG;
+    }
+    FILE *f = fopen(path, "wb");
+    if (!f) {
+        set_error(std::string("dlr_dataset_save_binary: cannot write ") + path);
+        return DLR_E_IO;
+    }
+    const int64_t hdr[3] = {ds->n_rows, ds->D, (int64_t)ds->col.size()};
+    const uint64_t sum = csr_checksum(*ds);
+    bool ok = fwrite(kBinMagic, 1, 8, f) == 8 && fwrite(hdr, 8, 3, f) == 3 && fwrite(&sum, 8, 1, f) == 1;
+    ok = ok && fwrite(ds->row_ptr.data(), 8, ds->row_ptr.size(), f) == ds->row_ptr.size();
+    ok = ok && fwrite(ds->col.data(), 4, ds->col.size(), f) == ds->col.size();
+    ok = ok && fwrite(ds->val.data(), 4, ds->val.size(), f) == ds->val.size();
+    ok = ok && fwrite(ds->label.data(), 4, ds->label.size(), f) == ds->label.size();
+    ok = (fclose(f) == 0) && ok;
+    if (!ok) {
+        set_error(std::string("dlr_dataset_save_binary: write failed: ") + path);
+        return DLR_E_IO;
+    }
+    return DLR_OK;
+}
+
+extern "C" int dlr_dataset_load_binary(const char *path, dlr_dataset **out) {
+    if (!path || !out) {
+        set_error("dlr_dataset_load_binary: bad argument");
+        return DLR_E_ARG;
+    }
+    *out = nullptr;
+    FILE *f = fopen(path, "rb");
+    if (!f) {
+        set_error(std::string("dlr_dataset_load_binary: cannot open ") + path);
+        return DLR_E_IO;
+    }
+    auto bad = [&](const std::string &why) {
+        fclose(f);
+        set_error("dlr_dataset_load_binary: " + std::string(path) + ": " + why);
+        return DLR_E_PARSE;
+    };
+    char magic[8];
+    int64_t hdr[3];
+    uint64_t sum = 0;
+    if (fread(magic, 1, 8, f) != 8 || memcmp(magic, kBinMagic, 8) != 0) return bad("not a DLRCSR v1 file");
+    if (fread(hdr, 8, 3, f) != 3 || fread(&sum, 8, 1, f) != 1) return bad("truncated header");
+    const int64_t n = hdr[0], D = hdr[1], nnz = hdr[2];
+    if (n < 0 || D <= 0 || D > INT32_MAX || nnz < 0) return bad("bad header");
+    if (fseeko(f, 0, SEEK_END) != 0) return bad("cannot size the file");
+    const int64_t expect = 40 + 8 * (n + 1) + 8 * nnz + 4 * n;
+    if ((int64_t)ftello(f) != expect) return bad("size does not match the header");
+    fseeko(f, 40, SEEK_SET);
+    auto ds = std::make_unique<dlr_dataset>();
+    ds->n_rows = n;
+    ds->D = D;
+    try {
+        ds->row_ptr.resize((size_t)n + 1);
+        ds->col.resize((size_t)nnz);
+        ds->val.resize((size_t)nnz);
+        ds->label.resize((size_t)n);
+    } catch (const std::bad_alloc &) {
+        fclose(f);
+        set_error("dlr_dataset_load_binary: out of host memory");
+        return DLR_E_NOMEM;
+    }
+    bool ok = fread(ds->row_ptr.data(), 8, ds->row_ptr.size(), f) == ds->row_ptr.size();
+    ok = ok && fread(ds->col.data(), 4, ds->col.size(), f) == ds->col.size();
+    ok = ok && fread(ds->val.data(), 4, ds->val.size(), f) == ds->val.size();
+    ok = ok && fread(ds->label.data(), 4, ds->label.size(), f) == ds->label.size();
+    if (!ok) return bad("short read");
+    fclose(f);
+    if (csr_checksum(*ds) != sum) {
+        set_error(std::string("dlr_dataset_load_binary: ") + path + ": checksum mismatch");
+        return DLR_E_PARSE;
+    }
+    if (ds->row_ptr[0] != 0 || ds->row_ptr[(size_t)n] != nnz) {
+        set_error(std::string("dlr_dataset_load_binary: ") + path + ": row offsets do not span the entries");
+        return DLR_E_PARSE;
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t a = ds->row_ptr[(size_t)i], b = ds->row_ptr[(size_t)i + 1];
+        bool rowok = a <= b && (ds->label[(size_t)i] == 0 || ds->label[(size_t)i] == 1);
+        for (int64_t k = a; rowok && k < b; ++k)
+            rowok = ds->col[(size_t)k] >= 0 && ds->col[(size_t)k] < D && (k == a || ds->col[(size_t)k] > ds->col[(size_t)k - 1]);
+        if (!rowok) {
+            set_error(std::string("dlr_dataset_load_binary: ") + path + ": invalid row " + std::to_string(i));
+            return DLR_E_PARSE;
+        }
+    }
+    *out = ds.release();
+    return DLR_OK;
+}
+
 // ------------------------------------------------------------------ batching
 
 extern "C" int64_t dlr_num_batches(int64_t n_rows, int64_t batch_size) {

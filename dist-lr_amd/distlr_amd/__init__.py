@@ -31,7 +31,8 @@ STAGE_MARGIN, STAGE_GRADIENT, STAGE_UPDATE = 0, 1, 2
 SYMBOLS = [
     "dlr_to_int", "dlr_to_float", "dlr_split",
     "dlr_dataset_load_libsvm", "dlr_dataset_from_csr", "dlr_dataset_generate", "dlr_dataset_generate_hashed",
-    "dlr_dataset_write_libsvm", "dlr_dataset_info", "dlr_dataset_view", "dlr_dataset_free",
+    "dlr_dataset_write_libsvm", "dlr_dataset_save_binary", "dlr_dataset_load_binary", "dlr_dataset_info",
+    "dlr_dataset_view", "dlr_dataset_free",
     "dlr_dense_from_dataset", "dlr_dense_from_array", "dlr_dense_generate", "dlr_dense_info", "dlr_dense_view",
     "dlr_dense_free",
     "dlr_num_batches", "dlr_batch_rows",
@@ -119,6 +120,8 @@ _sig("dlr_load_test_dense", C.c_int, P, P)
 _sig("dlr_set_residency", C.c_int, P, C.c_int)
 _sig("dlr_train_residency", C.c_int, P)
 _sig("dlr_dataset_write_libsvm", C.c_int, P, C.c_char_p, C.c_int)
+_sig("dlr_dataset_save_binary", C.c_int, P, C.c_char_p)
+_sig("dlr_dataset_load_binary", C.c_int, C.c_char_p, C.POINTER(P))
 _sig("dlr_dataset_info", C.c_int, P, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64))
 _sig("dlr_dataset_view", C.c_int, P, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P))
 _sig("dlr_dataset_free", None, P)
@@ -243,6 +246,37 @@ class Dataset:
 
     def write_libsvm(self, path: str, value_mode: int = 0) -> None:
         _check(lib.dlr_dataset_write_libsvm(self._h, path.encode(), value_mode))
+
+    def save_binary(self, path: str) -> None:
+        """Binary CSR cache (dlr_dataset_save_binary)."""
+        _check(lib.dlr_dataset_save_binary(self._h, path.encode()))
+
+    @classmethod
+    def load_binary(cls, path: str) -> "Dataset":
+        h = P()
+        _check(lib.dlr_dataset_load_binary(path.encode(), C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def load_cached(cls, path: str, num_feature_dim: int, nthreads: int = 0) -> "Dataset":
+        """A libsvm shard through its binary cache `path + '.dlrcsr'`: parsed
+        and cached on first use, reloaded while the cache is newer than the
+        text and was written for the same D."""
+        cache = path + ".dlrcsr"
+        if os.path.exists(cache) and os.path.getmtime(cache) >= os.path.getmtime(path):
+            try:
+                ds = cls.load_binary(cache)
+                if ds.info()[2] == num_feature_dim:
+                    return ds
+                ds.free()
+            except DLRError:
+                pass
+        ds = cls.load_libsvm(path, num_feature_dim, nthreads)
+        try:
+            ds.save_binary(cache)
+        except DLRError:
+            pass  # a read-only data dir still trains from the text
+        return ds
 
     def info(self) -> Tuple[int, int, int]:
         n, nnz, d = i64(), i64(), i64()

@@ -113,6 +113,12 @@ int dlr_dataset_generate_hashed(const dlr_hashed_spec *spec, dlr_dataset **out);
 /* Writes a dataset as libsvm text ("+1 idx:val ...", 1-based indices). */
 int dlr_dataset_write_libsvm(const dlr_dataset *ds, const char *path, int value_mode);
 
+/* Binary CSR cache: the parsed shard's four arrays with a checksum, so a
+ * large text shard is parsed once (SURVEY 8(f) ingest).  Loading verifies
+ * the checksum and the CSR invariants (DLR_E_PARSE otherwise). */
+int dlr_dataset_save_binary(const dlr_dataset *ds, const char *path);
+int dlr_dataset_load_binary(const char *path, dlr_dataset **out);
+
 int dlr_dataset_info(const dlr_dataset *ds, int64_t *n_rows, int64_t *nnz, int64_t *num_feature_dim);
 /* Borrowed views of the CSR arrays (valid until dlr_dataset_free). */
 int dlr_dataset_view(const dlr_dataset *ds, const int64_t **row_ptr, const int32_t **col, const float **val,
