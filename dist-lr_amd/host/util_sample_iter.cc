@@ -3,6 +3,8 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <stdexcept>
@@ -130,12 +132,34 @@ DataIter::DataIter(std::string filename, int num_feature_dim)
         }
     }
     dlr_dataset *ds = nullptr;
-    const int rc = dlr_dataset_load_libsvm(filename_.c_str(), num_feature_dim, 0, &ds);
-    if (rc == DLR_E_IO) {
-        shard_ = empty_shard(num_feature_dim);
-        return;
+    // DISTLR_CSR_CACHE=1: reuse <file>.dlrcsr (dlr_dataset_save_binary) when
+    // it is newer than the text and holds the same D; else parse and write it
+    const char *cc = getenv("DISTLR_CSR_CACHE");
+    const bool use_cache = cc && strcmp(cc, "1") == 0;
+    const std::string cache = filename_ + ".dlrcsr";
+    if (use_cache) {
+        struct stat cs;
+        if (stat(cache.c_str(), &cs) == 0 &&
+            (cs.st_mtim.tv_sec > st.st_mtim.tv_sec ||
+             (cs.st_mtim.tv_sec == st.st_mtim.tv_sec && cs.st_mtim.tv_nsec >= st.st_mtim.tv_nsec)) &&
+            dlr_dataset_load_binary(cache.c_str(), &ds) == DLR_OK) {
+            int64_t n = 0, nnz = 0, d = 0;
+            dlr_dataset_info(ds, &n, &nnz, &d);
+            if (d != num_feature_dim) {
+                dlr_dataset_free(ds);
+                ds = nullptr;
+            }
+        }
     }
-    if (rc != DLR_OK) throw std::runtime_error(std::string("DataIter: ") + dlr_last_error(nullptr));
+    if (!ds) {
+        const int rc = dlr_dataset_load_libsvm(filename_.c_str(), num_feature_dim, 0, &ds);
+        if (rc == DLR_E_IO) {
+            shard_ = empty_shard(num_feature_dim);
+            return;
+        }
+        if (rc != DLR_OK) throw std::runtime_error(std::string("DataIter: ") + dlr_last_error(nullptr));
+        if (use_cache) (void)dlr_dataset_save_binary(ds, cache.c_str());  // best effort (read-only dirs)
+    }
     shard_ = std::make_shared<Shard>(ds);
     std::lock_guard<std::mutex> g(g_cache_mu);
     g_cache[key] = shard_;

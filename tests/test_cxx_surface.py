@@ -63,3 +63,24 @@ def test_bad_index_is_an_error(tmp_path):
 
 def test_missing_file_is_empty_like_reference(tmp_path):
     assert tool("parse", tmp_path / "nope", 10) == "n 0\n"
+
+
+def test_dataiter_binary_cache(tmp_path):
+    # DISTLR_CSR_CACHE=1: the first DataIter writes <file>.dlrcsr, later ones
+    # load it -- the parse output stays byte-identical to the text parse
+    import shutil
+    src = os.path.join(GOLDEN, "quirks", "quirks.libsvm")
+    q = str(tmp_path / "q.libsvm")
+    shutil.copy(src, q)
+    plain = tool("parse", q, 10)
+    env = dict(os.environ, DISTLR_CSR_CACHE="1")
+    run = lambda: subprocess.run([TOOL, "parse", q, "10"], check=True, capture_output=True,  # noqa: E731
+                                 env=env).stdout.decode("latin-1")
+    assert run() == plain
+    assert os.path.exists(q + ".dlrcsr")
+    cached_mtime = os.path.getmtime(q + ".dlrcsr")
+    assert run() == plain
+    assert os.path.getmtime(q + ".dlrcsr") == cached_mtime  # reused, not rewritten
+    # a cache for another D is ignored (and replaced)
+    assert subprocess.run([TOOL, "parse", q, "12"], check=True, capture_output=True,
+                          env=env).stdout.decode("latin-1") == tool("parse", q, 12)
