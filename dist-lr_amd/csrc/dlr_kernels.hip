@@ -409,7 +409,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     const int P = pc.phases;
     const int64_t ng = (D + 63) / 64;
     const int64_t gfirst = (int64_t)blockIdx.x * (kGradWaves * NG) + wv;
-    unsigned bs[NG][2], off[NG][2], cnt[NG][2];
+    unsigned bs[NG][2], off[NG][2], cnt[NG][2], nblk[NG][2];
     float acc[NG], wj[NG];
     ushort4 rq[NG][2];
     float4 vq[NG][2];
@@ -426,6 +426,9 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
         for (int p = 0; p < 2; ++p) {
             const int64_t blk = gc * P + (p < P ? p : P - 1);
             bs[gi][p] = pc.base[blk];
+            // the block's entries rounded up to 4 (blocks are 4-aligned): a
+            // lane's first window slot 4*lane is an entry iff 4*lane < this
+            nblk[gi][p] = pc.base[blk + 1] - bs[gi][p];
             const unsigned hi = pc.ends[blk * 64 + lane];
             const unsigned lo = pc.ends[blk * 64 + (lane ? lane - 1 : 0)];
             off[gi][p] = lane ? lo : 0u;
@@ -482,14 +485,19 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
                 asm volatile("" ::: "memory");
             }
             if (gfirst + kGradWaves * gi >= ng) break;  // wave-uniform
-            const ushort4 r4 = rq[gi][p];
-            const float4 v4 = vq[gi][p];
-            float4 q;
-            q.x = s_r[r4.x] * v4.x;
-            q.y = s_r[r4.y] * v4.y;
-            q.z = s_r[r4.z] * v4.z;
-            q.w = s_r[r4.w] * v4.w;
-            *reinterpret_cast<float4 *>(s_p + lane * 4) = q;
+            // products of the block's entries only: the window's other slots
+            // (the next blocks' entries) are never read, so those lanes skip
+            // their residual gathers (LDS bank cycles) and the slab write
+            if ((unsigned)lane * 4 < nblk[gi][p]) {
+                const ushort4 r4 = rq[gi][p];
+                const float4 v4 = vq[gi][p];
+                float4 q;
+                q.x = s_r[r4.x] * v4.x;
+                q.y = s_r[r4.y] * v4.y;
+                q.z = s_r[r4.z] * v4.z;
+                q.w = s_r[r4.w] * v4.w;
+                *reinterpret_cast<float4 *>(s_p + lane * 4) = q;
+            }
             wave_sync();
             // this lane's column: cnt products in order from off.  The first
             // eight are read at immediate offsets from s_p + o (the slab is
