@@ -1292,6 +1292,7 @@ int dlr_sync(dlr_ctx *c) {
     if (!c) return DLR_E_ARG;
     HIPC(c, hipSetDevice(c->device));
     HIPC(c, hipStreamSynchronize(c->stream));
+    if (c->cstream) HIPC(c, hipStreamSynchronize(c->cstream));  // a streamed shard's batch copies
     return DLR_OK;
 }
 
