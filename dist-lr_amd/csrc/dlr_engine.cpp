@@ -88,7 +88,20 @@ struct TrainShard {
     void *crow = nullptr;
     float *cval = nullptr;
     std::vector<int64_t> coff;  // entry offset of each batch
+    // classic layout: entry-balanced wave schedules (DevCsc::wstart), per batch
+    // wsoff[b] .. wsoff[b+1]-1 in wsched (column starts, then D)
+    uint32_t *wsched = nullptr;
+    std::vector<int64_t> wsoff;
     int64_t bytes = 0;
+};
+
+// What the column-major builders read of a CSR shard (the caller's arrays,
+// or the same rows with relabeled columns).
+struct CsrView {
+    int64_t n_rows;
+    const int64_t *row_ptr;
+    const int32_t *col;
+    const float *val;
 };
 
 struct TestShard {
@@ -133,6 +146,11 @@ struct dlr_ctx {
     dlr::RankSizes rs{};
     // residency of the next dense training shard, and the streamed shard's
     // copy stream + slot events (created on first use)
+    // column relabeling of Zipf-skewed sparse shards: perm[j] = the internal
+    // id of column j (frequency order); empty = identity.  Device weights,
+    // gradients and shard columns are internal; every D-length host boundary
+    // (weights, pushed gradients) and the test shard's columns are mapped.
+    std::vector<int32_t> perm;
     int residency = DLR_RESIDENCY_AUTO;
     hipStream_t cstream = nullptr;
     hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
@@ -212,7 +230,7 @@ void free_train(dlr_ctx *c) {
                     (void *)t.w_col, (void *)t.w_val, (void *)t.w_label, (void *)t.cptr, t.crow, (void *)t.cval,
                     (void *)t.pbase, (void *)t.pends, (void *)t.prow, (void *)t.pval, (void *)t.tcols,
                     (void *)t.lcols, (void *)t.lcseg, (void *)t.lsptr, t.lrow, (void *)t.lval, (void *)t.lpart,
-                    (void *)t.dX, (void *)t.dpart})
+                    (void *)t.dX, (void *)t.dpart, (void *)t.wsched})
         dev_free(c, p);
     t = TrainShard();
 }
@@ -303,6 +321,105 @@ int coll_gather_f32(dlr_ctx *c, float v, std::vector<float> &out) {
     return DLR_OK;
 }
 
+// Sum of an int64 vector over the ranks (RCCL), in place.
+int coll_sum_i64(dlr_ctx *c, std::vector<int64_t> &v) {
+    if (!c->comm || v.empty()) return DLR_OK;
+    int64_t *d = nullptr;
+    int rc = dev_alloc(c, (void **)&d, v.size() * 8);
+    if (rc) return rc;
+    hipError_t e = hipMemcpyAsync(d, v.data(), v.size() * 8, hipMemcpyHostToDevice, c->stream);
+    ncclResult_t r =
+        e == hipSuccess ? ncclAllReduce(d, d, v.size(), ncclInt64, ncclSum, c->comm, c->stream) : ncclSuccess;
+    if (e == hipSuccess && r == ncclSuccess) e = hipMemcpyAsync(v.data(), d, v.size() * 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dev_free(c, d);
+    if (r != ncclSuccess) return fail(c, DLR_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    if (e != hipSuccess) return fail(c, DLR_E_HIP, std::string("coll_sum_i64: ") + hipGetErrorString(e));
+    return DLR_OK;
+}
+
+inline int64_t pid(const std::vector<int32_t> &p, int64_t j) { return p.empty() ? j : (int64_t)p[(size_t)j]; }
+
+// Frequency order of the columns of a sparse training shard, summed over
+// the ranks (every rank gets the same numbering): internal id k = the k-th
+// most frequent column (ties by id).  Returned empty (identity) unless
+// DLR_RELABEL=1 forces it or (default) the counts are Zipf-skewed -- the top
+// 1% of columns hold over half of the entries, as C3's hashed fields do --
+// when the hot weights then share cache lines in the margin's gathers.  A
+// pure renaming: every sum keeps its order, results are bitwise unchanged.
+int column_order(dlr_ctx *c, const dlr_dataset &ds, std::vector<int32_t> &np) {
+    np.clear();
+    const char *rl = getenv("DLR_RELABEL");
+    const int mode = rl ? atoi(rl) : -1;  // -1 auto, 0 off, 1 on
+    const int64_t D = c->D;
+    int64_t want = (mode == 1 || (mode < 0 && D >= 65536)) && D <= ((int64_t)1 << 25) ? 1 : 0;
+    int rc;
+    if ((rc = coll_max_i64(c, &want))) return rc;  // ranks agree before any collective below
+    if (!want) return DLR_OK;
+    std::vector<int64_t> cnt((size_t)D, 0);
+    {
+        const int nt = std::max(1, std::min(8, dlr::default_threads()));
+        std::vector<std::vector<int32_t>> part((size_t)nt);
+        std::vector<std::thread> th;
+        const int64_t nnz = (int64_t)ds.col.size();
+        for (int k = 0; k < nt; ++k)
+            th.emplace_back([&, k] {
+                std::vector<int32_t> &pc = part[(size_t)k];
+                pc.assign((size_t)D, 0);
+                for (int64_t e = nnz * k / nt; e < nnz * (k + 1) / nt; ++e) ++pc[(size_t)ds.col[(size_t)e]];
+            });
+        for (auto &x : th) x.join();
+        for (auto &pc : part)
+            for (int64_t j = 0; j < D; ++j) cnt[(size_t)j] += pc[(size_t)j];
+    }
+    if ((rc = coll_sum_i64(c, cnt))) return rc;
+    std::vector<uint64_t> key((size_t)D);
+    int64_t total = 0;
+    for (int64_t j = 0; j < D; ++j) {
+        total += cnt[(size_t)j];
+        const uint64_t cj = (uint64_t)std::min<int64_t>(cnt[(size_t)j], ((int64_t)1 << 38) - 1);
+        key[(size_t)j] = ((((uint64_t)1 << 38) - 1 - cj) << 25) | (uint64_t)j;  // count desc, id asc
+    }
+    std::sort(key.begin(), key.end());
+    if (mode < 0) {  // auto: relabel only skewed shards
+        const int64_t top = std::max<int64_t>(1, D / 100);
+        int64_t hot = 0;
+        for (int64_t k = 0; k < top; ++k) hot += cnt[(size_t)(key[(size_t)k] & (((uint64_t)1 << 25) - 1))];
+        if (2 * hot <= total) return DLR_OK;
+    }
+    np.assign((size_t)D, 0);
+    for (int64_t k = 0; k < D; ++k) np[(size_t)(key[(size_t)k] & (((uint64_t)1 << 25) - 1))] = (int32_t)k;
+    return DLR_OK;
+}
+
+// Re-express the device weights and a loaded sparse test shard's columns in
+// a new column numbering (load time only).
+int change_perm(dlr_ctx *c, std::vector<int32_t> &&np) {
+    if (np == c->perm) return DLR_OK;
+    const int64_t D = c->D;
+    std::vector<float> oldw((size_t)D), neww((size_t)D);
+    HIPC(c, hipMemcpyAsync(oldw.data(), c->w, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    for (int64_t j = 0; j < D; ++j) neww[(size_t)pid(np, j)] = oldw[(size_t)pid(c->perm, j)];
+    HIPC(c, hipMemcpyAsync(c->w, neww.data(), (size_t)D * 4, hipMemcpyHostToDevice, c->stream));
+    TestShard &t = c->test;
+    if (t.loaded && !t.dense && t.nnz > 0) {
+        std::vector<int32_t> inv;
+        if (!c->perm.empty()) {
+            inv.assign((size_t)D, 0);
+            for (int64_t j = 0; j < D; ++j) inv[(size_t)c->perm[(size_t)j]] = (int32_t)j;
+        }
+        std::vector<int32_t> col((size_t)t.nnz);
+        HIPC(c, hipMemcpyAsync(col.data(), t.col, (size_t)t.nnz * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPC(c, hipStreamSynchronize(c->stream));
+        for (auto &x : col) x = (int32_t)pid(np, inv.empty() ? x : inv[(size_t)x]);
+        HIPC(c, hipMemcpyAsync(t.col, col.data(), (size_t)t.nnz * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->perm = std::move(np);
+    return DLR_OK;
+}
+
 // Long columns of one batch, built beside the classic copy (see
 // dlr_kernels.hip "Long columns").
 template <typename RowT>
@@ -319,7 +436,7 @@ struct LongBatch {
 // (4-aligned starts); their pointer entry carries kLongFlag and their
 // segment in the classic copy is empty.
 template <typename RowT>
-void build_csc(const dlr_dataset &ds, const std::vector<dlr::BatchSpan> &plan, int64_t D,
+void build_csc(const CsrView &ds, const std::vector<dlr::BatchSpan> &plan, int64_t D,
                const std::vector<int64_t> &coff, std::vector<uint32_t> &cptr, std::vector<RowT> &crow,
                std::vector<float> &cval, int64_t long_min, std::vector<LongBatch<RowT>> &lb, int nthreads) {
     const int64_t nb = (int64_t)plan.size();
@@ -428,7 +545,7 @@ void for_batches(int64_t nb, int nthreads, Fn fn) {
 }
 
 // Counts of (column, phase) for batch sp; cnt has D*P entries.
-void pcsc_count(const dlr_dataset &ds, const dlr::BatchSpan &sp, const PcscBuild &pb, std::vector<uint32_t> &cnt) {
+void pcsc_count(const CsrView &ds, const dlr::BatchSpan &sp, const PcscBuild &pb, std::vector<uint32_t> &cnt) {
     std::fill(cnt.begin(), cnt.end(), 0u);
     const int64_t N = ds.n_rows;
     for (int64_t i = 0; i < sp.rows; ++i) {
@@ -439,7 +556,7 @@ void pcsc_count(const dlr_dataset &ds, const dlr::BatchSpan &sp, const PcscBuild
     }
 }
 
-bool pcsc_plan(const dlr_dataset &ds, const std::vector<dlr::BatchSpan> &plan, int64_t D, PcscBuild &pb,
+bool pcsc_plan(const CsrView &ds, const std::vector<dlr::BatchSpan> &plan, int64_t D, PcscBuild &pb,
                int nthreads) {
     const int64_t nb = (int64_t)plan.size();
     pb.size.assign((size_t)nb, 0);
@@ -464,7 +581,7 @@ bool pcsc_plan(const dlr_dataset &ds, const std::vector<dlr::BatchSpan> &plan, i
     return ok;
 }
 
-void pcsc_fill(const dlr_dataset &ds, const std::vector<dlr::BatchSpan> &plan, int64_t D, const PcscBuild &pb,
+void pcsc_fill(const CsrView &ds, const std::vector<dlr::BatchSpan> &plan, int64_t D, const PcscBuild &pb,
                const std::vector<int64_t> &poff, std::vector<uint32_t> &base, std::vector<uint8_t> &ends,
                std::vector<uint16_t> &row, std::vector<float> &val, int nthreads) {
     const int64_t nb = (int64_t)plan.size();
@@ -517,7 +634,7 @@ struct TouchedBatch {
     std::vector<float> val;
 };
 
-void touched_batch(const dlr_dataset &ds, const dlr::BatchSpan &sp, TouchedBatch &tb) {
+void touched_batch(const CsrView &ds, const dlr::BatchSpan &sp, TouchedBatch &tb) {
     const int64_t N = ds.n_rows;
     struct E {
         uint32_t col, row;
@@ -632,8 +749,13 @@ dlr::DevCsc csc_view(const dlr_ctx *c, int64_t b) {
     const TrainShard &t = c->train;
     const size_t esz = t.row16 ? 2 : 4;
     const size_t po = t.touched ? (size_t)t.tpoff[(size_t)b] : (size_t)b * (size_t)(c->D + 1);
-    return {t.cptr + po, (const char *)t.crow + esz * (size_t)t.coff[(size_t)b], t.cval + t.coff[(size_t)b],
-            t.row16};
+    dlr::DevCsc cs{t.cptr + po, (const char *)t.crow + esz * (size_t)t.coff[(size_t)b], t.cval + t.coff[(size_t)b],
+                   t.row16};
+    if (t.wsched) {
+        cs.wstart = t.wsched + t.wsoff[(size_t)b];
+        cs.nwaves = t.wsoff[(size_t)b + 1] - t.wsoff[(size_t)b] - 1;
+    }
+    return cs;
 }
 
 hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float lr, float C, bool fused) {
@@ -741,6 +863,12 @@ void dlr_destroy(dlr_ctx *ctx) {
 int dlr_set_weights(dlr_ctx *c, const float *w, int64_t D) {
     if (!c || !w || D != c->D) return fail(c, DLR_E_ARG, "dlr_set_weights: D mismatch");
     HIPC(c, hipSetDevice(c->device));
+    std::vector<float> tmp;
+    if (!c->perm.empty()) {  // internal column order
+        tmp.resize((size_t)D);
+        for (int64_t j = 0; j < D; ++j) tmp[(size_t)c->perm[(size_t)j]] = w[j];
+        w = tmp.data();
+    }
     HIPC(c, hipMemcpyAsync(c->w, w, (size_t)D * 4, hipMemcpyHostToDevice, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     return DLR_OK;
@@ -749,8 +877,15 @@ int dlr_set_weights(dlr_ctx *c, const float *w, int64_t D) {
 int dlr_get_weights(dlr_ctx *c, float *w, int64_t D) {
     if (!c || !w || D != c->D) return fail(c, DLR_E_ARG, "dlr_get_weights: D mismatch");
     HIPC(c, hipSetDevice(c->device));
-    HIPC(c, hipMemcpyAsync(w, c->w, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
+    if (c->perm.empty()) {
+        HIPC(c, hipMemcpyAsync(w, c->w, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPC(c, hipStreamSynchronize(c->stream));
+        return DLR_OK;
+    }
+    std::vector<float> tmp((size_t)D);
+    HIPC(c, hipMemcpyAsync(tmp.data(), c->w, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
+    for (int64_t j = 0; j < D; ++j) w[j] = tmp[(size_t)c->perm[(size_t)j]];
     return DLR_OK;
 }
 
@@ -806,9 +941,30 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
     if (!t.touched && cptr_bytes > 64.0 * (1ull << 30))
         return fail(c, DLR_E_NOMEM, "dlr_load_train: per-batch column pointers would need " +
                                         std::to_string((long long)(cptr_bytes / (1 << 20))) + " MiB");
+    // Column numbering (frequency order for skewed shards; identity otherwise)
+    // and the shard's columns in it.
+    std::vector<int32_t> mapped;
+    {
+        std::vector<int32_t> np;
+        if (!t.touched && (rc = column_order(c, *ds, np))) return rc;
+        if ((rc = change_perm(c, std::move(np)))) return rc;
+        if (!c->perm.empty()) {
+            mapped.resize(ds->col.size());
+            const int nt = dlr::default_threads();
+            std::vector<std::thread> th;
+            for (int k = 0; k < nt; ++k)
+                th.emplace_back([&, k] {
+                    const size_t n = mapped.size();
+                    for (size_t e = n * k / nt; e < n * (k + 1) / nt; ++e) mapped[e] = c->perm[(size_t)ds->col[e]];
+                });
+            for (auto &x : th) x.join();
+        }
+    }
+    const CsrView src{ds->n_rows, ds->row_ptr.data(), c->perm.empty() ? ds->col.data() : mapped.data(),
+                      ds->val.data()};
     // Shard CSR.
     if ((rc = upload(c, &t.row_ptr, ds->row_ptr.data(), (size_t)t.n_rows + 1))) return rc;
-    if ((rc = upload(c, &t.col, ds->col.data(), (size_t)t.nnz, kPad))) return rc;
+    if ((rc = upload(c, &t.col, src.col, (size_t)t.nnz, kPad))) return rc;
     if ((rc = upload(c, &t.val, ds->val.data(), (size_t)t.nnz, kPad))) return rc;
     {
         std::vector<float> lab(ds->label.begin(), ds->label.end());
@@ -828,7 +984,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         for (int64_t i = 0; i < sp.rows; ++i) {
             const int64_t r = (sp.first_row + i) % ds->n_rows;
             for (int64_t k = ds->row_ptr[(size_t)r]; k < ds->row_ptr[(size_t)r + 1]; ++k) {
-                cc.push_back(ds->col[(size_t)k]);
+                cc.push_back(src.col[(size_t)k]);
                 vv.push_back(ds->val[(size_t)k]);
             }
             rp[(size_t)i + 1] = (int64_t)cc.size();
@@ -854,7 +1010,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         pb.P = (int)((t.B + pb.R - 1) / pb.R);
         pb.groups = (D + 63) / 64;
         pb.pblocks = pb.groups * pb.P;
-        t.pcsc = pb.P <= 2 && pcsc_plan(*ds, t.plan, D, pb, nthreads);
+        t.pcsc = pb.P <= 2 && pcsc_plan(src, t.plan, D, pb, nthreads);
     }
     if (gk && strcmp(gk, "lds") == 0 && !t.pcsc)
         return fail(c, DLR_E_ARG, "dlr_load_train: DLR_GRAD_KERNEL=lds but the batches do not fit the LDS layout");
@@ -868,7 +1024,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         std::vector<uint8_t> ends((size_t)nb * (size_t)pb.pblocks * 64);
         std::vector<uint16_t> prow((size_t)total, 0);
         std::vector<float> pval((size_t)total, 0.0f);
-        pcsc_fill(*ds, t.plan, D, pb, t.poff, base, ends, prow, pval, nthreads);
+        pcsc_fill(src, t.plan, D, pb, t.poff, base, ends, prow, pval, nthreads);
         if ((rc = upload(c, &t.pbase, base.data(), base.size()))) return rc;
         if ((rc = upload(c, &t.pends, ends.data(), ends.size()))) return rc;
         if ((rc = upload(c, &t.prow, prow.data(), prow.size(), 256))) return rc;
@@ -878,7 +1034,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
     } else if (t.touched) {
         t.row16 = t.B <= 65536;
         std::vector<TouchedBatch> tbs((size_t)nb);
-        for_batches(nb, nthreads, [&](int64_t b) { touched_batch(*ds, t.plan[(size_t)b], tbs[(size_t)b]); });
+        for_batches(nb, nthreads, [&](int64_t b) { touched_batch(src, t.plan[(size_t)b], tbs[(size_t)b]); });
         t.tcoff.assign((size_t)nb + 1, 0);
         t.tpoff.assign((size_t)nb + 1, 0);
         t.tncols.assign((size_t)nb, 0);
@@ -988,19 +1144,52 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         if (t.row16) {
             std::vector<uint16_t> crow((size_t)total);
             std::vector<LongBatch<uint16_t>> lb;
-            build_csc(*ds, t.plan, D, t.coff, cptr, crow, cval, long_min, lb, nthreads);
+            build_csc(src, t.plan, D, t.coff, cptr, crow, cval, long_min, lb, nthreads);
             if ((rc = upload(c, (uint16_t **)&t.crow, crow.data(), crow.size(), kPad))) return rc;
             if ((rc = finish_long(lb))) return rc;
         } else {
             std::vector<uint32_t> crow((size_t)total);
             std::vector<LongBatch<uint32_t>> lb;
-            build_csc(*ds, t.plan, D, t.coff, cptr, crow, cval, long_min, lb, nthreads);
+            build_csc(src, t.plan, D, t.coff, cptr, crow, cval, long_min, lb, nthreads);
             if ((rc = upload(c, (uint32_t **)&t.crow, crow.data(), crow.size(), kPad))) return rc;
             if ((rc = finish_long(lb))) return rc;
         }
         if ((rc = upload(c, &t.cptr, cptr.data(), cptr.size()))) return rc;
         if ((rc = upload(c, &t.cval, cval.data(), cval.size(), kPad))) return rc;
-        csc_bytes = (int64_t)(cptr.size() * 4 + (total + kPad) * ((t.row16 ? 2 : 4) + 4)) + lbytes;
+        // Entry-balanced wave schedule: a wave takes consecutive columns until
+        // it has 64 or about one window (kWin entries) of them -- a column
+        // order with runs of long columns (frequency order) would otherwise
+        // give some waves 64 x thousands of entries.
+        {
+            std::vector<std::vector<uint32_t>> ws((size_t)nb);
+            for_batches(nb, nthreads, [&](int64_t b) {
+                const uint32_t *cp = cptr.data() + (size_t)b * (size_t)(D + 1);
+                std::vector<uint32_t> &v = ws[(size_t)b];
+                v.reserve((size_t)(D / 64 + 16));
+                v.push_back(0);
+                int64_t acc = 0;
+                int cols = 0;
+                for (int64_t j = 0; j < D; ++j) {
+                    const int64_t cj = (int64_t)(cp[j + 1] & 0x7FFFFFFFu) - (int64_t)(cp[j] & 0x7FFFFFFFu);
+                    if (cols == 64 || (cols > 0 && acc + cj > 1024)) {
+                        v.push_back((uint32_t)j);
+                        acc = 0;
+                        cols = 0;
+                    }
+                    acc += cj;
+                    ++cols;
+                }
+                v.push_back((uint32_t)D);
+            });
+            t.wsoff.assign((size_t)nb + 1, 0);
+            for (int64_t b = 0; b < nb; ++b) t.wsoff[(size_t)b + 1] = t.wsoff[(size_t)b] + (int64_t)ws[(size_t)b].size();
+            std::vector<uint32_t> all;
+            all.reserve((size_t)t.wsoff[(size_t)nb]);
+            for (auto &v : ws) all.insert(all.end(), v.begin(), v.end());
+            if ((rc = upload(c, &t.wsched, all.data(), all.size()))) return rc;
+            csc_bytes += (int64_t)all.size() * 4;
+        }
+        csc_bytes += (int64_t)(cptr.size() * 4 + (total + kPad) * ((t.row16 ? 2 : 4) + 4)) + lbytes;
     }
     // Residual buffer (padded to whole LDS phases for the LDS kernel).
     if (c->resid_cap < resid_need) {
@@ -1027,8 +1216,13 @@ int dlr_load_test(dlr_ctx *c, const dlr_dataset *ds) {
     t.n_rows = ds->n_rows;
     t.nnz = (int64_t)ds->col.size();
     int rc;
+    std::vector<int32_t> mapped;  // the training shard's column numbering
+    if (!c->perm.empty()) {
+        mapped.resize(ds->col.size());
+        for (size_t e = 0; e < mapped.size(); ++e) mapped[e] = c->perm[(size_t)ds->col[e]];
+    }
     if ((rc = upload(c, &t.row_ptr, ds->row_ptr.data(), (size_t)t.n_rows + 1))) return rc;
-    if ((rc = upload(c, &t.col, ds->col.data(), (size_t)t.nnz, kPad))) return rc;
+    if ((rc = upload(c, &t.col, c->perm.empty() ? ds->col.data() : mapped.data(), (size_t)t.nnz, kPad))) return rc;
     if ((rc = upload(c, &t.val, ds->val.data(), (size_t)t.nnz, kPad))) return rc;
     std::vector<float> lab(ds->label.begin(), ds->label.end());
     if ((rc = upload(c, &t.label, lab.data(), lab.size()))) return rc;
@@ -1053,6 +1247,8 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
     HIPC(c, hipStreamSynchronize(c->stream));
     free_train(c);
     free_touched_bufs(c);
+    int rc;
+    if ((rc = change_perm(c, {}))) return rc;  // dense rows are in the original column order
     TrainShard &t = c->train;
     t.dense = true;
     t.n_rows = ds->n_rows;
@@ -1061,7 +1257,6 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
     const int64_t D = c->D;
     const char *dg = getenv("DLR_DENSE_GRAD");
     t.dblocked = dg ? strcmp(dg, "blocked") == 0 : (t.B * D > ((int64_t)1 << 24));
-    int rc;
     // Residency: device-resident unless asked to stream, or (auto) the rows
     // would not leave room in HBM (20M x 4096 fp32 = 328 GB
     // on one 288 GB GPU).  Streamed rows are staged per batch over PCIe.
@@ -1117,6 +1312,10 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
 int dlr_load_test_dense(dlr_ctx *c, const dlr_dense *ds) {
     if (!c || !ds) return fail(c, DLR_E_ARG, "dlr_load_test_dense: bad argument");
     if (ds->D != c->D) return fail(c, DLR_E_ARG, "dlr_load_test_dense: dataset D != context D");
+    if (!c->perm.empty())
+        return fail(c, DLR_E_STATE,
+                    "dlr_load_test_dense: the loaded sparse training shard uses relabeled columns (DLR_RELABEL=0 "
+                    "keeps the original order)");
     HIPC(c, hipSetDevice(c->device));
     HIPC(c, hipStreamSynchronize(c->stream));
     free_test(c);
@@ -1246,8 +1445,15 @@ int dlr_worker_gradient(dlr_ctx *c, int64_t b, float C, float *grad_out, int64_t
     } else {
         HIPC(c, launch_gradient(c, b, bt.rows, c->g, 0.0f, C, false));
     }
-    HIPC(c, hipMemcpyAsync(grad_out, c->g, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
+    if (c->perm.empty()) {
+        HIPC(c, hipMemcpyAsync(grad_out, c->g, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPC(c, hipStreamSynchronize(c->stream));
+        return DLR_OK;
+    }
+    std::vector<float> tmp((size_t)D);
+    HIPC(c, hipMemcpyAsync(tmp.data(), c->g, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
+    for (int64_t j = 0; j < D; ++j) grad_out[j] = tmp[(size_t)c->perm[(size_t)j]];
     return DLR_OK;
 }
 
@@ -1255,6 +1461,14 @@ int dlr_server_apply(dlr_ctx *c, const float *grads, int W, int64_t D, float lr,
     if (!c || !grads || W <= 0 || D != c->D || mode < 0 || mode > 2)
         return fail(c, DLR_E_ARG, "dlr_server_apply: bad argument");
     HIPC(c, hipSetDevice(c->device));
+    std::vector<float> tmp;
+    if (!c->perm.empty()) {  // the pushes in the internal column order
+        tmp.resize((size_t)W * (size_t)D);
+        for (int r = 0; r < W; ++r)
+            for (int64_t j = 0; j < D; ++j)
+                tmp[(size_t)r * (size_t)D + (size_t)c->perm[(size_t)j]] = grads[(size_t)r * (size_t)D + (size_t)j];
+        grads = tmp.data();
+    }
     float *buf = nullptr;
     int rc = dev_alloc(c, (void **)&buf, (size_t)W * (size_t)D * 4);
     if (rc) return rc;
@@ -1381,6 +1595,11 @@ int dlr_train_residency(dlr_ctx *c) {
     if (!c) return DLR_E_ARG;
     if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_residency: no training shard loaded");
     return c->train.streamed ? DLR_RESIDENCY_STREAM : DLR_RESIDENCY_DEVICE;
+}
+
+int dlr_train_relabeled(dlr_ctx *c) {
+    if (!c) return DLR_E_ARG;
+    return c->perm.empty() ? 0 : 1;
 }
 
 int dlr_train_layout(dlr_ctx *c) {

@@ -26,6 +26,11 @@ struct DevCsc {
     const void *row;
     const float *val;
     bool row16;
+    // classic layout: wave k sums columns [wstart[k], wstart[k+1]) -- at most
+    // 64 columns and about one window of entries (built at load); null:
+    // 64 consecutive columns per wave
+    const uint32_t *wstart = nullptr;
+    int64_t nwaves = 0;
 };
 
 // Long columns of one batch (classic layout): ncols columns cols[] (their

@@ -258,13 +258,21 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad(DevCsc cs, const RowT *_
                                                         float C) {
     __shared__ float s_p[kWaves][kWin];
     const int lane = threadIdx.x & (kWave - 1);
-    const int wv = threadIdx.x / kWave;
-    const int64_t j0 = ((int64_t)blockIdx.x * kWaves + wv) * kWave;
-    if (j0 >= D) return;  // wave-uniform
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t wid = (int64_t)blockIdx.x * kWaves + wv;
+    int64_t j0, jl;
+    if (cs.wstart) {  // entry-balanced schedule (frequency-ordered columns are not)
+        if (wid >= cs.nwaves) return;  // wave-uniform
+        j0 = cs.wstart[wid];
+        jl = cs.wstart[wid + 1];
+    } else {
+        j0 = wid * kWave;
+        if (j0 >= D) return;  // wave-uniform
+        jl = min(j0 + kWave, D);
+    }
     const int64_t j = j0 + lane;
-    const bool valid = j < D;
+    const bool valid = j < jl;
     const float wj = valid ? w[j] : 0.0f;
-    const int64_t jl = min(j0 + kWave, D);
     // bit 31 of ptr[j] marks a LONG column: its entries live in the long
     // arrays (k_long_segments / k_long_combine update it), its segment here
     // is empty
@@ -1017,7 +1025,8 @@ hipError_t launch_predict(const DevBatch &bt, const float *w, unsigned long long
 hipError_t launch_grad(const DevCsc &cs, int64_t D, const float *resid, float *w, float *gout, int64_t B, float lr,
                        float C, bool fused, hipStream_t s) {
     if (D <= 0) return hipSuccess;
-    const unsigned grid = grid_for(D, kWaves * kWave);
+    const unsigned grid = cs.wstart ? (unsigned)((cs.nwaves + kWaves - 1) / kWaves) : grid_for(D, kWaves * kWave);
+    if (grid == 0) return hipSuccess;
     const dim3 blk(kWaves * kWave);
     const float Bf = (float)B;
     const double Bd = (double)B;

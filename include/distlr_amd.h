@@ -290,6 +290,15 @@ int dlr_stage_time(dlr_ctx *ctx, int stage, int64_t first_batch, int64_t count, 
 #define DLR_LAYOUT_TOUCHED 2
 int dlr_train_layout(dlr_ctx *ctx);
 
+/* 1 when the loaded sparse training shard's columns are relabeled in
+ * frequency order (Zipf-skewed shards such as BASELINE C3: the hot weights
+ * then share cache lines in the margin's gathers), else 0.  Chosen at load
+ * over the ranks' summed column counts (DLR_RELABEL=0|1 forces it).  A pure
+ * renaming: every sum keeps its order and results are bitwise unchanged;
+ * weights, pushed gradients and test shards keep the original numbering at
+ * this API (a dense test shard cannot be loaded beside a relabeled one). */
+int dlr_train_relabeled(dlr_ctx *ctx);
+
 /* Device bytes resident for the loaded shards (for reporting). */
 int dlr_memory_info(dlr_ctx *ctx, int64_t *train_bytes, int64_t *test_bytes);
 
