@@ -69,6 +69,7 @@ struct TrainShard {
     // long columns of the classic layout (per batch: lcoff cols, lsoff
     // segments, leoff entries; cseg/sptr have one extra entry per batch)
     bool any_long = false;
+    uint32_t *lsched = nullptr;  // long chunks by first row (lsoff offsets, one pad entry per batch)
     uint32_t *lcols = nullptr, *lcseg = nullptr, *lsptr = nullptr;
     void *lrow = nullptr;
     float *lval = nullptr, *lpart = nullptr;
@@ -229,7 +230,7 @@ void free_train(dlr_ctx *c) {
     for (void *p : {(void *)t.row_ptr, (void *)t.col, (void *)t.val, (void *)t.label, (void *)t.w_row_ptr,
                     (void *)t.w_col, (void *)t.w_val, (void *)t.w_label, (void *)t.cptr, t.crow, (void *)t.cval,
                     (void *)t.pbase, (void *)t.pends, (void *)t.prow, (void *)t.pval, (void *)t.tcols,
-                    (void *)t.lcols, (void *)t.lcseg, (void *)t.lsptr, t.lrow, (void *)t.lval, (void *)t.lpart,
+                    (void *)t.lcols, (void *)t.lcseg, (void *)t.lsptr, t.lrow, (void *)t.lval, (void *)t.lpart, (void *)t.lsched,
                     (void *)t.dX, (void *)t.dpart, (void *)t.wsched})
         dev_free(c, p);
     t = TrainShard();
@@ -776,9 +777,10 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
     const int64_t nl = t.lcoff[bb + 1] - t.lcoff[bb];
     if (nl == 0) return hipSuccess;
     const size_t esz = t.row16 ? 2 : 4;
-    const dlr::DevLong lg{t.lcols + t.lcoff[bb], t.lcseg + (t.lcoff[bb] + (int64_t)b), t.lsptr + t.lsoff[bb],
-                          (const char *)t.lrow + esz * (size_t)t.leoff[bb], t.lval + t.leoff[bb], nl,
-                          t.lsoff[bb + 1] - t.lsoff[bb] - 1, t.row16};
+    dlr::DevLong lg{t.lcols + t.lcoff[bb], t.lcseg + (t.lcoff[bb] + (int64_t)b), t.lsptr + t.lsoff[bb],
+                    (const char *)t.lrow + esz * (size_t)t.leoff[bb], t.lval + t.leoff[bb], nl,
+                    t.lsoff[bb + 1] - t.lsoff[bb] - 1, t.row16};
+    if (t.lsched) lg.sched = t.lsched + t.lsoff[bb];
     return dlr::launch_grad_long(lg, B, c->resid, c->w, gout, t.lpart, lr, C, fused, c->stream);
 }
 
@@ -1119,10 +1121,19 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             }
             t.any_long = t.lcoff[(size_t)nb] > 0;
             if (!t.any_long) return DLR_OK;
-            std::vector<uint32_t> cols, cseg, sptr;
+            std::vector<uint32_t> cols, cseg, sptr, sched;
             std::vector<RowT> row;
             std::vector<float> val;
             for (auto &L : lb) {
+                // chunk schedule: by first row (stable), padded to sptr's length
+                const size_t ns = L.sptr.empty() ? 0 : L.sptr.size() - 1;
+                std::vector<uint32_t> order(ns);
+                for (size_t k = 0; k < ns; ++k) order[k] = (uint32_t)k;
+                std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+                    return L.row[L.sptr[x]] < L.row[L.sptr[y]];
+                });
+                sched.insert(sched.end(), order.begin(), order.end());
+                if (!L.sptr.empty()) sched.push_back(0);
                 cols.insert(cols.end(), L.cols.begin(), L.cols.end());
                 cseg.insert(cseg.end(), L.cseg.begin(), L.cseg.end());
                 sptr.insert(sptr.end(), L.sptr.begin(), L.sptr.end());
@@ -1134,6 +1145,9 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             if ((r = upload(c, &t.lcols, cols.data(), cols.size()))) return r;
             if ((r = upload(c, &t.lcseg, cseg.data(), cseg.size()))) return r;
             if ((r = upload(c, &t.lsptr, sptr.data(), sptr.size()))) return r;
+            if (!(getenv("DLR_LONG_SCHED") && strcmp(getenv("DLR_LONG_SCHED"), "0") == 0) &&
+                (r = upload(c, &t.lsched, sched.data(), sched.size())))
+                return r;
             if ((r = upload(c, (RowT **)&t.lrow, row.data(), row.size(), dlr::kLongChunk))) return r;
             if ((r = upload(c, &t.lval, val.data(), val.size(), dlr::kLongChunk))) return r;
             if ((r = dev_alloc(c, (void **)&t.lpart, (size_t)maxseg * 4))) return r;

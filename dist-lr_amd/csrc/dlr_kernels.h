@@ -47,6 +47,9 @@ struct DevLong {
     const float *val;
     int64_t ncols, nseg;
     bool row16;
+    // chunks in order of their first row (null: chunk order): the chunks in
+    // flight at once then gather from a narrow band of the residuals
+    const uint32_t *sched = nullptr;
 };
 
 // One batch column-major, PHASE-SPLIT for the LDS-resident gradient

@@ -312,22 +312,27 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad(DevCsc cs, const RowT *_
 
 template <typename RowT>
 __global__ __launch_bounds__(256) void k_long_segments(const uint32_t *__restrict__ sptr, int64_t nseg,
+                                                       const uint32_t *__restrict__ sched,
                                                        const RowT *__restrict__ row, const float *__restrict__ val,
                                                        const float *__restrict__ resid, float *__restrict__ part) {
     using RV = typename Vec4<RowT>::type;
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wpb = blockDim.x / kWave;
     const int64_t nw = (int64_t)gridDim.x * wpb;
-    for (int64_t s = (int64_t)blockIdx.x * wpb + threadIdx.x / kWave; s < nseg; s += nw) {  // wave-uniform
+    for (int64_t k = (int64_t)blockIdx.x * wpb + threadIdx.x / kWave; k < nseg; k += nw) {  // wave-uniform
+        const int64_t s = sched ? (int64_t)sched[k] : k;
         const uint32_t a = sptr[s], b = sptr[s + 1];  // a 4-aligned; b - a <= kLongChunk (+3 padding)
         const uint32_t e = a + (uint32_t)lane * 4;      // arrays padded by kLongChunk entries
         const RV r4 = *reinterpret_cast<const RV *>(row + e);
         const float4 v4 = *reinterpret_cast<const float4 *>(val + e);
-        float x0 = 0.0f, x1 = 0.0f, x2 = 0.0f, x3 = 0.0f;
-        if (e < b) x0 = resid[r4.x] * v4.x;
-        if (e + 1 < b) x1 = resid[r4.y] * v4.y;
-        if (e + 2 < b) x2 = resid[r4.z] * v4.z;
-        if (e + 3 < b) x3 = resid[r4.w] * v4.w;
+        // gathers unconditional (past the chunk the rows are the next
+        // chunk's or padding: valid indices), masked after -- a load in a
+        // divergent branch makes the compiler wait at the join
+        const float g0 = resid[r4.x], g1 = resid[r4.y], g2 = resid[r4.z], g3 = resid[r4.w];
+        const float x0 = e < b ? g0 * v4.x : 0.0f;
+        const float x1 = e + 1 < b ? g1 * v4.y : 0.0f;
+        const float x2 = e + 2 < b ? g2 * v4.z : 0.0f;
+        const float x3 = e + 3 < b ? g3 * v4.w : 0.0f;
         float t = x0 + x1;
         t = t + x2;
         t = t + x3;
@@ -1161,10 +1166,10 @@ hipError_t launch_grad_long(const DevLong &lg, int64_t B, const float *resid, fl
     if (lg.ncols <= 0) return hipSuccess;
     const unsigned sgrid = (unsigned)std::min<int64_t>((lg.nseg + 3) / 4, 256 * 16);  // a wave per chunk
     if (lg.row16)
-        hipLaunchKernelGGL(k_long_segments<uint16_t>, dim3(sgrid), dim3(256), 0, s, lg.sptr, lg.nseg,
+        hipLaunchKernelGGL(k_long_segments<uint16_t>, dim3(sgrid), dim3(256), 0, s, lg.sptr, lg.nseg, lg.sched,
                            static_cast<const uint16_t *>(lg.row), lg.val, resid, part);
     else
-        hipLaunchKernelGGL(k_long_segments<uint32_t>, dim3(sgrid), dim3(256), 0, s, lg.sptr, lg.nseg,
+        hipLaunchKernelGGL(k_long_segments<uint32_t>, dim3(sgrid), dim3(256), 0, s, lg.sptr, lg.nseg, lg.sched,
                            static_cast<const uint32_t *>(lg.row), lg.val, resid, part);
     const float Bf = (float)B;
     const double Bd = (double)B;
