@@ -49,6 +49,16 @@ __global__ __launch_bounds__(256) void mb_empty(float *out) {
     if (threadIdx.x == 0 && blockIdx.x == 0 && out[0] == 12345.0f) out[1] = 1.0f;
 }
 
+// Streams n4 float4s (grid-stride) to evict L2 and the Infinity Cache.
+__global__ __launch_bounds__(256) void mb_flush(const float4 *buf, int64_t n4, float *out) {
+    float acc = 0.f;
+    for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n4; t += (int64_t)gridDim.x * 256) {
+        const float4 v = buf[t];
+        acc += v.x + v.y + v.z + v.w;
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
 __global__ __launch_bounds__(256) void mb_stream(const int4 *idx, const float4 *val, float *out, int64_t n4) {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= n4) return;
@@ -1419,7 +1429,32 @@ int main(int argc, char **argv) {
             }
             CK(hipFree(d_o));
         }
-        for (int it = 0; it < 20; ++it) CK(dlr::launch_grad_lds(pc, D, B, d_rp, d_w, d_g2, 0.2f, 1.0f, false, 0));
+        {   // cold: a 1 GiB stream through L2 / the Infinity Cache before every launch
+            const int64_t fl4 = (int64_t)1 << 26;  // float4s = 1 GiB
+            float4 *fb = nullptr;
+            float *fo = nullptr;
+            CK(hipMalloc(&fb, fl4 * 16));
+            CK(hipMemset(fb, 0, fl4 * 16));
+            CK(hipMalloc(&fo, 1 << 22));
+            hipEvent_t ea, eb;
+            CK(hipEventCreate(&ea));
+            CK(hipEventCreate(&eb));
+            double tot = 0;
+            const int cr = 20;
+            for (int it = 0; it < cr; ++it) {
+                hipLaunchKernelGGL(mb_flush, dim3(4096), dim3(256), 0, 0, (const float4 *)fb, fl4, fo);
+                CK(hipEventRecord(ea, 0));
+                CK(dlr::launch_grad_lds(pc, D, B, d_rp, d_w, d_g2, 0.2f, 1.0f, false, 0));
+                CK(hipEventRecord(eb, 0));
+                CK(hipEventSynchronize(eb));
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, ea, eb));
+                tot += ms;
+            }
+            printf("K3 production lds, cold MALL %8.2f us\n", tot * 1000.0 / cr);
+            CK(hipFree(fb));
+            CK(hipFree(fo));
+        }
         CK(hipDeviceSynchronize());
         std::vector<unsigned long long> st((size_t)G * 8);
         CK(hipMemcpy(st.data(), d_st, (size_t)G * 8 * 8, hipMemcpyDeviceToHost));
