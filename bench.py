@@ -103,12 +103,13 @@ def parse_args():
     return args
 
 
-def alg_bytes_per_step(B: int, nnz: float, D: int, dense: bool = False) -> int:
+def alg_bytes_per_step(B: int, nnz: float, D: int, dense: bool = False, unit: bool = False) -> int:
     """sparse 8*nnz + 8 bytes per sample (int32 col + fp32
     val per nnz; row offset + label per row), dense 4*D + 4 (the row + its
     label), + 8*D/B per sample (dense-L2 weight read + write), times the B
-    samples of one step."""
-    per = 4 * D + 4 if dense else 8 * nnz + 8
+    samples of one step.  A unit-valued shard (every value 1.0f: C3, C5)
+    has no values to read: 4*nnz + 8."""
+    per = 4 * D + 4 if dense else (4 if unit else 8) * nnz + 8
     return int(round(B * per + 8 * D))
 
 
@@ -245,7 +246,8 @@ def main():
     avg_us = {k: (ms / n * 1000.0 if n else 0.0) for k, (ms, n) in kt.items()}
     # the step's kernels: stage averages, plus the key-range merge (N>1)
     kern_us = sum(stage_us.values()) + (avg_us["merge"] if world > 1 and layout != "touched" else 0.0)
-    step_bytes = alg_bytes_per_step(B_eff, nnz_avg, D, args.kind == "dense")
+    unit = args.kind != "dense" and eng.train_unit_values()
+    step_bytes = alg_bytes_per_step(B_eff, nnz_avg, D, args.kind == "dense", unit)
     achieved = step_bytes / (kern_us * 1e-6) / 1e9 if kern_us > 0 else 0.0
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -313,6 +315,7 @@ def main():
             "config": {"workload": f"{args.label}: {args.rows} rows/GPU x {D} features, {args.nnz} nnz/row, "
                                    f"batch {B}, sync SGD lr {args.lr}, C=1",
                        "name": args.config, "gradient_layout": layout,
+                       "values": "unit (all 1.0f, not stored)" if unit else "fp32",
                        "rows_per_gpu": args.rows, "num_feature_dim": D, "nnz_per_row": args.nnz,
                        "batch_size": B, "parallelism": f"dp{world}"},
             "roofline": roofline,

@@ -36,6 +36,9 @@ struct DeviceBuf {
 
 struct TrainShard {
     bool loaded = false;
+    // every value is 1.0f (one-hot / binary features): no value arrays are
+    // stored and the kernels' UNIT variants run (dlr_kernels.h DevBatch)
+    bool unit = false;
     int64_t n_rows = 0, nnz = 0, B = 0;
     std::vector<dlr::BatchSpan> plan;
     // shard CSR
@@ -112,7 +115,7 @@ struct TestShard {
     int64_t n_rows = 0, nnz = 0;
     int64_t *row_ptr = nullptr;
     int32_t *col = nullptr;
-    float *val = nullptr;
+    float *val = nullptr;  // null: unit values (TrainShard::unit)
     float *label = nullptr;
     int grid = 0;
     int64_t bytes = 0;
@@ -435,11 +438,13 @@ struct LongBatch {
 // segment lists its rows in the order lr.cc:37 visits them.  Columns with
 // more than long_min entries (0: none) go to `lb` in chunks of kLongChunk
 // (4-aligned starts); their pointer entry carries kLongFlag and their
-// segment in the classic copy is empty.
+// segment in the classic copy is empty.  unit: no values are written (cval
+// and the long values stay empty).
 template <typename RowT>
 void build_csc(const CsrView &ds, const std::vector<dlr::BatchSpan> &plan, int64_t D,
                const std::vector<int64_t> &coff, std::vector<uint32_t> &cptr, std::vector<RowT> &crow,
-               std::vector<float> &cval, int64_t long_min, std::vector<LongBatch<RowT>> &lb, int nthreads) {
+               std::vector<float> &cval, int64_t long_min, std::vector<LongBatch<RowT>> &lb, bool unit,
+               int nthreads) {
     const int64_t nb = (int64_t)plan.size();
     const int64_t N = ds.n_rows;
     lb.assign((size_t)nb, LongBatch<RowT>());
@@ -470,14 +475,18 @@ void build_csc(const CsrView &ds, const std::vector<dlr::BatchSpan> &plan, int64
                 uint32_t *ptr = cptr.data() + (size_t)b * (size_t)(D + 1);
                 ptr[0] = 0;
                 uint32_t lat = 0;  // long-array cursor
+                uint32_t pad = 0;  // padding entries of the previous long column
                 for (int64_t j = 0; j < D; ++j) {
                     const uint32_t c = cnt[(size_t)j + 1];
                     if (any_long && is_long[(size_t)j]) {
                         ptr[j + 1] = ptr[j];
                         L.cols.push_back((uint32_t)j);
                         L.cseg.push_back((uint32_t)L.sptr.size());
-                        for (uint32_t o = 0; o < c; o += dlr::kLongChunk) L.sptr.push_back(lat + o);
+                        // a start is 4-aligned; its low bits carry the previous
+                        // column's padding count (DevLong)
+                        for (uint32_t o = 0; o < c; o += dlr::kLongChunk) L.sptr.push_back((lat + o) | (o ? 0u : pad));
                         cnt[(size_t)j + 1] = lat;  // long cursor
+                        pad = ((c + 3) & ~3u) - c;
                         lat += (c + 3) & ~3u;
                     } else {
                         ptr[j + 1] = ptr[j] + c;
@@ -489,16 +498,16 @@ void build_csc(const CsrView &ds, const std::vector<dlr::BatchSpan> &plan, int64
                 // its <= 3 padding entries (row 0, value 0), whose products
                 // are +-0 and leave a sum unchanged.
                 L.cseg.push_back((uint32_t)L.sptr.size());
-                L.sptr.push_back(lat);
+                L.sptr.push_back(lat | pad);
                 if (any_long) {
                     L.row.assign((size_t)lat + dlr::kLongChunk, 0);
-                    L.val.assign((size_t)lat + dlr::kLongChunk, 0.0f);
+                    if (!unit) L.val.assign((size_t)lat + dlr::kLongChunk, 0.0f);
                 }
                 // cursors: short columns in the classic copy, long ones in L
                 for (int64_t j = 0; j < D; ++j)
                     if (!(any_long && is_long[(size_t)j])) cnt[(size_t)j + 1] = ptr[j];
                 RowT *rr = crow.data() + coff[(size_t)b];
-                float *vv = cval.data() + coff[(size_t)b];
+                float *vv = unit ? nullptr : cval.data() + coff[(size_t)b];
                 for (int64_t i = 0; i < sp.rows; ++i) {
                     const int64_t r = (sp.first_row + i) % N;
                     for (int64_t k = ds.row_ptr[(size_t)r]; k < ds.row_ptr[(size_t)r + 1]; ++k) {
@@ -506,10 +515,10 @@ void build_csc(const CsrView &ds, const std::vector<dlr::BatchSpan> &plan, int64
                         const uint32_t pos = cnt[(size_t)cj + 1]++;
                         if (any_long && is_long[(size_t)cj]) {
                             L.row[pos] = (RowT)i;
-                            L.val[pos] = ds.val[(size_t)k];
+                            if (!unit) L.val[pos] = ds.val[(size_t)k];
                         } else {
                             rr[pos] = (RowT)i;
-                            vv[pos] = ds.val[(size_t)k];
+                            if (!unit) vv[pos] = ds.val[(size_t)k];
                         }
                     }
                 }
@@ -663,6 +672,35 @@ void touched_batch(const CsrView &ds, const dlr::BatchSpan &sp, TouchedBatch &tb
     tb.ptr.push_back((uint32_t)es.size());
 }
 
+// True when every value is exactly 1.0f (one-hot / binary features, e.g.
+// a9a and Criteo-style hashed fields): fl32(t * 1.0f) == t, so the UNIT
+// kernels that never read values give the same bits.  DLR_UNIT_VALUES=0
+// keeps the value arrays (A/B and tests).
+bool unit_values(const std::vector<float> &val) {
+    const char *env = getenv("DLR_UNIT_VALUES");  // read at every load (tests switch it)
+    if ((env && strcmp(env, "0") == 0) || val.empty()) return false;
+    const size_t n = val.size();
+    const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)dlr::default_threads(), n >> 20));
+    std::atomic<bool> all{true};
+    std::vector<std::thread> th;
+    for (int k = 0; k < nt; ++k)
+        th.emplace_back([&, k] {
+            const uint32_t *v = reinterpret_cast<const uint32_t *>(val.data());
+            for (size_t e = n * k / nt; e < n * (k + 1) / nt; e += 4096) {
+                if (!all.load(std::memory_order_relaxed)) return;
+                const size_t end = std::min(n * (k + 1) / nt, e + 4096);
+                uint32_t acc = 0;
+                for (size_t i = e; i < end; ++i) acc |= v[i] ^ 0x3F800000u;
+                if (acc) {
+                    all = false;
+                    return;
+                }
+            }
+        });
+    for (auto &x : th) x.join();
+    return all;
+}
+
 dlr::DevBatch batch_view(const dlr_ctx *c, int64_t b) {
     const TrainShard &t = c->train;
     const dlr::BatchSpan &sp = t.plan[(size_t)b];
@@ -750,8 +788,8 @@ dlr::DevCsc csc_view(const dlr_ctx *c, int64_t b) {
     const TrainShard &t = c->train;
     const size_t esz = t.row16 ? 2 : 4;
     const size_t po = t.touched ? (size_t)t.tpoff[(size_t)b] : (size_t)b * (size_t)(c->D + 1);
-    dlr::DevCsc cs{t.cptr + po, (const char *)t.crow + esz * (size_t)t.coff[(size_t)b], t.cval + t.coff[(size_t)b],
-                   t.row16};
+    dlr::DevCsc cs{t.cptr + po, (const char *)t.crow + esz * (size_t)t.coff[(size_t)b],
+                   t.cval ? t.cval + t.coff[(size_t)b] : nullptr, t.row16};
     if (t.wsched) {
         cs.wstart = t.wsched + t.wsoff[(size_t)b];
         cs.nwaves = t.wsoff[(size_t)b + 1] - t.wsoff[(size_t)b] - 1;
@@ -778,7 +816,7 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
     if (nl == 0) return hipSuccess;
     const size_t esz = t.row16 ? 2 : 4;
     dlr::DevLong lg{t.lcols + t.lcoff[bb], t.lcseg + (t.lcoff[bb] + (int64_t)b), t.lsptr + t.lsoff[bb],
-                    (const char *)t.lrow + esz * (size_t)t.leoff[bb], t.lval + t.leoff[bb], nl,
+                    (const char *)t.lrow + esz * (size_t)t.leoff[bb], t.lval ? t.lval + t.leoff[bb] : nullptr, nl,
                     t.lsoff[bb + 1] - t.lsoff[bb] - 1, t.row16};
     if (t.lsched) lg.sched = t.lsched + t.lsoff[bb];
     return dlr::launch_grad_long(lg, B, c->resid, c->w, gout, t.lpart, lr, C, fused, c->stream);
@@ -964,10 +1002,11 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
     }
     const CsrView src{ds->n_rows, ds->row_ptr.data(), c->perm.empty() ? ds->col.data() : mapped.data(),
                       ds->val.data()};
-    // Shard CSR.
+    // Shard CSR (no value array for a unit-valued shard).
+    t.unit = unit_values(ds->val);
     if ((rc = upload(c, &t.row_ptr, ds->row_ptr.data(), (size_t)t.n_rows + 1))) return rc;
     if ((rc = upload(c, &t.col, src.col, (size_t)t.nnz, kPad))) return rc;
-    if ((rc = upload(c, &t.val, ds->val.data(), (size_t)t.nnz, kPad))) return rc;
+    if (!t.unit && (rc = upload(c, &t.val, ds->val.data(), (size_t)t.nnz, kPad))) return rc;
     {
         std::vector<float> lab(ds->label.begin(), ds->label.end());
         if ((rc = upload(c, &t.label, lab.data(), lab.size()))) return rc;
@@ -994,7 +1033,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         }
         if ((rc = upload(c, &t.w_row_ptr, rp.data(), rp.size()))) return rc;
         if ((rc = upload(c, &t.w_col, cc.data(), cc.size(), kPad))) return rc;
-        if ((rc = upload(c, &t.w_val, vv.data(), vv.size(), kPad))) return rc;
+        if (!t.unit && (rc = upload(c, &t.w_val, vv.data(), vv.size(), kPad))) return rc;
         if ((rc = upload(c, &t.w_label, ll.data(), ll.size()))) return rc;
         break;  // NextBatch wraps at most once per epoch
     }
@@ -1080,8 +1119,9 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         } else {
             if ((rc = upload(c, (uint32_t **)&t.crow, crow32.data(), crow32.size(), kPad))) return rc;
         }
-        if ((rc = upload(c, &t.cval, cval.data(), cval.size(), kPad))) return rc;
-        csc_bytes = (int64_t)(tcols.size() * 4 + tptr.size() * 4 + (total + kPad) * ((t.row16 ? 2 : 4) + 4));
+        if (!t.unit && (rc = upload(c, &t.cval, cval.data(), cval.size(), kPad))) return rc;
+        csc_bytes = (int64_t)(tcols.size() * 4 + tptr.size() * 4 +
+                              (total + kPad) * ((t.row16 ? 2 : 4) + (t.unit ? 0 : 4)));
         // step buffers and every rank's batch size (L2 term of its pushes)
         free_touched_bufs(c);
         std::vector<float> bs;
@@ -1104,7 +1144,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         const char *lm = getenv("DLR_LONG_COLUMN");
         const int64_t long_min = lm ? atoll(lm) : 4096;
         std::vector<uint32_t> cptr((size_t)nb * (size_t)(D + 1));
-        std::vector<float> cval((size_t)total);
+        std::vector<float> cval(t.unit ? 0 : (size_t)total);
         int64_t lbytes = 0;
         auto finish_long = [&](auto &lb) -> int {
             // concatenate the batches' long columns
@@ -1130,7 +1170,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 std::vector<uint32_t> order(ns);
                 for (size_t k = 0; k < ns; ++k) order[k] = (uint32_t)k;
                 std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
-                    return L.row[L.sptr[x]] < L.row[L.sptr[y]];
+                    return L.row[L.sptr[x] & ~3u] < L.row[L.sptr[y] & ~3u];
                 });
                 sched.insert(sched.end(), order.begin(), order.end());
                 if (!L.sptr.empty()) sched.push_back(0);
@@ -1149,7 +1189,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 (r = upload(c, &t.lsched, sched.data(), sched.size())))
                 return r;
             if ((r = upload(c, (RowT **)&t.lrow, row.data(), row.size(), dlr::kLongChunk))) return r;
-            if ((r = upload(c, &t.lval, val.data(), val.size(), dlr::kLongChunk))) return r;
+            if (!t.unit && (r = upload(c, &t.lval, val.data(), val.size(), dlr::kLongChunk))) return r;
             if ((r = dev_alloc(c, (void **)&t.lpart, (size_t)maxseg * 4))) return r;
             lbytes = (int64_t)(cols.size() * 4 + cseg.size() * 4 + sptr.size() * 4 + row.size() * sizeof(RowT) +
                                val.size() * 4);
@@ -1158,18 +1198,18 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         if (t.row16) {
             std::vector<uint16_t> crow((size_t)total);
             std::vector<LongBatch<uint16_t>> lb;
-            build_csc(src, t.plan, D, t.coff, cptr, crow, cval, long_min, lb, nthreads);
+            build_csc(src, t.plan, D, t.coff, cptr, crow, cval, long_min, lb, t.unit, nthreads);
             if ((rc = upload(c, (uint16_t **)&t.crow, crow.data(), crow.size(), kPad))) return rc;
             if ((rc = finish_long(lb))) return rc;
         } else {
             std::vector<uint32_t> crow((size_t)total);
             std::vector<LongBatch<uint32_t>> lb;
-            build_csc(src, t.plan, D, t.coff, cptr, crow, cval, long_min, lb, nthreads);
+            build_csc(src, t.plan, D, t.coff, cptr, crow, cval, long_min, lb, t.unit, nthreads);
             if ((rc = upload(c, (uint32_t **)&t.crow, crow.data(), crow.size(), kPad))) return rc;
             if ((rc = finish_long(lb))) return rc;
         }
         if ((rc = upload(c, &t.cptr, cptr.data(), cptr.size()))) return rc;
-        if ((rc = upload(c, &t.cval, cval.data(), cval.size(), kPad))) return rc;
+        if (!t.unit && (rc = upload(c, &t.cval, cval.data(), cval.size(), kPad))) return rc;
         // Entry-balanced wave schedule: a wave takes consecutive columns until
         // it has 64 or about one window (kWin entries) of them -- a column
         // order with runs of long columns (frequency order) would otherwise
@@ -1203,7 +1243,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             if ((rc = upload(c, &t.wsched, all.data(), all.size()))) return rc;
             csc_bytes += (int64_t)all.size() * 4;
         }
-        csc_bytes += (int64_t)(cptr.size() * 4 + (total + kPad) * ((t.row16 ? 2 : 4) + 4)) + lbytes;
+        csc_bytes += (int64_t)(cptr.size() * 4 + (total + kPad) * ((t.row16 ? 2 : 4) + (t.unit ? 0 : 4))) + lbytes;
     }
     // Residual buffer (padded to whole LDS phases for the LDS kernel).
     if (c->resid_cap < resid_need) {
@@ -1214,7 +1254,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         HIPC(c, hipStreamSynchronize(c->stream));
         c->resid_cap = resid_need;
     }
-    t.bytes = (int64_t)((t.n_rows + 1) * 8 + (t.nnz + kPad) * 8 + t.n_rows * 4) + csc_bytes;
+    t.bytes = (int64_t)((t.n_rows + 1) * 8 + (t.nnz + kPad) * (t.unit ? 4 : 8) + t.n_rows * 4) + csc_bytes;
     t.loaded = true;
     if (n_batches) *n_batches = nb;
     return DLR_OK;
@@ -1237,7 +1277,7 @@ int dlr_load_test(dlr_ctx *c, const dlr_dataset *ds) {
     }
     if ((rc = upload(c, &t.row_ptr, ds->row_ptr.data(), (size_t)t.n_rows + 1))) return rc;
     if ((rc = upload(c, &t.col, c->perm.empty() ? ds->col.data() : mapped.data(), (size_t)t.nnz, kPad))) return rc;
-    if ((rc = upload(c, &t.val, ds->val.data(), (size_t)t.nnz, kPad))) return rc;
+    if (!unit_values(ds->val) && (rc = upload(c, &t.val, ds->val.data(), (size_t)t.nnz, kPad))) return rc;
     std::vector<float> lab(ds->label.begin(), ds->label.end());
     if ((rc = upload(c, &t.label, lab.data(), lab.size()))) return rc;
     t.grid = dlr::predict_grid(t.n_rows);
@@ -1614,6 +1654,12 @@ int dlr_train_residency(dlr_ctx *c) {
 int dlr_train_relabeled(dlr_ctx *c) {
     if (!c) return DLR_E_ARG;
     return c->perm.empty() ? 0 : 1;
+}
+
+int dlr_train_unit_values(dlr_ctx *c) {
+    if (!c) return DLR_E_ARG;
+    if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_unit_values: no training shard loaded");
+    return c->train.unit ? 1 : 0;
 }
 
 int dlr_train_layout(dlr_ctx *c) {

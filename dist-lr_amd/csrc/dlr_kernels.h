@@ -9,6 +9,8 @@ namespace dlr {
 
 // One batch as CSR: rows [0, rows) with row_ptr[i] absolute offsets into
 // col/val (row_ptr may point into the middle of the shard's array).
+// val == nullptr (here and in DevCsc / DevLong): a unit-valued shard, every
+// value 1.0f (one-hot / binary features), so no value array is stored.
 struct DevBatch {
     const int64_t *row_ptr;
     const int32_t *col;
@@ -37,7 +39,9 @@ struct DevCsc {
 // ptr entries in DevCsc carry bit 31), column l's chunks are segments
 // [cseg[l], cseg[l+1]); segment s spans entries [sptr[s], sptr[s+1]) of
 // row/val (4-aligned starts; at most kLongChunk entries + 3 padding; the
-// arrays are padded by kLongChunk entries).
+// arrays are padded by kLongChunk entries).  The low 2 bits of a column's
+// end pointer (the next start, or the batch's terminal entry) hold the
+// column's padding count.
 constexpr int kLongChunk = 256;
 struct DevLong {
     const uint32_t *cols;

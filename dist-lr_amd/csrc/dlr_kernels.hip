@@ -89,7 +89,9 @@ __device__ __forceinline__ V load_stream(const V *p) {
 // Sum over this lane's segment [a, b) of fl32(table[idx[k]] * val[k]), in
 // k order.  The wave's entries are [e0, e1).  lds: kWin floats of this wave.
 // Only lanes < SEG own a segment; all 64 lanes load and gather.
-template <typename IdxT>
+// UNIT: every value is 1.0f and val is not read (one-hot / binary shards:
+// fl32(t * 1.0f) == t exactly, so the sums are the same bits).
+template <typename IdxT, bool UNIT = false>
 __device__ __forceinline__ float ordered_segment_dot(int64_t e0, int64_t e1, int64_t a, int64_t b, int lane,
                                                      const IdxT *__restrict__ idx, const float *__restrict__ val,
                                                      const float *__restrict__ table, float *lds) {
@@ -111,7 +113,10 @@ __device__ __forceinline__ float ordered_segment_dot(int64_t e0, int64_t e1, int
                 const int64_t e = ws + t * kChunk + lane * kVec;
                 const int64_t ec = e < e1 ? e : ws + t * kChunk;
                 iv[t] = load_stream(reinterpret_cast<const IV *>(idx + ec));
-                v[t] = load_stream(reinterpret_cast<const float4 *>(val + ec));
+                if constexpr (UNIT)
+                    v[t] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+                else
+                    v[t] = load_stream(reinterpret_cast<const float4 *>(val + ec));
             }
         }
         // (2) every gather of the window, then the products.  Entries outside
@@ -178,7 +183,7 @@ __device__ __forceinline__ float sigmoid_ref(float z) {
 // K2: margin + sigmoid + residual.  A wave owns SEG consecutive batch rows
 // (lane l < SEG owns row row0 + l); SEG < 64 gives small batches more waves
 // to hide latency with (the loads and gathers still use all 64 lanes).
-template <int SEG>
+template <int SEG, bool UNIT = false>
 __global__ __launch_bounds__(kWaves *kWave) void k_margin_residual(DevBatch bt, const float *__restrict__ w,
                                                                    float *__restrict__ resid) {
     __shared__ float s_p[kWaves][kWin];
@@ -192,7 +197,7 @@ __global__ __launch_bounds__(kWaves *kWave) void k_margin_residual(DevBatch bt, 
     const int64_t rlast = min(row0 + SEG, bt.rows);
     const int64_t e0 = bt.row_ptr[row0], e1 = bt.row_ptr[rlast];
     const int64_t a = valid ? bt.row_ptr[my] : e1, b = valid ? bt.row_ptr[my + 1] : e1;
-    const float z = ordered_segment_dot<int32_t>(e0, e1, a, b, lane, bt.col, bt.val, w, s_p[wv]);
+    const float z = ordered_segment_dot<int32_t, UNIT>(e0, e1, a, b, lane, bt.col, bt.val, w, s_p[wv]);
     if (valid) resid[my] = sigmoid_ref(z) - y;
 }
 
@@ -201,6 +206,7 @@ __device__ __forceinline__ double softplus(double t) { return t > 0 ? t + log1p(
 // K5: LR::Test / Predict_ (lr.cc:47-63, 100-106): pred = z > 0; correct
 // count by wave ballot (integer atomics: order-free), log-loss partial per
 // workgroup in a fixed order (deterministic for a fixed grid).
+template <bool UNIT>
 __global__ __launch_bounds__(kWaves *kWave) void k_predict(DevBatch bt, const float *__restrict__ w,
                                                            unsigned long long *__restrict__ correct,
                                                            double *__restrict__ ll_part) {
@@ -216,7 +222,7 @@ __global__ __launch_bounds__(kWaves *kWave) void k_predict(DevBatch bt, const fl
         const int64_t rlast = min(row0 + kWave, bt.rows);
         const int64_t e0 = bt.row_ptr[row0], e1 = bt.row_ptr[rlast];
         const int64_t a = valid ? bt.row_ptr[my] : e1, b = valid ? bt.row_ptr[my + 1] : e1;
-        const float z = ordered_segment_dot<int32_t>(e0, e1, a, b, lane, bt.col, bt.val, w, s_p[wv]);
+        const float z = ordered_segment_dot<int32_t, UNIT>(e0, e1, a, b, lane, bt.col, bt.val, w, s_p[wv]);
         bool hit = false;
         if (valid) {
             const float y = bt.label[my];
@@ -251,7 +257,7 @@ __global__ void k_sum_partials(const double *__restrict__ part, int n, double *_
 // the lr.cc:40 normalisation + L2 term.  FUSED (single rank) applies the
 // server update in place: with W == 1, fl32(fl32(lr*g)/1.0f) == fl32(lr*g)
 // for every mode (main.cc:71, 81).
-template <typename RowT, bool FUSED>
+template <typename RowT, bool FUSED, bool UNIT = false>
 __global__ __launch_bounds__(kWaves *kWave) void k_grad(DevCsc cs, const RowT *__restrict__ crow, int64_t D,
                                                         const float *__restrict__ resid, float *__restrict__ w,
                                                         float *__restrict__ gout, float Bf, double Bd, float lr,
@@ -279,7 +285,7 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad(DevCsc cs, const RowT *_
     const int64_t e0 = cs.ptr[j0] & kPtrMask, e1 = cs.ptr[jl] & kPtrMask;
     const uint32_t pj = valid ? cs.ptr[j] : 0u;
     const int64_t a = valid ? (int64_t)(pj & kPtrMask) : e1, b = valid ? (int64_t)(cs.ptr[j + 1] & kPtrMask) : e1;
-    const float G = ordered_segment_dot<RowT>(e0, e1, a, b, lane, crow, cs.val, resid, s_p[wv]);
+    const float G = ordered_segment_dot<RowT, UNIT>(e0, e1, a, b, lane, crow, cs.val, resid, s_p[wv]);
     if (!valid || (pj & kLongFlag)) return;
     const float cw = C * wj;
     const float l2 = cw / Bf;
@@ -310,7 +316,12 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad(DevCsc cs, const RowT *_
 // sequential version took 5.35 ms on the C3 shard: each lane streamed its
 // own region and the rows' locality was lost.)
 
-template <typename RowT>
+// Chunk starts are 4-aligned; the low 2 bits of a column's end pointer (the
+// next column's first start, or the batch's terminal entry) hold the
+// column's padding count.  Valued: padding entries are (row 0, value 0) and
+// summed like the others.  UNIT (no value array, every value 1.0f): the
+// chunk ends before its padding.
+template <typename RowT, bool UNIT = false>
 __global__ __launch_bounds__(256) void k_long_segments(const uint32_t *__restrict__ sptr, int64_t nseg,
                                                        const uint32_t *__restrict__ sched,
                                                        const RowT *__restrict__ row, const float *__restrict__ val,
@@ -321,10 +332,15 @@ __global__ __launch_bounds__(256) void k_long_segments(const uint32_t *__restric
     const int64_t nw = (int64_t)gridDim.x * wpb;
     for (int64_t k = (int64_t)blockIdx.x * wpb + threadIdx.x / kWave; k < nseg; k += nw) {  // wave-uniform
         const int64_t s = sched ? (int64_t)sched[k] : k;
-        const uint32_t a = sptr[s], b = sptr[s + 1];  // a 4-aligned; b - a <= kLongChunk (+3 padding)
-        const uint32_t e = a + (uint32_t)lane * 4;      // arrays padded by kLongChunk entries
+        const uint32_t a = sptr[s] & ~3u, bn = sptr[s + 1];  // b - a <= kLongChunk (+3 padding)
+        const uint32_t b = UNIT ? (bn & ~3u) - (bn & 3u) : bn & ~3u;
+        const uint32_t e = a + (uint32_t)lane * 4;  // arrays padded by kLongChunk entries
         const RV r4 = *reinterpret_cast<const RV *>(row + e);
-        const float4 v4 = *reinterpret_cast<const float4 *>(val + e);
+        float4 v4;
+        if constexpr (UNIT)
+            v4 = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+        else
+            v4 = *reinterpret_cast<const float4 *>(val + e);
         // gathers unconditional (past the chunk the rows are the next
         // chunk's or padding: valid indices), masked after -- a load in a
         // divergent branch makes the compiler wait at the join
@@ -578,7 +594,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
 
 // K3t: segment s = column cols[s].  FUSED (one rank): out[s] = new w of the
 // column (w - fl32(lr*g)); else out[s] = g (this rank's pushed gradient).
-template <typename RowT, bool FUSED>
+template <typename RowT, bool FUSED, bool UNIT = false>
 __global__ __launch_bounds__(kWaves *kWave) void k_grad_touched(DevCsc cs, const RowT *__restrict__ crow,
                                                                 const uint32_t *__restrict__ cols, int64_t ncols,
                                                                 const float *__restrict__ resid,
@@ -594,7 +610,7 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad_touched(DevCsc cs, const
     const int64_t sl = min(s0 + kWave, ncols);
     const int64_t e0 = cs.ptr[s0], e1 = cs.ptr[sl];
     const int64_t a = valid ? (int64_t)cs.ptr[sg] : e1, b = valid ? (int64_t)cs.ptr[sg + 1] : e1;
-    const float G = ordered_segment_dot<RowT>(e0, e1, a, b, lane, crow, cs.val, resid, s_p[wv]);
+    const float G = ordered_segment_dot<RowT, UNIT>(e0, e1, a, b, lane, crow, cs.val, resid, s_p[wv]);
     if (!valid) return;
     const float wj = w[cols[sg]];
     const float cw = C * wj;
@@ -1003,16 +1019,24 @@ int margin_seg(const DevBatch &bt) {
 hipError_t launch_margin_residual(const DevBatch &bt, const float *w, float *resid, hipStream_t s) {
     if (bt.rows <= 0) return hipSuccess;
     const dim3 blk(kWaves * kWave);
+    const bool unit = bt.val == nullptr;  // unit-valued shard: no value array
+#define DLR_MR(SEG)                                                                                              \
+    case SEG:                                                                                                    \
+        if (unit)                                                                                                \
+            hipLaunchKernelGGL((k_margin_residual<SEG, true>), dim3(grid_for(bt.rows, kWaves * SEG)), blk, 0, s, bt, \
+                               w, resid);                                                                        \
+        else                                                                                                     \
+            hipLaunchKernelGGL((k_margin_residual<SEG, false>), dim3(grid_for(bt.rows, kWaves * SEG)), blk, 0, s,    \
+                               bt, w, resid);                                                                    \
+        break;
     switch (margin_seg(bt)) {
-        case 16:
-            hipLaunchKernelGGL(k_margin_residual<16>, dim3(grid_for(bt.rows, kWaves * 16)), blk, 0, s, bt, w, resid);
-            break;
-        case 32:
-            hipLaunchKernelGGL(k_margin_residual<32>, dim3(grid_for(bt.rows, kWaves * 32)), blk, 0, s, bt, w, resid);
-            break;
+        DLR_MR(16)
+        DLR_MR(32)
+        DLR_MR(64)
         default:
-            hipLaunchKernelGGL(k_margin_residual<64>, dim3(grid_for(bt.rows, kWaves * 64)), blk, 0, s, bt, w, resid);
+            return hipErrorInvalidValue;
     }
+#undef DLR_MR
     return hipGetLastError();
 }
 
@@ -1021,8 +1045,10 @@ int predict_grid(int64_t rows) { return rows <= 0 ? 0 : (int)grid_for(rows, kWav
 hipError_t launch_predict(const DevBatch &bt, const float *w, unsigned long long *correct, double *ll_part,
                           double *ll_out, hipStream_t s) {
     const int grid = predict_grid(bt.rows);
-    if (grid > 0)
-        hipLaunchKernelGGL(k_predict, dim3(grid), dim3(kWaves * kWave), 0, s, bt, w, correct, ll_part);
+    if (grid > 0 && bt.val == nullptr)
+        hipLaunchKernelGGL(k_predict<true>, dim3(grid), dim3(kWaves * kWave), 0, s, bt, w, correct, ll_part);
+    else if (grid > 0)
+        hipLaunchKernelGGL(k_predict<false>, dim3(grid), dim3(kWaves * kWave), 0, s, bt, w, correct, ll_part);
     hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(64), 0, s, ll_part, grid, ll_out);
     return hipGetLastError();
 }
@@ -1035,23 +1061,29 @@ hipError_t launch_grad(const DevCsc &cs, int64_t D, const float *resid, float *w
     const dim3 blk(kWaves * kWave);
     const float Bf = (float)B;
     const double Bd = (double)B;
+#define DLR_G(RT, F, U)                                                                                          \
+    hipLaunchKernelGGL((k_grad<RT, F, U>), dim3(grid), blk, 0, s, cs, static_cast<const RT *>(cs.row), D, resid, w, \
+                       gout, Bf, Bd, lr, C)
+#define DLR_GU(RT, F)      \
+    if (cs.val == nullptr) \
+        DLR_G(RT, F, true);  \
+    else                   \
+        DLR_G(RT, F, false);
     if (cs.row16) {
-        const uint16_t *r = static_cast<const uint16_t *>(cs.row);
-        if (fused)
-            hipLaunchKernelGGL((k_grad<uint16_t, true>), dim3(grid), blk, 0, s, cs, r, D, resid, w, gout, Bf, Bd, lr,
-                               C);
-        else
-            hipLaunchKernelGGL((k_grad<uint16_t, false>), dim3(grid), blk, 0, s, cs, r, D, resid, w, gout, Bf, Bd,
-                               lr, C);
+        if (fused) {
+            DLR_GU(uint16_t, true)
+        } else {
+            DLR_GU(uint16_t, false)
+        }
     } else {
-        const uint32_t *r = static_cast<const uint32_t *>(cs.row);
-        if (fused)
-            hipLaunchKernelGGL((k_grad<uint32_t, true>), dim3(grid), blk, 0, s, cs, r, D, resid, w, gout, Bf, Bd, lr,
-                               C);
-        else
-            hipLaunchKernelGGL((k_grad<uint32_t, false>), dim3(grid), blk, 0, s, cs, r, D, resid, w, gout, Bf, Bd,
-                               lr, C);
+        if (fused) {
+            DLR_GU(uint32_t, true)
+        } else {
+            DLR_GU(uint32_t, false)
+        }
     }
+#undef DLR_GU
+#undef DLR_G
     return hipGetLastError();
 }
 
@@ -1113,21 +1145,29 @@ hipError_t launch_grad_touched(const DevCsc &cs, const uint32_t *cols, int64_t n
     const dim3 blk(kWaves * kWave);
     const float Bf = (float)B;
     const double Bd = (double)B;
-#define DLR_GT(RT, F)                                                                                          \
-    hipLaunchKernelGGL((k_grad_touched<RT, F>), dim3(grid), blk, 0, s, cs, static_cast<const RT *>(cs.row), cols, \
+#define DLR_GT1(RT, F, U)                                                                                         \
+    hipLaunchKernelGGL((k_grad_touched<RT, F, U>), dim3(grid), blk, 0, s, cs, static_cast<const RT *>(cs.row), cols, \
                        ncols, resid, w, out, Bf, Bd, lr, C)
+#define DLR_GT(RT, F)          \
+    if (cs.val == nullptr)     \
+        DLR_GT1(RT, F, true);  \
+    else                       \
+        DLR_GT1(RT, F, false);
     if (cs.row16) {
-        if (fused)
-            DLR_GT(uint16_t, true);
-        else
-            DLR_GT(uint16_t, false);
+        if (fused) {
+            DLR_GT(uint16_t, true)
+        } else {
+            DLR_GT(uint16_t, false)
+        }
     } else {
-        if (fused)
-            DLR_GT(uint32_t, true);
-        else
-            DLR_GT(uint32_t, false);
+        if (fused) {
+            DLR_GT(uint32_t, true)
+        } else {
+            DLR_GT(uint32_t, false)
+        }
     }
 #undef DLR_GT
+#undef DLR_GT1
     return hipGetLastError();
 }
 
@@ -1165,12 +1205,18 @@ hipError_t launch_grad_long(const DevLong &lg, int64_t B, const float *resid, fl
                             float lr, float C, bool fused, hipStream_t s) {
     if (lg.ncols <= 0) return hipSuccess;
     const unsigned sgrid = (unsigned)std::min<int64_t>((lg.nseg + 3) / 4, 256 * 16);  // a wave per chunk
-    if (lg.row16)
-        hipLaunchKernelGGL(k_long_segments<uint16_t>, dim3(sgrid), dim3(256), 0, s, lg.sptr, lg.nseg, lg.sched,
-                           static_cast<const uint16_t *>(lg.row), lg.val, resid, part);
+#define DLR_LS(RT, U)                                                                                      \
+    hipLaunchKernelGGL((k_long_segments<RT, U>), dim3(sgrid), dim3(256), 0, s, lg.sptr, lg.nseg, lg.sched, \
+                       static_cast<const RT *>(lg.row), lg.val, resid, part)
+    if (lg.row16 && lg.val == nullptr)
+        DLR_LS(uint16_t, true);
+    else if (lg.row16)
+        DLR_LS(uint16_t, false);
+    else if (lg.val == nullptr)
+        DLR_LS(uint32_t, true);
     else
-        hipLaunchKernelGGL(k_long_segments<uint32_t>, dim3(sgrid), dim3(256), 0, s, lg.sptr, lg.nseg, lg.sched,
-                           static_cast<const uint32_t *>(lg.row), lg.val, resid, part);
+        DLR_LS(uint32_t, false);
+#undef DLR_LS
     const float Bf = (float)B;
     const double Bd = (double)B;
     const unsigned cgrid = grid_for(lg.ncols, 4);  // a wave per long column

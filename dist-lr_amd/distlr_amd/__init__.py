@@ -41,7 +41,8 @@ SYMBOLS = [
     "dlr_set_weights", "dlr_get_weights", "dlr_load_train", "dlr_load_test", "dlr_load_train_dense",
     "dlr_load_test_dense", "dlr_set_residency", "dlr_train_residency",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
-    "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_train_relabeled", "dlr_memory_info",
+    "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_train_relabeled", "dlr_train_unit_values",
+    "dlr_memory_info",
 ]
 
 if not os.path.exists(LIB_PATH):
@@ -149,6 +150,7 @@ _sig("dlr_kernel_time", C.c_int, P, C.c_int, C.POINTER(C.c_double), C.POINTER(i6
 _sig("dlr_stage_time", C.c_int, P, C.c_int, i64, i64, C.c_float, C.c_float, C.POINTER(C.c_double))
 _sig("dlr_train_layout", C.c_int, P)
 _sig("dlr_train_relabeled", C.c_int, P)
+_sig("dlr_train_unit_values", C.c_int, P)
 _sig("dlr_memory_info", C.c_int, P, C.POINTER(i64), C.POINTER(i64))
 
 
@@ -517,6 +519,14 @@ class Engine:
         """Whether the loaded sparse shard's columns are in frequency order
         (dlr_train_relabeled)."""
         rc = lib.dlr_train_relabeled(self._h)
+        self._c(min(rc, 0))
+        return rc == 1
+
+    def train_unit_values(self) -> bool:
+        """Whether the loaded sparse shard is unit-valued (every value 1.0f):
+        no value arrays are stored and the UNIT kernels run
+        (dlr_train_unit_values)."""
+        rc = lib.dlr_train_unit_values(self._h)
         self._c(min(rc, 0))
         return rc == 1
 

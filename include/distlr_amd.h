@@ -299,6 +299,15 @@ int dlr_train_layout(dlr_ctx *ctx);
  * this API (a dense test shard cannot be loaded beside a relabeled one). */
 int dlr_train_relabeled(dlr_ctx *ctx);
 
+/* 1 when every value of the loaded sparse training shard is exactly 1.0f
+ * (one-hot / binary features: a9a, Criteo-style hashed fields, BASELINE C1,
+ * C3, C5), else 0.  Such a shard stores no value arrays (4 bytes per entry
+ * less in HBM and per pass) and its kernels never read values:
+ * fl32(t * 1.0f) == t, so results are bitwise those of the valued path.
+ * Decided at load; DLR_UNIT_VALUES=0 keeps the value arrays.  A test shard
+ * is checked the same way on its own. */
+int dlr_train_unit_values(dlr_ctx *ctx);
+
 /* Device bytes resident for the loaded shards (for reporting). */
 int dlr_memory_info(dlr_ctx *ctx, int64_t *train_bytes, int64_t *test_bytes);
 
