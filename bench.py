@@ -183,6 +183,7 @@ def main():
     t_load = time.perf_counter() - t_setup - t_gen
     layout = "dense" if args.kind == "dense" else \
         {dlr.LAYOUT_CLASSIC: "classic", dlr.LAYOUT_LDS: "lds", dlr.LAYOUT_TOUCHED: "touched"}[eng.train_layout()]
+    band_rows = eng.train_band_rows() if args.kind != "dense" else 0
     log(f"[rank {rank}] shard {args.rows} x {D}, nnz/row {args.nnz}: generated {t_gen:.1f}s, "
         f"{'streamed from host' if streamed else 'resident'} {train_bytes / 2**30:.2f} GiB in {t_load:.1f}s, "
         f"{nb} batches/epoch, gradient layout {layout}")
@@ -314,7 +315,7 @@ def main():
                     f"{'pinned host memory, staged per batch' if streamed else 'resident in HBM'})",
             "config": {"workload": f"{args.label}: {args.rows} rows/GPU x {D} features, {args.nnz} nnz/row, "
                                    f"batch {B}, sync SGD lr {args.lr}, C=1",
-                       "name": args.config, "gradient_layout": layout,
+                       "name": args.config, "gradient_layout": layout + (f"+bands({band_rows} rows)" if band_rows else ""),
                        "values": "unit (all 1.0f, not stored)" if unit else "fp32",
                        "rows_per_gpu": args.rows, "num_feature_dim": D, "nnz_per_row": args.nnz,
                        "batch_size": B, "parallelism": f"dp{world}"},

@@ -96,6 +96,26 @@ struct TrainShard {
     // wsoff[b] .. wsoff[b+1]-1 in wsched (column starts, then D)
     uint32_t *wsched = nullptr;
     std::vector<int64_t> wsoff;
+    // row-band layout of the classic copy's short columns (large batches,
+    // dlr_kernels.hip "Row-band layout"): band_shift > 0 replaces
+    // cptr/crow/cval/wsched; band k of batch b is bands[bfirst[b] + k]
+    struct Band {
+        int64_t pair, ptr, ent, ws, nwaves;  // offsets into bcols, bptr, brow/bval, bws
+    };
+    int band_shift = 0;
+    std::vector<Band> bands;
+    std::vector<int64_t> bfirst;
+    uint32_t *bcols = nullptr, *bptr = nullptr, *bws = nullptr;
+    void *brow = nullptr;
+    float *bval = nullptr;
+    float *gacc = nullptr;  // D running column sums
+    // band mode: long columns in row phases (dlr_kernels.h DevLPhase); batch
+    // b's phases are lpdesc[b * lnph ..], its columns lcols/lcseg as above
+    int64_t lnph = 0;
+    dlr::PhaseDesc *lpdesc = nullptr;
+    uint32_t *lpptr = nullptr, *lpslot = nullptr, *lpws = nullptr;
+    uint16_t *lprow = nullptr;
+    float *lpval = nullptr;
     int64_t bytes = 0;
 };
 
@@ -234,7 +254,9 @@ void free_train(dlr_ctx *c) {
                     (void *)t.w_col, (void *)t.w_val, (void *)t.w_label, (void *)t.cptr, t.crow, (void *)t.cval,
                     (void *)t.pbase, (void *)t.pends, (void *)t.prow, (void *)t.pval, (void *)t.tcols,
                     (void *)t.lcols, (void *)t.lcseg, (void *)t.lsptr, t.lrow, (void *)t.lval, (void *)t.lpart, (void *)t.lsched,
-                    (void *)t.dX, (void *)t.dpart, (void *)t.wsched})
+                    (void *)t.dX, (void *)t.dpart, (void *)t.wsched, (void *)t.bcols, (void *)t.bptr,
+                    (void *)t.bws, t.brow, (void *)t.bval, (void *)t.gacc, (void *)t.lpdesc, (void *)t.lpptr,
+                    (void *)t.lpslot, (void *)t.lpws, (void *)t.lprow, (void *)t.lpval})
         dev_free(c, p);
     t = TrainShard();
 }
@@ -530,6 +552,225 @@ void build_csc(const CsrView &ds, const std::vector<dlr::BatchSpan> &plan, int64
     for (auto &x : th) x.join();
 }
 
+// Row-band copy (DevBand) of the classic copy's short columns: for each
+// batch and each band of 2^shift rows, the (column, segment) pairs of the
+// short columns with entries in the band, columns ascending, entries in
+// batch-row order; each band's entries start 4-aligned.  Built from the
+// classic copy (whose column segments are already in row order) in
+// parallel over column ranges; `ws` gets each band's entry-balanced wave
+// schedule (as the classic one: <= 64 pairs, ~kWin entries per wave).
+template <typename RowT>
+struct BandBuild {
+    std::vector<uint32_t> cols, ptr, ws;
+    std::vector<RowT> row;
+    std::vector<float> val;
+    std::vector<TrainShard::Band> bands;
+    std::vector<int64_t> bfirst;
+};
+
+template <typename RowT>
+void build_bands(const std::vector<uint32_t> &cptr, const std::vector<RowT> &crow, const std::vector<float> &cval,
+                 const std::vector<int64_t> &coff, int64_t nb, int64_t D, int64_t B, int shift, bool unit,
+                 int nthreads, BandBuild<RowT> &out) {
+    const int64_t nbands = (B + ((int64_t)1 << shift) - 1) >> shift;
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, D / 4096 + 1));
+    out.bfirst.assign((size_t)nb + 1, 0);
+    int64_t pair_at = 0, ptr_at = 0, ent_at = 0, ws_at = 0;
+    std::vector<int64_t> np((size_t)nt * (size_t)nbands), ne((size_t)nt * (size_t)nbands);
+    for (int64_t b = 0; b < nb; ++b) {
+        const uint32_t *cp = cptr.data() + (size_t)b * (size_t)(D + 1);
+        const RowT *rr = crow.data() + coff[(size_t)b];
+        const float *vv = unit ? nullptr : cval.data() + coff[(size_t)b];
+        auto lo = [&](int k) { return D * k / nt; };
+        // pass 1: pairs and entries per (thread range, band)
+        std::fill(np.begin(), np.end(), 0);
+        std::fill(ne.begin(), ne.end(), 0);
+        {
+            std::vector<std::thread> th;
+            for (int k = 0; k < nt; ++k)
+                th.emplace_back([&, k] {
+                    int64_t *P = np.data() + (size_t)k * (size_t)nbands, *E = ne.data() + (size_t)k * (size_t)nbands;
+                    for (int64_t j = lo(k); j < lo(k + 1); ++j) {
+                        if (cp[j] & 0x80000000u) continue;  // long column
+                        const uint32_t a = cp[j] & 0x7FFFFFFFu, e = cp[j + 1] & 0x7FFFFFFFu;
+                        int64_t last = -1;
+                        for (uint32_t q = a; q < e; ++q) {
+                            const int64_t s = (int64_t)rr[q] >> shift;
+                            if (s != last) ++P[s], last = s;
+                            ++E[s];
+                        }
+                    }
+                });
+            for (auto &x : th) x.join();
+        }
+        // band-major offsets (thread ranges ascend in column order)
+        std::vector<int64_t> po((size_t)nt * (size_t)nbands), eo((size_t)nt * (size_t)nbands);
+        const size_t bb0 = out.bands.size();
+        for (int64_t s = 0; s < nbands; ++s) {
+            TrainShard::Band bd{pair_at, ptr_at, ent_at, 0, 0};
+            int64_t p = 0, e = 0;
+            for (int k = 0; k < nt; ++k) {
+                po[(size_t)k * nbands + s] = p;
+                eo[(size_t)k * nbands + s] = e;
+                p += np[(size_t)k * nbands + s];
+                e += ne[(size_t)k * nbands + s];
+            }
+            out.bands.push_back(bd);
+            pair_at += p;
+            ptr_at += p + 1;
+            ent_at += (e + 3) & ~int64_t(3);
+        }
+        out.cols.resize((size_t)pair_at);
+        out.ptr.resize((size_t)ptr_at);
+        out.row.resize((size_t)ent_at + 64, 0);
+        if (!unit) out.val.resize((size_t)ent_at + 64, 0.0f);
+        // pass 2: fill
+        {
+            std::vector<std::thread> th;
+            for (int k = 0; k < nt; ++k)
+                th.emplace_back([&, k] {
+                    std::vector<int64_t> pc((size_t)nbands), ec((size_t)nbands);
+                    for (int64_t s = 0; s < nbands; ++s) {
+                        pc[(size_t)s] = po[(size_t)k * nbands + s];
+                        ec[(size_t)s] = eo[(size_t)k * nbands + s];
+                    }
+                    for (int64_t j = lo(k); j < lo(k + 1); ++j) {
+                        if (cp[j] & 0x80000000u) continue;
+                        const uint32_t a = cp[j] & 0x7FFFFFFFu, e = cp[j + 1] & 0x7FFFFFFFu;
+                        int64_t last = -1;
+                        for (uint32_t q = a; q < e; ++q) {
+                            const int64_t s = (int64_t)rr[q] >> shift;
+                            const TrainShard::Band &bd = out.bands[bb0 + (size_t)s];
+                            if (s != last) {
+                                out.cols[(size_t)(bd.pair + pc[(size_t)s])] = (uint32_t)j;
+                                out.ptr[(size_t)(bd.ptr + pc[(size_t)s])] = (uint32_t)ec[(size_t)s];
+                                ++pc[(size_t)s];
+                                last = s;
+                            }
+                            const size_t o = (size_t)(bd.ent + ec[(size_t)s]++);
+                            out.row[o] = rr[q];
+                            if (!unit) out.val[o] = vv[q];
+                        }
+                    }
+                });
+            for (auto &x : th) x.join();
+        }
+        // terminal pointers and wave schedules
+        for (int64_t s = 0; s < nbands; ++s) {
+            TrainShard::Band &bd = out.bands[bb0 + (size_t)s];
+            int64_t p = 0, e = 0;
+            for (int k = 0; k < nt; ++k) p += np[(size_t)k * nbands + s], e += ne[(size_t)k * nbands + s];
+            out.ptr[(size_t)(bd.ptr + p)] = (uint32_t)e;
+            bd.ws = ws_at;
+            const uint32_t *pp = out.ptr.data() + bd.ptr;
+            out.ws.push_back(0);
+            int64_t acc = 0;
+            int cols = 0;
+            for (int64_t q = 0; q < p; ++q) {
+                const int64_t cq = (int64_t)pp[q + 1] - (int64_t)pp[q];
+                if (cols == 64 || (cols > 0 && acc + cq > 1024)) {
+                    out.ws.push_back((uint32_t)q);
+                    acc = 0;
+                    cols = 0;
+                }
+                acc += cq;
+                ++cols;
+            }
+            out.ws.push_back((uint32_t)p);
+            bd.nwaves = p > 0 ? (int64_t)out.ws.size() - ws_at - 1 : 0;
+            ws_at = (int64_t)out.ws.size();
+        }
+        out.bfirst[(size_t)b + 1] = (int64_t)out.bands.size();
+    }
+}
+
+// Long columns of every batch regrouped in row phases of kLPhase rows
+// (band mode): from the chunked long arrays (LongBatch, rows ascending per
+// column), for each batch and phase the entries of each long column with a
+// row in the phase (phase-local uint16 rows), columns in long-column order,
+// each phase's entries starting 4-aligned.  A column's entries in a phase
+// are cut into PIECES of <= kPiece consecutive entries (a lane sums one
+// piece in row order); piece partials are numbered column-major -- column
+// l's pieces, phase by phase, from cseg[l] -- so k_long_combine adds each
+// column's partials in row order.  Per phase an entry-balanced wave
+// schedule over the pieces (<= 64 pieces, ~kWin entries per wave).
+constexpr int64_t kPiece = 64;
+struct LPhaseBuild {
+    std::vector<dlr::PhaseDesc> desc;
+    std::vector<uint32_t> ptr, slot, ws, cseg;
+    std::vector<uint16_t> row;
+    std::vector<float> val;
+    int64_t maxpart = 0;
+};
+
+template <typename RowT>
+void build_long_phases(const std::vector<LongBatch<RowT>> &lb, int64_t B, bool unit, LPhaseBuild &out) {
+    const int64_t nph = (B + dlr::kLPhase - 1) / dlr::kLPhase;
+    for (const LongBatch<RowT> &L : lb) {
+        const int64_t nl = (int64_t)L.cols.size();
+        std::vector<int64_t> cnt((size_t)(nph * nl), 0);  // [p][l]
+        std::vector<int64_t> a((size_t)nl), e((size_t)nl);
+        for (int64_t l = 0; l < nl; ++l) {
+            a[(size_t)l] = L.sptr[L.cseg[(size_t)l]] & ~3u;
+            const uint32_t nx = L.sptr[L.cseg[(size_t)l + 1]];
+            e[(size_t)l] = (int64_t)(nx & ~3u) - (int64_t)(nx & 3u);
+            for (int64_t q = a[(size_t)l]; q < e[(size_t)l]; ++q)
+                ++cnt[(size_t)(((int64_t)L.row[(size_t)q] / dlr::kLPhase) * nl + l)];
+        }
+        // piece slots: column-major
+        std::vector<int64_t> cs((size_t)nl + 1, 0), pslot((size_t)(nph * nl));
+        for (int64_t l = 0; l < nl; ++l) {
+            int64_t n = cs[(size_t)l];
+            for (int64_t p = 0; p < nph; ++p) {
+                pslot[(size_t)(p * nl + l)] = n;
+                n += (cnt[(size_t)(p * nl + l)] + kPiece - 1) / kPiece;
+            }
+            cs[(size_t)l + 1] = n;
+        }
+        std::vector<int64_t> cur((size_t)(nph * nl));
+        for (int64_t p = 0; p < nph; ++p) {
+            dlr::PhaseDesc d{(int64_t)out.ptr.size(), (int64_t)out.row.size(), (int64_t)out.ws.size(), 0};
+            int64_t at = 0, np = 0, acc = 0;
+            int pieces = 0;
+            out.ws.push_back(0);
+            for (int64_t l = 0; l < nl; ++l) {
+                const int64_t c = cnt[(size_t)(p * nl + l)];
+                cur[(size_t)(p * nl + l)] = d.ent + at;
+                for (int64_t o = 0; o < c; o += kPiece) {
+                    const int64_t n = std::min(kPiece, c - o);
+                    if (pieces == 64 || (pieces > 0 && acc + n > 1024)) {
+                        out.ws.push_back((uint32_t)np);
+                        acc = 0;
+                        pieces = 0;
+                    }
+                    out.ptr.push_back((uint32_t)(at + o));
+                    out.slot.push_back((uint32_t)(pslot[(size_t)(p * nl + l)] + o / kPiece));
+                    acc += n;
+                    ++pieces;
+                    ++np;
+                }
+                at += c;
+            }
+            out.ptr.push_back((uint32_t)at);
+            out.slot.push_back(0);  // keeps slot indexed like ptr
+            out.ws.push_back((uint32_t)np);
+            d.ntasks = np > 0 ? (int64_t)out.ws.size() - d.ws - 1 : 0;
+            out.desc.push_back(d);
+            out.row.resize((size_t)(d.ent + ((at + 3) & ~int64_t(3))), 0);
+        }
+        if (!unit) out.val.resize(out.row.size(), 0.0f);
+        for (int64_t l = 0; l < nl; ++l)
+            for (int64_t q = a[(size_t)l]; q < e[(size_t)l]; ++q) {
+                const int64_t r = (int64_t)L.row[(size_t)q];
+                const size_t o = (size_t)cur[(size_t)((r / dlr::kLPhase) * nl + l)]++;
+                out.row[o] = (uint16_t)(r % dlr::kLPhase);
+                if (!unit) out.val[o] = L.val[(size_t)q];
+            }
+        for (int64_t l = 0; l <= nl; ++l) out.cseg.push_back((uint32_t)cs[(size_t)l]);
+        out.maxpart = std::max(out.maxpart, cs[(size_t)nl]);
+    }
+}
+
 // Phase-split column-major copy (DevPcsc, dlr_kernels.h) of every batch.
 // Rows of batch b fall in phases of R rows; for each 64-column group and
 // phase, a block lists the entries of the group's columns whose row is in
@@ -809,17 +1050,38 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
         return e;
     }
     if (t.pcsc) return dlr::launch_grad_lds(pcsc_view(c, b), c->D, B, c->resid, c->w, gout, lr, C, fused, c->stream);
-    hipError_t e = dlr::launch_grad(csc_view(c, b), c->D, c->resid, c->w, gout, B, lr, C, fused, c->stream);
-    if (e != hipSuccess || !t.any_long) return e;
     const size_t bb = (size_t)b;
-    const int64_t nl = t.lcoff[bb + 1] - t.lcoff[bb];
-    if (nl == 0) return hipSuccess;
     const size_t esz = t.row16 ? 2 : 4;
-    dlr::DevLong lg{t.lcols + t.lcoff[bb], t.lcseg + (t.lcoff[bb] + (int64_t)b), t.lsptr + t.lsoff[bb],
-                    (const char *)t.lrow + esz * (size_t)t.leoff[bb], t.lval ? t.lval + t.leoff[bb] : nullptr, nl,
-                    t.lsoff[bb + 1] - t.lsoff[bb] - 1, t.row16};
-    if (t.lsched) lg.sched = t.lsched + t.lsoff[bb];
-    return dlr::launch_grad_long(lg, B, c->resid, c->w, gout, t.lpart, lr, C, fused, c->stream);
+    hipError_t e = hipSuccess;
+    if (t.band_shift) {
+        // short columns band by band into gacc, the long columns' raw sums
+        // into gacc, then the update of every column
+        e = hipMemsetAsync(t.gacc, 0, (size_t)c->D * 4, c->stream);
+        for (int64_t k = t.bfirst[bb]; e == hipSuccess && k < t.bfirst[bb + 1]; ++k) {
+            const TrainShard::Band &bd = t.bands[(size_t)k];
+            dlr::DevBand dv{t.bcols + bd.pair, t.bptr + bd.ptr, t.bws + bd.ws, (const char *)t.brow + esz * (size_t)bd.ent,
+                            t.bval ? t.bval + bd.ent : nullptr, bd.nwaves, t.row16};
+            e = dlr::launch_grad_band(dv, c->resid, t.gacc, c->stream);
+        }
+    } else {
+        e = dlr::launch_grad(csc_view(c, b), c->D, c->resid, c->w, gout, B, lr, C, fused, c->stream);
+    }
+    const int64_t nl = t.any_long ? t.lcoff[bb + 1] - t.lcoff[bb] : 0;
+    if (e == hipSuccess && nl > 0 && t.lnph > 0) {
+        dlr::DevLPhase lp{t.lpdesc + b * t.lnph, t.lpptr, t.lpslot, t.lpws, t.lprow, t.lpval, t.lnph};
+        e = dlr::launch_long_phase(lp, t.lcols + t.lcoff[bb], t.lcseg + (t.lcoff[bb] + (int64_t)b), nl, c->resid,
+                                   t.lpart, t.gacc, c->stream);
+    } else if (e == hipSuccess && nl > 0) {
+        dlr::DevLong lg{t.lcols + t.lcoff[bb], t.lcseg + (t.lcoff[bb] + (int64_t)b), t.lsptr + t.lsoff[bb],
+                        (const char *)t.lrow + esz * (size_t)t.leoff[bb], t.lval ? t.lval + t.leoff[bb] : nullptr, nl,
+                        t.lsoff[bb + 1] - t.lsoff[bb] - 1, t.row16};
+        if (t.lsched) lg.sched = t.lsched + t.lsoff[bb];
+        e = dlr::launch_grad_long(lg, B, c->resid, c->w, gout, t.lpart, lr, C, fused, c->stream,
+                                  t.band_shift ? t.gacc : nullptr);
+    }
+    if (e == hipSuccess && t.band_shift)
+        e = dlr::launch_band_finalize(t.gacc, c->w, gout, c->D, B, lr, C, fused, c->stream);
+    return e;
 }
 
 }  // namespace
@@ -1145,6 +1407,15 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         const int64_t long_min = lm ? atoll(lm) : 4096;
         std::vector<uint32_t> cptr((size_t)nb * (size_t)(D + 1));
         std::vector<float> cval(t.unit ? 0 : (size_t)total);
+        // Row bands for the short columns of large batches (DLR_BAND_ROWS:
+        // rows per band, rounded down to a power of two; 0 = off; default
+        // 2^20 rows, a 4 MB residual slice, for batches of >= 2 bands); the
+        // long columns then go in row phases (build_long_phases)
+        const char *brs = getenv("DLR_BAND_ROWS");
+        const int64_t band_rows = brs ? atoll(brs) : (int64_t)1 << 20;
+        int shift = 0;
+        while (band_rows > 0 && ((int64_t)2 << shift) <= band_rows) ++shift;
+        const bool band = band_rows > 0 && shift > 0 && (brs ? t.B > ((int64_t)1 << shift) : t.B >= ((int64_t)2 << shift));
         int64_t lbytes = 0;
         auto finish_long = [&](auto &lb) -> int {
             // concatenate the batches' long columns
@@ -1161,6 +1432,31 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             }
             t.any_long = t.lcoff[(size_t)nb] > 0;
             if (!t.any_long) return DLR_OK;
+            if (band) {
+                LPhaseBuild ph;
+                build_long_phases(lb, t.B, t.unit, ph);
+                std::vector<uint32_t> cols;
+                for (auto &L : lb) {
+                    cols.insert(cols.end(), L.cols.begin(), L.cols.end());
+                    L = {};
+                }
+                int r;
+                t.lnph = (t.B + dlr::kLPhase - 1) / dlr::kLPhase;
+                if ((r = upload(c, &t.lcols, cols.data(), cols.size()))) return r;
+                if ((r = upload(c, &t.lcseg, ph.cseg.data(), ph.cseg.size()))) return r;
+                if ((r = upload(c, &t.lpdesc, ph.desc.data(), ph.desc.size()))) return r;
+                if ((r = upload(c, &t.lpptr, ph.ptr.data(), ph.ptr.size()))) return r;
+                if ((r = upload(c, &t.lpslot, ph.slot.data(), ph.slot.size()))) return r;
+                if ((r = upload(c, &t.lpws, ph.ws.data(), ph.ws.size()))) return r;
+                if ((r = upload(c, &t.lprow, ph.row.data(), ph.row.size(), kPad))) return r;
+                if (!t.unit && (r = upload(c, &t.lpval, ph.val.data(), ph.val.size(), kPad))) return r;
+                if ((r = dev_alloc(c, (void **)&t.lpart, (size_t)std::max<int64_t>(1, ph.maxpart) * 4))) return r;
+                lbytes = (int64_t)(cols.size() * 4 + ph.cseg.size() * 4 + ph.desc.size() * sizeof(dlr::PhaseDesc) +
+                                   (ph.ptr.size() * 2 + ph.ws.size()) * 4 + (ph.row.size() + kPad) * (t.unit ? 2 : 6) +
+                                   ph.maxpart * 4);
+                resid_need = std::max(resid_need, t.lnph * (int64_t)dlr::kLPhase);
+                return DLR_OK;
+            }
             std::vector<uint32_t> cols, cseg, sptr, sched;
             std::vector<RowT> row;
             std::vector<float> val;
@@ -1195,26 +1491,48 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                                val.size() * 4);
             return DLR_OK;
         };
+        auto classic = [&](auto &crow, auto &lb) -> int {
+            using RowT = typename std::decay_t<decltype(crow)>::value_type;
+            build_csc(src, t.plan, D, t.coff, cptr, crow, cval, long_min, lb, t.unit, nthreads);
+            int r;
+            if ((r = finish_long(lb))) return r;
+            if (!band) {
+                if ((r = upload(c, (RowT **)&t.crow, crow.data(), crow.size(), kPad))) return r;
+                return DLR_OK;
+            }
+            BandBuild<RowT> bb;
+            build_bands(cptr, crow, cval, t.coff, nb, D, t.B, shift, t.unit, nthreads, bb);
+            t.band_shift = shift;
+            t.bands = std::move(bb.bands);
+            t.bfirst = std::move(bb.bfirst);
+            if ((r = upload(c, &t.bcols, bb.cols.data(), bb.cols.size(), 64))) return r;
+            if ((r = upload(c, &t.bptr, bb.ptr.data(), bb.ptr.size()))) return r;
+            if ((r = upload(c, &t.bws, bb.ws.data(), bb.ws.size()))) return r;
+            if ((r = upload(c, (RowT **)&t.brow, bb.row.data(), bb.row.size(), kPad))) return r;
+            if (!t.unit && (r = upload(c, &t.bval, bb.val.data(), bb.val.size(), kPad))) return r;
+            if ((r = dev_alloc(c, (void **)&t.gacc, (size_t)D * 4))) return r;
+            csc_bytes += (int64_t)((bb.cols.size() + bb.ptr.size() + bb.ws.size()) * 4 +
+                                   (bb.row.size() + kPad) * (sizeof(RowT) + (t.unit ? 0 : 4)) + D * 4);
+            return DLR_OK;
+        };
         if (t.row16) {
             std::vector<uint16_t> crow((size_t)total);
             std::vector<LongBatch<uint16_t>> lb;
-            build_csc(src, t.plan, D, t.coff, cptr, crow, cval, long_min, lb, t.unit, nthreads);
-            if ((rc = upload(c, (uint16_t **)&t.crow, crow.data(), crow.size(), kPad))) return rc;
-            if ((rc = finish_long(lb))) return rc;
+            if ((rc = classic(crow, lb))) return rc;
         } else {
             std::vector<uint32_t> crow((size_t)total);
             std::vector<LongBatch<uint32_t>> lb;
-            build_csc(src, t.plan, D, t.coff, cptr, crow, cval, long_min, lb, t.unit, nthreads);
-            if ((rc = upload(c, (uint32_t **)&t.crow, crow.data(), crow.size(), kPad))) return rc;
-            if ((rc = finish_long(lb))) return rc;
+            if ((rc = classic(crow, lb))) return rc;
         }
-        if ((rc = upload(c, &t.cptr, cptr.data(), cptr.size()))) return rc;
-        if (!t.unit && (rc = upload(c, &t.cval, cval.data(), cval.size(), kPad))) return rc;
+        if (!band) {
+            if ((rc = upload(c, &t.cptr, cptr.data(), cptr.size()))) return rc;
+            if (!t.unit && (rc = upload(c, &t.cval, cval.data(), cval.size(), kPad))) return rc;
+        }
         // Entry-balanced wave schedule: a wave takes consecutive columns until
         // it has 64 or about one window (kWin entries) of them -- a column
         // order with runs of long columns (frequency order) would otherwise
         // give some waves 64 x thousands of entries.
-        {
+        if (!band) {
             std::vector<std::vector<uint32_t>> ws((size_t)nb);
             for_batches(nb, nthreads, [&](int64_t b) {
                 const uint32_t *cp = cptr.data() + (size_t)b * (size_t)(D + 1);
@@ -1243,7 +1561,9 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             if ((rc = upload(c, &t.wsched, all.data(), all.size()))) return rc;
             csc_bytes += (int64_t)all.size() * 4;
         }
-        csc_bytes += (int64_t)(cptr.size() * 4 + (total + kPad) * ((t.row16 ? 2 : 4) + (t.unit ? 0 : 4))) + lbytes;
+        if (!band)
+            csc_bytes += (int64_t)(cptr.size() * 4 + (total + kPad) * ((t.row16 ? 2 : 4) + (t.unit ? 0 : 4)));
+        csc_bytes += lbytes;
     }
     // Residual buffer (padded to whole LDS phases for the LDS kernel).
     if (c->resid_cap < resid_need) {
@@ -1660,6 +1980,11 @@ int dlr_train_unit_values(dlr_ctx *c) {
     if (!c) return DLR_E_ARG;
     if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_unit_values: no training shard loaded");
     return c->train.unit ? 1 : 0;
+}
+
+int dlr_train_band_rows(dlr_ctx *c) {
+    if (!c || !c->train.loaded) return 0;
+    return c->train.band_shift ? 1 << c->train.band_shift : 0;
 }
 
 int dlr_train_layout(dlr_ctx *c) {

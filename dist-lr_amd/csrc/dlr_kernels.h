@@ -72,6 +72,44 @@ struct DevPcsc {
     int phases;
 };
 
+// Short columns of one batch in ROW BANDS of 2^k rows (classic layout, large
+// batches): for one band, the (column, segment) pairs of the short columns
+// with entries in the band, columns ascending; pair s is column cols[s] with
+// entries [ptr[s], ptr[s+1]) of row/val (batch-local rows, ascending).  Wave
+// k sums pairs [wstart[k], wstart[k+1]) (<= 64 pairs, ~one window of
+// entries).  row/val are padded by >= 64 entries.
+struct DevBand {
+    const uint32_t *cols;
+    const uint32_t *ptr;
+    const uint32_t *wstart;
+    const void *row;
+    const float *val;
+    int64_t nwaves;
+    bool row16;
+};
+
+// Long columns of one batch in ROW PHASES of kLPhase rows (band mode):
+// phase p's entries (phase-local rows, ascending per column) are cut into
+// PIECES of <= 64 consecutive entries of one column; piece s of the phase
+// spans [ptr[desc[p].ptr + s], ... + s + 1) of row/val offset by
+// desc[p].ent, and its partial goes to part[slot[desc[p].ptr + s]]; waves
+// take pieces [ws[desc[p].ws + t], ... + t + 1) (<= 64 pieces, ~one window
+// of entries).
+constexpr int kLPhase = 16384;  // rows per phase (64 KB of residuals in LDS)
+constexpr int kLPWaves = 16;    // waves per workgroup (one workgroup per phase)
+struct PhaseDesc {
+    int64_t ptr, ent, ws, ntasks;
+};
+struct DevLPhase {
+    const PhaseDesc *desc;
+    const uint32_t *ptr;
+    const uint32_t *slot;
+    const uint32_t *ws;
+    const uint16_t *row;
+    const float *val;
+    int64_t nph;
+};
+
 // Dense rows (row-major N x D fp32) and 0/1 labels as floats.
 struct DevDense {
     const float *X;
@@ -95,8 +133,19 @@ hipError_t launch_grad(const DevCsc &cs, int64_t D, const float *resid, float *w
                        float C, bool fused, hipStream_t s);
 // Long columns: chunk sums (part[nseg] scratch), then the ordered combine
 // and the update (fused) / pushed gradient (gout).
+// graw != null (band layout): the long columns' raw sums G go to graw[j]
+// and k_band_finalize applies the update.
 hipError_t launch_grad_long(const DevLong &lg, int64_t B, const float *resid, float *w, float *gout, float *part,
-                            float lr, float C, bool fused, hipStream_t s);
+                            float lr, float C, bool fused, hipStream_t s, float *graw = nullptr);
+// Row bands: one launch per band, in band order, continuing gacc (zeroed
+// before the first band); then the update of every column from gacc.
+hipError_t launch_grad_band(const DevBand &bd, const float *resid, float *gacc, hipStream_t s);
+// Long columns in row phases: piece partials part[slot], then the fixed
+// combine of each column's partials [cseg[l], cseg[l+1]) into graw[j].
+hipError_t launch_long_phase(const DevLPhase &lp, const uint32_t *cols, const uint32_t *cseg, int64_t ncols,
+                             const float *resid, float *part, float *graw, hipStream_t s);
+hipError_t launch_band_finalize(const float *gacc, float *w, float *gout, int64_t D, int64_t B, float lr, float C,
+                                bool fused, hipStream_t s);
 int grad_lds_fill(int64_t B);  // float4 fills per thread = rows per phase / 4,096
 hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float *resid, float *w, float *gout,
                            float lr, float C, bool fused, hipStream_t s);

@@ -91,15 +91,19 @@ __device__ __forceinline__ V load_stream(const V *p) {
 // Only lanes < SEG own a segment; all 64 lanes load and gather.
 // UNIT: every value is 1.0f and val is not read (one-hot / binary shards:
 // fl32(t * 1.0f) == t exactly, so the sums are the same bits).
+// acc0: the sum the segment continues (0.0f: a whole segment; the band
+// kernel passes a column's sum over the earlier row bands, which continues
+// the same sequential chain).
 template <typename IdxT, bool UNIT = false>
 __device__ __forceinline__ float ordered_segment_dot(int64_t e0, int64_t e1, int64_t a, int64_t b, int lane,
                                                      const IdxT *__restrict__ idx, const float *__restrict__ val,
-                                                     const float *__restrict__ table, float *lds) {
+                                                     const float *__restrict__ table, float *lds,
+                                                     float acc0 = 0.0f) {
     using IV = typename Vec4<IdxT>::type;
     constexpr int kT = kWin / (kVec * kWave);
     constexpr int kChunk = kVec * kWave;  // entries per (t) step of the wave
     const int64_t base = e0 & ~int64_t(kVec - 1);
-    float acc = 0.0f;
+    float acc = acc0;
     for (int64_t ws = base; ws < e1; ws += kWin) {
         const int64_t left = e1 - ws;  // wave-uniform
         // (1) index/value loads of the window's chunks that hold entries
@@ -362,7 +366,9 @@ __global__ __launch_bounds__(256) void k_long_segments(const uint32_t *__restric
 // order, the wave adds the 64 lane sums with the fixed xor-shuffle tree
 // (deterministic); then lr.cc:40 and the update (FUSED) or the pushed
 // gradient.
-template <bool FUSED>
+// RAW (band layout): gout[j] = G, the column's raw sum; k_band_finalize
+// applies lr.cc:40 and the update to every column.
+template <bool FUSED, bool RAW = false>
 __global__ __launch_bounds__(256) void k_long_combine(const uint32_t *__restrict__ cols,
                                                       const uint32_t *__restrict__ cseg, int64_t ncols,
                                                       const float *__restrict__ part, float *__restrict__ w,
@@ -378,6 +384,10 @@ __global__ __launch_bounds__(256) void k_long_combine(const uint32_t *__restrict
     for (int off = 32; off > 0; off >>= 1) G = G + __shfl_xor(G, off);
     if (lane != 0) return;
     const uint32_t j = cols[l];
+    if (RAW) {
+        gout[j] = G;
+        return;
+    }
     const float wj = w[j];
     const float cw = C * wj;
     const float l2 = cw / Bf;
@@ -621,6 +631,110 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad_touched(DevCsc cs, const
         out[sg] = wj - step;
     } else {
         out[sg] = g;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Row-band layout (classic layout, large batches: BASELINE C3's full-shard
+// batch of 12.5M rows).  A short column's residual gathers hit random rows
+// of the whole batch -- a 50 MB residual array, far beyond an XCD's 4 MB L2,
+// so every gather went to the Infinity Cache (~60 G gathers/s).  Here the
+// batch's rows are cut into bands of 2^k rows (DevBand) and the short
+// columns are summed band by band, one launch per band in band order: a
+// launch gathers only from its band's slice of the residuals (L2-resident).
+// Column j's entries in band s precede those in band s+1 in batch-row
+// order, so continuing j's running sum (gacc[j], +0 before the first band)
+// band after band IS lr.cc:37's sequential order: bitwise the classic
+// kernel's result.  Each column appears at most once per band, so a launch
+// has no write conflicts; the kernel boundary orders the bands.
+template <typename RowT, bool UNIT = false>
+__global__ __launch_bounds__(kWaves *kWave) void k_grad_band(DevBand bd, const RowT *__restrict__ brow,
+                                                             const float *__restrict__ resid,
+                                                             float *__restrict__ gacc) {
+    __shared__ float s_p[kWaves][kWin];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    const int64_t wid = (int64_t)blockIdx.x * kWaves + wv;
+    if (wid >= bd.nwaves) return;  // wave-uniform
+    const int64_t s0 = bd.wstart[wid], sl = bd.wstart[wid + 1];
+    const int64_t sg = s0 + lane;
+    const bool valid = sg < sl;
+    const uint32_t j = valid ? bd.cols[sg] : 0u;
+    // non-temporal: the running sums (a 64 MB array at C3) must not evict
+    // the band's residual slice from L2
+    const float acc0 = valid ? __builtin_nontemporal_load(gacc + j) : 0.0f;
+    const int64_t e0 = bd.ptr[s0], e1 = bd.ptr[sl];
+    const int64_t a = valid ? (int64_t)bd.ptr[sg] : e1, b = valid ? (int64_t)bd.ptr[sg + 1] : e1;
+    const float G = ordered_segment_dot<RowT, UNIT>(e0, e1, a, b, lane, brow, bd.val, resid, s_p[wv], acc0);
+    if (valid) __builtin_nontemporal_store(G, gacc + j);
+}
+
+// Long columns in ROW PHASES (band mode).  The chunked long path gathers
+// each chunk's residuals from wherever its rows lie: a sparse long column's
+// 256-entry chunk spans up to ~1M rows, so its gathers miss L2.  Here the
+// batch's rows are cut into phases of kLPhase rows; one 1,024-thread
+// workgroup per phase stages the phase's residuals in LDS (64 KB), then its
+// waves sum the phase's pieces (<= 64 entries of one column each; lane per
+// piece, products parked in LDS, in batch-row order: ordered_segment_dot
+// with the LDS residuals as the table) into part[slot].  k_long_combine then
+// adds a column's piece partials with its fixed tree.  Deterministic; for
+// these columns not the single sequential sum (DLR_LONG_COLUMN=0 keeps
+// every column sequential and bitwise).  Pieces keep every lane's serial
+// chain <= 64 adds: a hot column's ~2,000 entries per phase would
+// otherwise be one lane's chain while its wave's other lanes idle.
+template <bool UNIT>
+__global__ __launch_bounds__(kLPWaves *kWave) void k_long_phase(DevLPhase lp, const float *__restrict__ resid,
+                                                                float *__restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float *s_r = smem;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int lane = threadIdx.x & (kWave - 1);
+    float *slab = smem + kLPhase + wv * kWin;
+    const int64_t p = blockIdx.x;
+    {
+        const float4 *src = reinterpret_cast<const float4 *>(resid + p * kLPhase);
+        float4 *dst = reinterpret_cast<float4 *>(s_r);
+#pragma unroll
+        for (int k = 0; k < kLPhase / 4 / (kLPWaves * kWave); ++k)
+            dst[k * kLPWaves * kWave + threadIdx.x] = src[k * kLPWaves * kWave + threadIdx.x];
+    }
+    __syncthreads();
+    const PhaseDesc d = lp.desc[p];
+    const uint32_t *ptr = lp.ptr + d.ptr;
+    const uint32_t *ws = lp.ws + d.ws;
+    const uint16_t *row = lp.row + d.ent;
+    const float *val = UNIT ? nullptr : lp.val + d.ent;
+    for (int64_t t = wv; t < d.ntasks; t += kLPWaves) {  // wave-uniform
+        const int64_t s0 = ws[t], sl = ws[t + 1];
+        const int64_t q = s0 + lane;
+        const bool valid = q < sl;
+        const int64_t e0 = ptr[s0], e1 = ptr[sl];
+        const int64_t a = valid ? (int64_t)ptr[q] : e1, b = valid ? (int64_t)ptr[q + 1] : e1;
+        const uint32_t slot = valid ? lp.slot[d.ptr + q] : 0u;
+        const float G = ordered_segment_dot<uint16_t, UNIT>(e0, e1, a, b, lane, row, val, s_r, slab);
+        if (valid) part[slot] = G;
+    }
+}
+
+// After the bands (and the long columns' combine, RAW into gacc): lr.cc:40
+// and the update (FUSED) or the pushed gradient, for every column -- an
+// untouched column has G = +0 there, as in k_grad.
+template <bool FUSED>
+__global__ __launch_bounds__(256) void k_band_finalize(const float *__restrict__ gacc, float *__restrict__ w,
+                                                       float *__restrict__ gout, int64_t D, float Bf, double Bd,
+                                                       float lr, float C) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= D) return;
+    const float G = gacc[j];
+    const float wj = w[j];
+    const float cw = C * wj;
+    const float l2 = cw / Bf;
+    const float g = (float)((double)G / Bd + (double)l2);
+    if (FUSED) {
+        const float step = lr * g;
+        w[j] = wj - step;
+    } else {
+        gout[j] = g;
     }
 }
 
@@ -1202,7 +1316,7 @@ hipError_t launch_sparse_merge(const uint32_t *lists, int64_t cap, int64_t strid
 }
 
 hipError_t launch_grad_long(const DevLong &lg, int64_t B, const float *resid, float *w, float *gout, float *part,
-                            float lr, float C, bool fused, hipStream_t s) {
+                            float lr, float C, bool fused, hipStream_t s, float *graw) {
     if (lg.ncols <= 0) return hipSuccess;
     const unsigned sgrid = (unsigned)std::min<int64_t>((lg.nseg + 3) / 4, 256 * 16);  // a wave per chunk
 #define DLR_LS(RT, U)                                                                                      \
@@ -1220,12 +1334,63 @@ hipError_t launch_grad_long(const DevLong &lg, int64_t B, const float *resid, fl
     const float Bf = (float)B;
     const double Bd = (double)B;
     const unsigned cgrid = grid_for(lg.ncols, 4);  // a wave per long column
-    if (fused)
+    if (graw)
+        hipLaunchKernelGGL((k_long_combine<false, true>), dim3(cgrid), dim3(256), 0, s, lg.cols, lg.cseg, lg.ncols,
+                           part, w, graw, Bf, Bd, lr, C);
+    else if (fused)
         hipLaunchKernelGGL(k_long_combine<true>, dim3(cgrid), dim3(256), 0, s, lg.cols, lg.cseg, lg.ncols, part, w,
                            gout, Bf, Bd, lr, C);
     else
         hipLaunchKernelGGL(k_long_combine<false>, dim3(cgrid), dim3(256), 0, s, lg.cols, lg.cseg, lg.ncols, part, w,
                            gout, Bf, Bd, lr, C);
+    return hipGetLastError();
+}
+
+hipError_t launch_grad_band(const DevBand &bd, const float *resid, float *gacc, hipStream_t s) {
+    if (bd.nwaves <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)((bd.nwaves + kWaves - 1) / kWaves);
+    const dim3 blk(kWaves * kWave);
+    if (bd.row16 && bd.val == nullptr)
+        hipLaunchKernelGGL((k_grad_band<uint16_t, true>), dim3(grid), blk, 0, s, bd,
+                           static_cast<const uint16_t *>(bd.row), resid, gacc);
+    else if (bd.row16)
+        hipLaunchKernelGGL((k_grad_band<uint16_t, false>), dim3(grid), blk, 0, s, bd,
+                           static_cast<const uint16_t *>(bd.row), resid, gacc);
+    else if (bd.val == nullptr)
+        hipLaunchKernelGGL((k_grad_band<uint32_t, true>), dim3(grid), blk, 0, s, bd,
+                           static_cast<const uint32_t *>(bd.row), resid, gacc);
+    else
+        hipLaunchKernelGGL((k_grad_band<uint32_t, false>), dim3(grid), blk, 0, s, bd,
+                           static_cast<const uint32_t *>(bd.row), resid, gacc);
+    return hipGetLastError();
+}
+
+hipError_t launch_long_phase(const DevLPhase &lp, const uint32_t *cols, const uint32_t *cseg, int64_t ncols,
+                             const float *resid, float *part, float *graw, hipStream_t s) {
+    if (ncols <= 0 || lp.nph <= 0) return hipSuccess;
+    const size_t lds = (size_t)(kLPhase + kLPWaves * kWin) * 4;
+    if (lp.val == nullptr)
+        hipLaunchKernelGGL(k_long_phase<true>, dim3((unsigned)lp.nph), dim3(kLPWaves * kWave), lds, s, lp, resid,
+                           part);
+    else
+        hipLaunchKernelGGL(k_long_phase<false>, dim3((unsigned)lp.nph), dim3(kLPWaves * kWave), lds, s, lp, resid,
+                           part);
+    hipLaunchKernelGGL((k_long_combine<false, true>), dim3(grid_for(ncols, 4)), dim3(256), 0, s, cols, cseg, ncols,
+                       part, nullptr, graw, 1.0f, 1.0, 0.0f, 0.0f);
+    return hipGetLastError();
+}
+
+hipError_t launch_band_finalize(const float *gacc, float *w, float *gout, int64_t D, int64_t B, float lr, float C,
+                                bool fused, hipStream_t s) {
+    if (D <= 0) return hipSuccess;
+    const float Bf = (float)B;
+    const double Bd = (double)B;
+    if (fused)
+        hipLaunchKernelGGL(k_band_finalize<true>, dim3(grid_for(D, 256)), dim3(256), 0, s, gacc, w, gout, D, Bf, Bd,
+                           lr, C);
+    else
+        hipLaunchKernelGGL(k_band_finalize<false>, dim3(grid_for(D, 256)), dim3(256), 0, s, gacc, w, gout, D, Bf, Bd,
+                           lr, C);
     return hipGetLastError();
 }
 

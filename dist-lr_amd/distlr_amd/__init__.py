@@ -41,7 +41,7 @@ SYMBOLS = [
     "dlr_set_weights", "dlr_get_weights", "dlr_load_train", "dlr_load_test", "dlr_load_train_dense",
     "dlr_load_test_dense", "dlr_set_residency", "dlr_train_residency",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
-    "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_train_relabeled", "dlr_train_unit_values",
+    "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_train_band_rows", "dlr_train_relabeled", "dlr_train_unit_values",
     "dlr_memory_info",
 ]
 
@@ -149,6 +149,7 @@ _sig("dlr_timing", C.c_int, P, C.c_int)
 _sig("dlr_kernel_time", C.c_int, P, C.c_int, C.POINTER(C.c_double), C.POINTER(i64))
 _sig("dlr_stage_time", C.c_int, P, C.c_int, i64, i64, C.c_float, C.c_float, C.POINTER(C.c_double))
 _sig("dlr_train_layout", C.c_int, P)
+_sig("dlr_train_band_rows", C.c_int, P)
 _sig("dlr_train_relabeled", C.c_int, P)
 _sig("dlr_train_unit_values", C.c_int, P)
 _sig("dlr_memory_info", C.c_int, P, C.POINTER(i64), C.POINTER(i64))
@@ -512,6 +513,13 @@ class Engine:
     def train_layout(self) -> int:
         """LAYOUT_CLASSIC / LAYOUT_LDS / LAYOUT_TOUCHED of the loaded shard."""
         rc = lib.dlr_train_layout(self._h)
+        self._c(min(rc, 0))
+        return rc
+
+    def train_band_rows(self) -> int:
+        """Rows per band when the classic layout's short columns are summed
+        in row bands (large batches), else 0 (dlr_train_band_rows)."""
+        rc = lib.dlr_train_band_rows(self._h)
         self._c(min(rc, 0))
         return rc
 

@@ -290,6 +290,17 @@ int dlr_stage_time(dlr_ctx *ctx, int stage, int64_t first_batch, int64_t count, 
 #define DLR_LAYOUT_TOUCHED 2
 int dlr_train_layout(dlr_ctx *ctx);
 
+/* Rows per band when the classic layout's short columns are summed in ROW
+ * BANDS (large batches such as BASELINE C3's 12.5M-row full-shard batch:
+ * each band's residual slice stays in an XCD's L2), else 0.  Bitwise the
+ * same sums as without bands (each column's running sum continues from band
+ * to band in batch-row order).  DLR_BAND_ROWS=<rows> (a power of two; 0 =
+ * off) overrides the default of 2^20 rows for batches of >= 2^21 rows.
+ * In band mode the long columns (DLR_LONG_COLUMN) are summed per row phase
+ * of 16,384 rows and the phase partials combined by a fixed tree
+ * (deterministic; within 1e-5 of the single sequential sum). */
+int dlr_train_band_rows(dlr_ctx *ctx);
+
 /* 1 when the loaded sparse training shard's columns are relabeled in
  * frequency order (Zipf-skewed shards such as BASELINE C3: the hot weights
  * then share cache lines in the margin's gathers), else 0.  Chosen at load

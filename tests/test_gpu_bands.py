@@ -1,0 +1,194 @@
+"""Row bands (dlr_train_band_rows): for large batches the classic layout's
+short columns are summed band by band -- one launch per band of 2^k batch
+rows, each column's running sum continued from band to band in batch-row
+order (dlr_kernels.hip "Row-band layout").  That is lr.cc:35-39's sequential
+order, so results must be bitwise those of the single-pass classic kernel
+and of the oracle.  DLR_BAND_ROWS forces small bands so the golden C1
+trajectories and reduced C3-shaped shards exercise many bands, ragged last
+bands, empty bands, both row widths (uint16 for <= 65,536-row batches, else
+uint32), unit and fp32 values, the pushed gradient (N > 1 path) and the
+key-range exchange.  Long columns in band mode are summed per row phase
+(deterministic, within the 1e-5 tolerance, as the chunked long path)."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+import distlr_amd as dlr
+import oracle
+from conftest import GOLDEN, read_golden_json
+from engine_driver import run_engine
+from test_gpu_layouts import _c3_shards, _csr_shard
+from test_gpu_parity import assert_same_weights, compare_runs, oracle_shard
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def classic(monkeypatch):
+    monkeypatch.setenv("DLR_GRAD_KERNEL", "classic")
+
+
+def _band_rows(ds, D, B):
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(dlr.init_weight(D))
+        eng.load_train(ds, B)
+        assert eng.train_layout() == dlr.LAYOUT_CLASSIC
+        return eng.train_band_rows()
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("rows", [2, 16, 1024])
+@pytest.mark.parametrize("name", ["c1_W1_Bfull_mean", "c1_W1_B7_mean", "c1_W2_B64_async", "real_W2_B50_mean"])
+def test_golden_trajectories_banded(classic, monkeypatch, rows, name):
+    monkeypatch.setenv("DLR_BAND_ROWS", str(rows))
+    meta = read_golden_json("trajectories.json")[name]
+    base = os.path.join(GOLDEN, meta["dataset"])
+    D = meta["D"]
+    shards = [dlr.Dataset.load_libsvm(os.path.join(base, "train", f"part-00{p + 1}"), D)
+              for p in range(meta["workers"])]
+    B = meta["batch_size"] if meta["batch_size"] > 0 else shards[0].n_rows
+    if B <= rows:
+        pytest.skip("batch not larger than one band: no bands")
+    assert _band_rows(shards[0], D, meta["batch_size"]) == rows
+    test = dlr.Dataset.load_libsvm(os.path.join(base, "test", "part-001"), D)
+    res = run_engine(shards, D, meta["num_iteration"], meta["batch_size"], meta["learning_rate"], test=test,
+                     test_interval=meta["test_interval"], mode=meta["mode"])
+    assert res.w.astype("<f4").tobytes().hex() == meta["w"]
+    assert [p.astype("<f4").tobytes().hex() for p in res.pulled] == meta["pulled"]
+
+
+def test_band_rows_choice(classic, monkeypatch):
+    ds = dlr.Dataset.generate(3000, 5000, 10, seed=2, stream=1)
+    monkeypatch.delenv("DLR_BAND_ROWS", raising=False)
+    assert _band_rows(ds, 5000, -1) == 0            # default bands start at 2^21-row batches
+    monkeypatch.setenv("DLR_BAND_ROWS", "1000")      # rounded down to a power of two
+    assert _band_rows(ds, 5000, -1) == 512
+    assert _band_rows(ds, 5000, 512) == 0           # one band: no bands
+    monkeypatch.setenv("DLR_BAND_ROWS", "0")
+    assert _band_rows(ds, 5000, -1) == 0
+
+
+@pytest.mark.parametrize("B", [7, 1001, 2500, -1])
+@pytest.mark.parametrize("value_mode", [0, 1])
+def test_batch_sizes_banded(classic, monkeypatch, B, value_mode):
+    # wrapping batches, a batch larger than the shard, ragged last bands
+    monkeypatch.setenv("DLR_BAND_ROWS", "4")
+    D = 3000
+    ds = dlr.Dataset.generate(1000, D, 20, value_mode=value_mode, seed=3, stream=1)
+    eng = run_engine([ds], D, 2, B, 0.1)
+    orc = oracle.run_worker([oracle_shard(ds, D)], D, 2, B, 0.1)
+    compare_runs(eng, orc)
+
+
+def test_ragged_and_empty_bands(classic, monkeypatch):
+    # rows with no entries make whole bands empty (a band with no pairs)
+    monkeypatch.setenv("DLR_BAND_ROWS", "8")
+    rng = np.random.default_rng(5)
+    D, n = 4000, 1200
+    lens = rng.integers(0, 30, size=n)
+    lens[100:180] = 0      # 80 empty rows: >= 9 empty bands of 8
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    col = np.concatenate([np.sort(rng.choice(D, k, replace=False)) for k in lens]).astype(np.int32)
+    val = rng.integers(1, 10001, size=len(col)).astype(np.float32) / np.float32(10000)
+    lab = rng.integers(0, 2, size=n).astype(np.int32)
+    ds = dlr.Dataset.from_csr(rp, col, val, lab, D)
+    eng = run_engine([ds], D, 2, 600, 0.3)
+    orc = oracle.run_worker([oracle_shard(ds, D)], D, 2, 600, 0.3)
+    compare_runs(eng, orc)
+
+
+@pytest.mark.parametrize("rows", [4096, 32768])
+def test_c3_bands_bitwise_without_chunking(monkeypatch, rows):
+    # every column one sequential sum, carried across bands: bitwise the
+    # oracle (uint32 rows: the full-shard batch has > 65,536 rows)
+    monkeypatch.setenv("DLR_LONG_COLUMN", "0")
+    monkeypatch.setenv("DLR_BAND_ROWS", str(rows))
+    D = 1 << 24
+    shards = _c3_shards(1, rows=80_000)
+    assert _band_rows(shards[0], D, -1) == rows
+    eng = run_engine(shards, D, 2, -1, 0.2)
+    orc = oracle.run_worker([_csr_shard(s) for s in shards], D, 2, -1, 0.2)
+    compare_runs(eng, orc)
+
+
+def _within(a, b, rel=1e-5, floor=1e-7):
+    a, b = a.astype(np.float64), b.astype(np.float64)
+    err = np.abs(a - b) - (rel * np.abs(b) + floor)
+    assert err.max() <= 0, f"max excess {err.max():.3g}"
+
+
+@pytest.mark.parametrize("W", [1, 2])
+def test_c3_bands_long_phases_within_tolerance(monkeypatch, W):
+    # band mode: long columns summed per row phase (16,384 rows) and the
+    # phase partials combined by a fixed tree -- deterministic, within the
+    # north-star bar of the reference's single sequential sum
+    D = 1 << 24
+    shards = _c3_shards(W, rows=80_000)
+    monkeypatch.setenv("DLR_BAND_ROWS", "8192")
+    assert _band_rows(shards[0], D, -1) == 8192
+    got = run_engine(shards, D, 3, -1, 0.2)
+    orc = oracle.run_worker([_csr_shard(s) for s in shards], D, 3, -1, 0.2)
+    _within(got.w, orc.w)
+    again = run_engine(shards, D, 3, -1, 0.2)
+    assert_same_weights(again.w, got.w)
+
+
+def test_c3_banded_pushed_gradient(monkeypatch):
+    # the N > 1 path's pushed gradient (non-fused finalize): short columns
+    # bitwise the unbanded classic kernel's, long columns within 1e-5 of the
+    # oracle's sequential sums
+    D = 1 << 24
+    ds = _c3_shards(1, rows=60_000)[0]
+    rp, col, val, lab = ds.csr()
+    hot = np.bincount(col, minlength=D) > 4096
+    assert hot.sum() >= 30
+    w0 = dlr.init_weight(D)
+    out = {}
+    for rows in ("0", "4096"):
+        monkeypatch.setenv("DLR_BAND_ROWS", rows)
+        eng = dlr.Engine(D)
+        try:
+            eng.set_weights(w0)
+            eng.load_train(ds, -1)
+            assert eng.train_band_rows() == int(rows)
+            out[rows] = eng.worker_gradient(0, 1.0)
+        finally:
+            eng.close()
+    assert_same_weights(out["4096"][~hot], out["0"][~hot], "short-column gradient")
+    go = oracle.grad_csr((rp, col, val), lab, oracle.batch_rows(len(lab), -1, 0), w0)
+    a, b = out["4096"][hot].astype(np.float64), go[hot].astype(np.float64)
+    assert np.all(np.abs(a - b) <= 1e-5 * np.abs(b) + 1e-9), np.max(np.abs(a - b) / np.abs(b))
+
+
+@pytest.mark.parametrize("B", [2000, -1])
+@pytest.mark.parametrize("value_mode", [0, 1])
+def test_long_phases_small_threshold(classic, monkeypatch, B, value_mode):
+    # many long columns (threshold 50 entries), several batches each with its
+    # own phases (row16 batches), valued and unit shards: within tolerance
+    # of the oracle and deterministic
+    monkeypatch.setenv("DLR_BAND_ROWS", "256")
+    monkeypatch.setenv("DLR_LONG_COLUMN", "50")
+    D = 2000
+    ds = dlr.Dataset.generate(20_000, D, 12, value_mode=value_mode, seed=9, stream=1)
+    got = run_engine([ds], D, 2, B, 0.1)
+    orc = oracle.run_worker([_csr_shard(ds)], D, 2, B, 0.1)
+    _within(got.w, orc.w)
+    again = run_engine([ds], D, 2, B, 0.1)
+    assert_same_weights(again.w, got.w)
+
+
+def test_banded_forced_collectives(classic, monkeypatch):
+    # key-range all-to-all + merge + all-gather (1-rank communicator)
+    monkeypatch.setenv("DLR_FORCE_COLLECTIVES", "1")
+    monkeypatch.setenv("DLR_BAND_ROWS", "16")
+    meta = read_golden_json("trajectories.json")["c1_W1_Bfull_mean"]
+    base = os.path.join(GOLDEN, meta["dataset"])
+    ds = dlr.Dataset.load_libsvm(os.path.join(base, "train", "part-001"), 123)
+    res = run_engine([ds], 123, meta["num_iteration"], meta["batch_size"], meta["learning_rate"],
+                     mode=meta["mode"])
+    assert res.w.astype("<f4").tobytes().hex() == meta["w"]

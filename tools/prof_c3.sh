@@ -1,3 +1,5 @@
+#!/bin/bash
+# C3 kernel-trace profile (rocprofv3 --stats), per-kernel averages printed.
 set -o pipefail
 R=$(pwd); export TMPDIR=/tmp; mkdir -p gpurun_out/pc3
 cd /tmp
