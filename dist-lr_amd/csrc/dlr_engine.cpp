@@ -103,6 +103,8 @@ struct TrainShard {
         int64_t pair, ptr, ent, ws, nwaves;  // offsets into bcols, bptr, brow/bval, bws
     };
     int band_shift = 0;
+    // margin with the hot (lowest, frequency-ordered) weights in LDS
+    bool margin_hot = false;
     std::vector<Band> bands;
     std::vector<int64_t> bfirst;
     uint32_t *bcols = nullptr, *bptr = nullptr, *bws = nullptr;
@@ -1016,6 +1018,7 @@ hipError_t launch_margin(dlr_ctx *c, int64_t b) {
         if (e != hipSuccess) return e;
         return dlr::launch_dense_margin(dd, first, t.plan[(size_t)b].rows, c->w, c->resid, c->stream);
     }
+    if (t.margin_hot) return dlr::launch_margin_hot(batch_view(c, b), c->w, c->resid, c->stream);
     return dlr::launch_margin_residual(batch_view(c, b), c->w, c->resid, c->stream);
 }
 
@@ -1250,6 +1253,10 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         std::vector<int32_t> np;
         if (!t.touched && (rc = column_order(c, *ds, np))) return rc;
         if ((rc = change_perm(c, std::move(np)))) return rc;
+        // DLR_MARGIN_HOT=0|1 forces the LDS hot-weight margin (it needs D >=
+        // kMarginHot); default: on for frequency-ordered shards
+        const char *mh = getenv("DLR_MARGIN_HOT");
+        t.margin_hot = D >= dlr::kMarginHot && (mh ? atoi(mh) != 0 : !c->perm.empty());
         if (!c->perm.empty()) {
             mapped.resize(ds->col.size());
             const int nt = dlr::default_threads();

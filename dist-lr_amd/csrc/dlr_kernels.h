@@ -126,6 +126,11 @@ struct RankSizes {
 };
 
 hipError_t launch_margin_residual(const DevBatch &bt, const float *w, float *resid, hipStream_t s);
+// The same margins with w[0, kMarginHot) staged in LDS (frequency-ordered
+// shards; needs D >= kMarginHot).
+constexpr int kMarginHot = 8192;
+constexpr int kMarginHotWaves = 8;
+hipError_t launch_margin_hot(const DevBatch &bt, const float *w, float *resid, hipStream_t s);
 int predict_grid(int64_t rows);
 hipError_t launch_predict(const DevBatch &bt, const float *w, unsigned long long *correct, double *ll_part,
                           double *ll_out, hipStream_t s);

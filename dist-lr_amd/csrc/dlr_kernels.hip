@@ -94,11 +94,15 @@ __device__ __forceinline__ V load_stream(const V *p) {
 // acc0: the sum the segment continues (0.0f: a whole segment; the band
 // kernel passes a column's sum over the earlier row bands, which continues
 // the same sequential chain).
-template <typename IdxT, bool UNIT = false>
+// HOT > 0: table[0, HOT) is also staged in LDS at `hot` (the frequency-
+// ordered hot weights); those gathers read LDS, the others read table
+// (each lane issues both, with the unused one clamped to index 0: no
+// divergent load, and the clamped global lanes share one L1 line).
+template <typename IdxT, bool UNIT = false, int HOT = 0>
 __device__ __forceinline__ float ordered_segment_dot(int64_t e0, int64_t e1, int64_t a, int64_t b, int lane,
                                                      const IdxT *__restrict__ idx, const float *__restrict__ val,
                                                      const float *__restrict__ table, float *lds,
-                                                     float acc0 = 0.0f) {
+                                                     float acc0 = 0.0f, const float *hot = nullptr) {
     using IV = typename Vec4<IdxT>::type;
     constexpr int kT = kWin / (kVec * kWave);
     constexpr int kChunk = kVec * kWave;  // entries per (t) step of the wave
@@ -134,10 +138,21 @@ __device__ __forceinline__ float ordered_segment_dot(int64_t e0, int64_t e1, int
                 const unsigned i1 = (e + 1 >= e0 && e + 1 < e1) ? (unsigned)iv[t].y : 0u;
                 const unsigned i2 = (e + 2 >= e0 && e + 2 < e1) ? (unsigned)iv[t].z : 0u;
                 const unsigned i3 = (e + 3 >= e0 && e + 3 < e1) ? (unsigned)iv[t].w : 0u;
-                g[t][0] = table[i0];
-                g[t][1] = table[i1];
-                g[t][2] = table[i2];
-                g[t][3] = table[i3];
+                if constexpr (HOT > 0) {
+                    const float h0 = hot[i0 < HOT ? i0 : 0u], h1 = hot[i1 < HOT ? i1 : 0u];
+                    const float h2 = hot[i2 < HOT ? i2 : 0u], h3 = hot[i3 < HOT ? i3 : 0u];
+                    const float c0 = table[i0 < HOT ? 0u : i0], c1 = table[i1 < HOT ? 0u : i1];
+                    const float c2 = table[i2 < HOT ? 0u : i2], c3 = table[i3 < HOT ? 0u : i3];
+                    g[t][0] = i0 < HOT ? h0 : c0;
+                    g[t][1] = i1 < HOT ? h1 : c1;
+                    g[t][2] = i2 < HOT ? h2 : c2;
+                    g[t][3] = i3 < HOT ? h3 : c3;
+                } else {
+                    g[t][0] = table[i0];
+                    g[t][1] = table[i1];
+                    g[t][2] = table[i2];
+                    g[t][3] = table[i3];
+                }
             }
         }
 #pragma unroll
@@ -203,6 +218,42 @@ __global__ __launch_bounds__(kWaves *kWave) void k_margin_residual(DevBatch bt, 
     const int64_t a = valid ? bt.row_ptr[my] : e1, b = valid ? bt.row_ptr[my + 1] : e1;
     const float z = ordered_segment_dot<int32_t, UNIT>(e0, e1, a, b, lane, bt.col, bt.val, w, s_p[wv]);
     if (valid) resid[my] = sigmoid_ref(z) - y;
+}
+
+// K2 for frequency-ordered (relabeled) shards, e.g. BASELINE C3: the HOT
+// lowest-numbered -- most frequent -- weights (58% of C3's entries fall in
+// the first 8,192 columns) are staged in LDS once per workgroup, so their
+// gathers read LDS and only the tail's go to L2.  Persistent workgroups
+// (two per CU) loop over blocks of NW*SEG rows; otherwise k_margin_residual
+// (same products, same in-order sums: bitwise the same margins).
+template <int HOT, int NW, int SEG, bool UNIT>
+__global__ __launch_bounds__(NW *kWave) void k_margin_hot(DevBatch bt, const float *__restrict__ w,
+                                                          float *__restrict__ resid) {
+    __shared__ __attribute__((aligned(16))) float s_w[HOT];
+    __shared__ float s_p[NW][kWin];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    {
+        const float4 *src = reinterpret_cast<const float4 *>(w);
+        float4 *dst = reinterpret_cast<float4 *>(s_w);
+#pragma unroll
+        for (int k = 0; k < HOT / 4 / (NW * kWave); ++k) dst[k * NW * kWave + threadIdx.x] = src[k * NW * kWave + threadIdx.x];
+    }
+    __syncthreads();
+    const int64_t nblk = (bt.rows + NW * SEG - 1) / (NW * SEG);
+    for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const int64_t row0 = (blk * NW + wv) * SEG;
+        if (row0 >= bt.rows) continue;  // wave-uniform (no barrier in the loop)
+        const int64_t my = row0 + lane;
+        const bool valid = lane < SEG && my < bt.rows;
+        const float y = valid ? bt.label[my] : 0.0f;
+        const int64_t rlast = min(row0 + SEG, bt.rows);
+        const int64_t e0 = bt.row_ptr[row0], e1 = bt.row_ptr[rlast];
+        const int64_t a = valid ? bt.row_ptr[my] : e1, b = valid ? bt.row_ptr[my + 1] : e1;
+        const float z = ordered_segment_dot<int32_t, UNIT, HOT>(e0, e1, a, b, lane, bt.col, bt.val, w, s_p[wv],
+                                                                 0.0f, s_w);
+        if (valid) resid[my] = sigmoid_ref(z) - y;
+    }
 }
 
 __device__ __forceinline__ double softplus(double t) { return t > 0 ? t + log1p(exp(-t)) : log1p(exp(t)); }
@@ -379,7 +430,16 @@ __global__ __launch_bounds__(256) void k_long_combine(const uint32_t *__restrict
     if (l >= ncols) return;  // wave-uniform
     const uint32_t s0 = cseg[l], s1 = cseg[l + 1];
     float G = 0.0f;
-    for (uint32_t s = s0 + (uint32_t)lane; s < s1; s += kWave) G = G + part[s];
+    uint32_t s = s0 + (uint32_t)lane;
+    // 8 partials in flight per lane, added in the same order
+    for (; s + 7 * kWave < s1; s += 8 * kWave) {
+        float x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = part[s + u * kWave];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) G = G + x[u];
+    }
+    for (; s < s1; s += kWave) G = G + part[s];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) G = G + __shfl_xor(G, off);
     if (lane != 0) return;
@@ -656,15 +716,17 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad_band(DevBand bd, const R
     const int wv = threadIdx.x / kWave;
     const int64_t wid = (int64_t)blockIdx.x * kWaves + wv;
     if (wid >= bd.nwaves) return;  // wave-uniform
-    const int64_t s0 = bd.wstart[wid], sl = bd.wstart[wid + 1];
+    // every access but the residual gathers is non-temporal: the pairs'
+    // columns and pointers (37 MB per band at C3) and the running sums (a
+    // 64 MB array) must not evict the band's residual slice from L2
+    const int64_t s0 = __builtin_nontemporal_load(bd.wstart + wid), sl = __builtin_nontemporal_load(bd.wstart + wid + 1);
     const int64_t sg = s0 + lane;
     const bool valid = sg < sl;
-    const uint32_t j = valid ? bd.cols[sg] : 0u;
-    // non-temporal: the running sums (a 64 MB array at C3) must not evict
-    // the band's residual slice from L2
+    const uint32_t j = valid ? __builtin_nontemporal_load(bd.cols + sg) : 0u;
     const float acc0 = valid ? __builtin_nontemporal_load(gacc + j) : 0.0f;
-    const int64_t e0 = bd.ptr[s0], e1 = bd.ptr[sl];
-    const int64_t a = valid ? (int64_t)bd.ptr[sg] : e1, b = valid ? (int64_t)bd.ptr[sg + 1] : e1;
+    const int64_t e0 = __builtin_nontemporal_load(bd.ptr + s0), e1 = __builtin_nontemporal_load(bd.ptr + sl);
+    const int64_t a = valid ? (int64_t)__builtin_nontemporal_load(bd.ptr + sg) : e1;
+    const int64_t b = valid ? (int64_t)__builtin_nontemporal_load(bd.ptr + sg + 1) : e1;
     const float G = ordered_segment_dot<RowT, UNIT>(e0, e1, a, b, lane, brow, bd.val, resid, s_p[wv], acc0);
     if (valid) __builtin_nontemporal_store(G, gacc + j);
 }
@@ -1151,6 +1213,38 @@ hipError_t launch_margin_residual(const DevBatch &bt, const float *w, float *res
             return hipErrorInvalidValue;
     }
 #undef DLR_MR
+    return hipGetLastError();
+}
+
+hipError_t launch_margin_hot(const DevBatch &bt, const float *w, float *resid, hipStream_t s) {
+    if (bt.rows <= 0) return hipSuccess;
+    static const int ncu = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            n = 256;
+        return n > 0 ? n : 256;
+    }();
+    constexpr int NW = kMarginHotWaves;
+    const bool unit = bt.val == nullptr;
+#define DLR_MH(SEG)                                                                                                 \
+    case SEG: {                                                                                                     \
+        const unsigned grid = std::min<unsigned>(grid_for(bt.rows, NW * SEG), (unsigned)ncu * 2);                  \
+        if (unit)                                                                                                   \
+            hipLaunchKernelGGL((k_margin_hot<kMarginHot, NW, SEG, true>), dim3(grid), dim3(NW * kWave), 0, s, bt, w, \
+                               resid);                                                                              \
+        else                                                                                                        \
+            hipLaunchKernelGGL((k_margin_hot<kMarginHot, NW, SEG, false>), dim3(grid), dim3(NW * kWave), 0, s, bt,  \
+                               w, resid);                                                                           \
+        break;                                                                                                      \
+    }
+    switch (margin_seg(bt)) {
+        DLR_MH(16)
+        DLR_MH(32)
+        DLR_MH(64)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef DLR_MH
     return hipGetLastError();
 }
 

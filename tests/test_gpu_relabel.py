@@ -120,3 +120,30 @@ def test_c3_shape_relabels_by_default():
         assert not eng.train_relabeled()
     finally:
         eng.close()
+
+
+# ---- the LDS hot-weight margin (k_margin_hot): on by default for relabeled
+# shards with D >= 8,192; the same products in the same order -> bitwise
+
+@pytest.mark.parametrize("relabel", ["0", "1"])
+@pytest.mark.parametrize("B", [7, 500, -1])
+def test_hot_margin_forced_bitwise(monkeypatch, relabel, B):
+    monkeypatch.setenv("DLR_MARGIN_HOT", "1")
+    monkeypatch.setenv("DLR_RELABEL", relabel)
+    D = 20000   # > 8,192 hot weights: rows mix LDS and global gathers
+    ds = dlr.Dataset.generate(3000, D, 30, value_mode=1, seed=4, stream=1)
+    eng = run_engine([ds], D, 2, B, 0.2)
+    rp, col, val, lab = ds.csr()
+    orc = oracle.run_worker([((rp, col, val), lab)], D, 2, B, 0.2)
+    compare_runs(eng, orc)
+
+
+def test_hot_margin_c3_equals_plain(monkeypatch):
+    # C3-shaped hashed rows (relabeled, Zipf): hot margin on vs off
+    D = 1 << 24
+    ds = dlr.Dataset.generate_hashed(40_000, D, 39, seed=10, stream=1)
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("DLR_MARGIN_HOT", flag)
+        out.append(run_engine([ds], D, 2, 4096, 0.2).w)
+    assert_same_weights(out[1], out[0])
