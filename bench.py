@@ -154,6 +154,8 @@ def main():
         if world == 1 and args.gpus > 1:
             sys.exit("--gpus N > 1 needs torch.distributed.run (one process per GPU)")
     distributed = world > 1
+    if torch is not None and torch.cuda.is_available():
+        torch.cuda.set_device(local)  # torch.cuda.synchronize() below then waits on this rank's GPU only
     if distributed:
         dist.init_process_group("gloo")   # control plane only; data path is RCCL inside the library
     D, B = args.features, args.batch
