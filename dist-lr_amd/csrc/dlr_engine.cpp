@@ -670,7 +670,7 @@ void build_bands(const std::vector<uint32_t> &cptr, const std::vector<RowT> &cro
             int cols = 0;
             for (int64_t q = 0; q < p; ++q) {
                 const int64_t cq = (int64_t)pp[q + 1] - (int64_t)pp[q];
-                if (cols == 64 || (cols > 0 && acc + cq > 1024)) {
+                if (cols == 64 * dlr::kBandPairsPerLane || (cols > 0 && acc + cq > 1024)) {
                     out.ws.push_back((uint32_t)q);
                     acc = 0;
                     cols = 0;
@@ -740,7 +740,7 @@ void build_long_phases(const std::vector<LongBatch<RowT>> &lb, int64_t B, bool u
                 cur[(size_t)(p * nl + l)] = d.ent + at;
                 for (int64_t o = 0; o < c; o += kPiece) {
                     const int64_t n = std::min(kPiece, c - o);
-                    if (pieces == 64 || (pieces > 0 && acc + n > 1024)) {
+                    if (pieces == 64 * dlr::kBandPairsPerLane || (pieces > 0 && acc + n > 1024)) {
                         out.ws.push_back((uint32_t)np);
                         acc = 0;
                         pieces = 0;

@@ -76,8 +76,9 @@ struct DevPcsc {
 // batches): for one band, the (column, segment) pairs of the short columns
 // with entries in the band, columns ascending; pair s is column cols[s] with
 // entries [ptr[s], ptr[s+1]) of row/val (batch-local rows, ascending).  Wave
-// k sums pairs [wstart[k], wstart[k+1]) (<= 64 pairs, ~one window of
-// entries).  row/val are padded by >= 64 entries.
+// k sums pairs [wstart[k], wstart[k+1]) (<= 64 * kBandPairsPerLane pairs,
+// ~one window of entries).  row/val are padded by >= 64 entries.
+constexpr int kBandPairsPerLane = 4;
 struct DevBand {
     const uint32_t *cols;
     const uint32_t *ptr;

@@ -192,6 +192,87 @@ __device__ __forceinline__ float ordered_segment_dot(int64_t e0, int64_t e1, int
     return acc;
 }
 
+// ordered_segment_dot for K segments per lane (short segments: the band
+// kernel's (column, band) pairs average ~3.6 entries, so 64 per wave left
+// its windows a quarter full).  Lane l owns segments [a[k], b[k]) for
+// k < K (empty: a == b), each summed in order from acc[k]; the wave's
+// entries are [e0, e1).  Same loads, gathers and products as
+// ordered_segment_dot.
+template <typename IdxT, bool UNIT, int K>
+__device__ __forceinline__ void ordered_segments_dot(int64_t e0, int64_t e1, const int64_t (&a)[K],
+                                                     const int64_t (&b)[K], float (&acc)[K], int lane,
+                                                     const IdxT *__restrict__ idx, const float *__restrict__ val,
+                                                     const float *__restrict__ table, float *lds) {
+    using IV = typename Vec4<IdxT>::type;
+    constexpr int kT = kWin / (kVec * kWave);
+    constexpr int kChunk = kVec * kWave;
+    const int64_t base = e0 & ~int64_t(kVec - 1);
+    for (int64_t ws = base; ws < e1; ws += kWin) {
+        const int64_t left = e1 - ws;  // wave-uniform
+        IV iv[kT];
+        float4 v[kT];
+#pragma unroll
+        for (int t = 0; t < kT; ++t) {
+            if (t * kChunk < left) {
+                const int64_t e = ws + t * kChunk + lane * kVec;
+                const int64_t ec = e < e1 ? e : ws + t * kChunk;
+                iv[t] = load_stream(reinterpret_cast<const IV *>(idx + ec));
+                if constexpr (UNIT)
+                    v[t] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+                else
+                    v[t] = load_stream(reinterpret_cast<const float4 *>(val + ec));
+            }
+        }
+        float g[kT][kVec];
+#pragma unroll
+        for (int t = 0; t < kT; ++t) {
+            if (t * kChunk < left) {
+                const int64_t e = ws + t * kChunk + lane * kVec;
+                const unsigned i0 = (e >= e0 && e < e1) ? (unsigned)iv[t].x : 0u;
+                const unsigned i1 = (e + 1 >= e0 && e + 1 < e1) ? (unsigned)iv[t].y : 0u;
+                const unsigned i2 = (e + 2 >= e0 && e + 2 < e1) ? (unsigned)iv[t].z : 0u;
+                const unsigned i3 = (e + 3 >= e0 && e + 3 < e1) ? (unsigned)iv[t].w : 0u;
+                g[t][0] = table[i0];
+                g[t][1] = table[i1];
+                g[t][2] = table[i2];
+                g[t][3] = table[i3];
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < kT; ++t) {
+            if (t * kChunk < left) {
+                const int o = t * kChunk + lane * kVec;
+                const int64_t e = ws + o;
+                float4 p;
+                p.x = (e >= e0 && e < e1) ? g[t][0] * v[t].x : 0.0f;
+                p.y = (e + 1 >= e0 && e + 1 < e1) ? g[t][1] * v[t].y : 0.0f;
+                p.z = (e + 2 >= e0 && e + 2 < e1) ? g[t][2] * v[t].z : 0.0f;
+                p.w = (e + 3 >= e0 && e + 3 < e1) ? g[t][3] * v[t].w : 0.0f;
+                *reinterpret_cast<float4 *>(lds + o) = p;
+            }
+        }
+        wave_sync();
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t lo = a[k] > ws ? a[k] : ws;
+            const int64_t hi = b[k] < ws + kWin ? b[k] : ws + kWin;
+            int o = (int)(lo - ws);
+            const int oe = (int)(hi - ws);
+            float s = acc[k];
+            for (; o + 4 <= oe; o += 4) {
+                const float x0 = lds[o], x1 = lds[o + 1], x2 = lds[o + 2], x3 = lds[o + 3];
+                s = s + x0;
+                s = s + x1;
+                s = s + x2;
+                s = s + x3;
+            }
+            for (; o < oe; ++o) s = s + lds[o];
+            acc[k] = s;
+        }
+        wave_sync();
+    }
+}
+
 __device__ __forceinline__ float sigmoid_ref(float z) {
     // lr.cc:113: 1. / (1. + exp(-z)) in double (glibc double exp there,
     // OCML's f64 exp here), returned as float.
@@ -712,6 +793,7 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad_band(DevBand bd, const R
                                                              const float *__restrict__ resid,
                                                              float *__restrict__ gacc) {
     __shared__ float s_p[kWaves][kWin];
+    constexpr int K = kBandPairsPerLane;
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
     const int64_t wid = (int64_t)blockIdx.x * kWaves + wv;
@@ -720,15 +802,25 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad_band(DevBand bd, const R
     // columns and pointers (37 MB per band at C3) and the running sums (a
     // 64 MB array) must not evict the band's residual slice from L2
     const int64_t s0 = __builtin_nontemporal_load(bd.wstart + wid), sl = __builtin_nontemporal_load(bd.wstart + wid + 1);
-    const int64_t sg = s0 + lane;
-    const bool valid = sg < sl;
-    const uint32_t j = valid ? __builtin_nontemporal_load(bd.cols + sg) : 0u;
-    const float acc0 = valid ? __builtin_nontemporal_load(gacc + j) : 0.0f;
     const int64_t e0 = __builtin_nontemporal_load(bd.ptr + s0), e1 = __builtin_nontemporal_load(bd.ptr + sl);
-    const int64_t a = valid ? (int64_t)__builtin_nontemporal_load(bd.ptr + sg) : e1;
-    const int64_t b = valid ? (int64_t)__builtin_nontemporal_load(bd.ptr + sg + 1) : e1;
-    const float G = ordered_segment_dot<RowT, UNIT>(e0, e1, a, b, lane, brow, bd.val, resid, s_p[wv], acc0);
-    if (valid) __builtin_nontemporal_store(G, gacc + j);
+    // lane l owns pairs s0 + l + 64k
+    int64_t a[K], b[K];
+    float acc[K];
+    uint32_t j[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int64_t sg = s0 + lane + (int64_t)k * kWave;
+        const bool valid = sg < sl;
+        j[k] = valid ? __builtin_nontemporal_load(bd.cols + sg) : 0u;
+        a[k] = valid ? (int64_t)__builtin_nontemporal_load(bd.ptr + sg) : e1;
+        b[k] = valid ? (int64_t)__builtin_nontemporal_load(bd.ptr + sg + 1) : e1;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = s0 + lane + (int64_t)k * kWave < sl ? __builtin_nontemporal_load(gacc + j[k]) : 0.0f;
+    ordered_segments_dot<RowT, UNIT, K>(e0, e1, a, b, acc, lane, brow, bd.val, resid, s_p[wv]);
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        if (s0 + lane + (int64_t)k * kWave < sl) __builtin_nontemporal_store(acc[k], gacc + j[k]);
 }
 
 // Long columns in ROW PHASES (band mode).  The chunked long path gathers
@@ -766,15 +858,26 @@ __global__ __launch_bounds__(kLPWaves *kWave) void k_long_phase(DevLPhase lp, co
     const uint32_t *ws = lp.ws + d.ws;
     const uint16_t *row = lp.row + d.ent;
     const float *val = UNIT ? nullptr : lp.val + d.ent;
+    constexpr int K = kBandPairsPerLane;  // pieces per lane: s0 + lane + 64k
     for (int64_t t = wv; t < d.ntasks; t += kLPWaves) {  // wave-uniform
         const int64_t s0 = ws[t], sl = ws[t + 1];
-        const int64_t q = s0 + lane;
-        const bool valid = q < sl;
         const int64_t e0 = ptr[s0], e1 = ptr[sl];
-        const int64_t a = valid ? (int64_t)ptr[q] : e1, b = valid ? (int64_t)ptr[q + 1] : e1;
-        const uint32_t slot = valid ? lp.slot[d.ptr + q] : 0u;
-        const float G = ordered_segment_dot<uint16_t, UNIT>(e0, e1, a, b, lane, row, val, s_r, slab);
-        if (valid) part[slot] = G;
+        int64_t a[K], b[K];
+        float acc[K];
+        uint32_t slot[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t q = s0 + lane + (int64_t)k * kWave;
+            const bool valid = q < sl;
+            a[k] = valid ? (int64_t)ptr[q] : e1;
+            b[k] = valid ? (int64_t)ptr[q + 1] : e1;
+            slot[k] = valid ? lp.slot[d.ptr + q] : 0u;
+            acc[k] = 0.0f;
+        }
+        ordered_segments_dot<uint16_t, UNIT, K>(e0, e1, a, b, acc, lane, row, val, s_r, slab);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (s0 + lane + (int64_t)k * kWave < sl) part[slot[k]] = acc[k];
     }
 }
 
