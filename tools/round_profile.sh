@@ -17,4 +17,5 @@ for cfg in c2 c3 c4 c5 c4s; do
       -d "$R/gpurun_out/rp/prof_$cfg" -o run -- python3 "$R/bench.py" --config $cfg $extra --no-cpu-baseline \
       > "$R/gpurun_out/rp/prof_$cfg.json" 2> "$R/gpurun_out/rp/prof_$cfg.err" ) || exit 1
 done && \
-echo "== pmc" && bash tools/pmc_pass.sh > gpurun_out/rp/pmc_pass.log 2>&1 && echo "round profile done"
+if [ "${RP_PMC:-1}" = 1 ]; then echo "== pmc" && bash tools/pmc_pass.sh > gpurun_out/rp/pmc_pass.log 2>&1; fi && \
+echo "round profile done"
