@@ -696,7 +696,12 @@ void build_bands(const std::vector<uint32_t> &cptr, const std::vector<RowT> &cro
 // l's pieces, phase by phase, from cseg[l] -- so k_long_combine adds each
 // column's partials in row order.  Per phase an entry-balanced wave
 // schedule over the pieces (<= 64 pieces, ~kWin entries per wave).
-constexpr int64_t kPiece = 64;
+// DLR_LONG_PIECE overrides the piece size (1..1024; default 64)
+int64_t long_piece() {
+    const char *e = getenv("DLR_LONG_PIECE");
+    const int64_t v = e ? atoll(e) : 64;
+    return v >= 1 && v <= 1024 ? v : 64;
+}
 struct LPhaseBuild {
     std::vector<dlr::PhaseDesc> desc;
     std::vector<uint32_t> ptr, slot, ws, cseg;
@@ -708,6 +713,7 @@ struct LPhaseBuild {
 template <typename RowT>
 void build_long_phases(const std::vector<LongBatch<RowT>> &lb, int64_t B, bool unit, LPhaseBuild &out) {
     const int64_t nph = (B + dlr::kLPhase - 1) / dlr::kLPhase;
+    const int64_t kPiece = long_piece();
     for (const LongBatch<RowT> &L : lb) {
         const int64_t nl = (int64_t)L.cols.size();
         std::vector<int64_t> cnt((size_t)(nph * nl), 0);  // [p][l]
