@@ -165,12 +165,12 @@ def test_c3_banded_pushed_gradient(monkeypatch):
     assert np.all(np.abs(a - b) <= 1e-5 * np.abs(b) + 1e-9), np.max(np.abs(a - b) / np.abs(b))
 
 
-@pytest.mark.parametrize("B", [2000, -1])
+@pytest.mark.parametrize("B", [2000, 3000, -1])
 @pytest.mark.parametrize("value_mode", [0, 1])
 def test_long_phases_small_threshold(classic, monkeypatch, B, value_mode):
     # many long columns (threshold 50 entries), several batches each with its
-    # own phases (row16 batches), valued and unit shards: within tolerance
-    # of the oracle and deterministic
+    # own phases (row16 batches; B = 3,000 wraps to row 0), valued and unit
+    # shards: within tolerance of the oracle and deterministic
     monkeypatch.setenv("DLR_BAND_ROWS", "256")
     monkeypatch.setenv("DLR_LONG_COLUMN", "50")
     D = 2000
