@@ -46,6 +46,11 @@ def log(*a):
 # (configs[1], the headline single-GPU workload); the others are run with
 # --config for their own bench lines.
 CONFIGS = {
+    # C1: examples/local.sh's a9a-shaped worker shard (D = 123, 14 binary
+    # features/row, 8,140 rows per part file, B = -1: one full-shard step per
+    # epoch); latency-bound, reported in absolute terms
+    "c1": dict(rows=8140, features=123, nnz=14, batch=-1, value_mode=0, steps=2000, warmup=50,
+               label="C1 local.sh a9a-shaped LR"),
     "c2": dict(rows=10_000_000, features=1_000_000, nnz=50, batch=65536, value_mode=1, steps=1000, warmup=50,
                label="C2 sparse LR"),
     # C3: per-GPU shard of the 100M-row Criteo-shaped set (8 GPUs); one step
@@ -119,7 +124,7 @@ def cpu_baseline(args, D: int) -> dict:
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # checker only: timed as the CPU baseline, never as the product
 
-    B = args.batch if args.batch > 0 else 200_000   # full-shard configs: a 200k-row shard, B = -1
+    B = args.batch if args.batch > 0 else min(args.rows, 200_000)  # full-shard configs: B = -1 over <=200k rows
     n_rows = 4 * B if args.batch > 0 else B
     ds = make_shard(args, n_rows, 1)
     if args.kind == "dense":

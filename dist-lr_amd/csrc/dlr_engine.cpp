@@ -1024,7 +1024,7 @@ hipError_t launch_margin(dlr_ctx *c, int64_t b) {
         if (e != hipSuccess) return e;
         return dlr::launch_dense_margin(dd, first, t.plan[(size_t)b].rows, c->w, c->resid, c->stream);
     }
-    if (t.margin_hot) return dlr::launch_margin_hot(batch_view(c, b), c->w, c->resid, c->stream);
+    if (t.margin_hot) return dlr::launch_margin_hot(batch_view(c, b), c->w, c->D, c->resid, c->stream);
     return dlr::launch_margin_residual(batch_view(c, b), c->w, c->resid, c->stream);
 }
 

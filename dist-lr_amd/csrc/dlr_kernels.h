@@ -131,7 +131,7 @@ hipError_t launch_margin_residual(const DevBatch &bt, const float *w, float *res
 // shards; needs D >= kMarginHot).
 constexpr int kMarginHot = 8192;
 constexpr int kMarginHotWaves = 8;
-hipError_t launch_margin_hot(const DevBatch &bt, const float *w, float *resid, hipStream_t s);
+hipError_t launch_margin_hot(const DevBatch &bt, const float *w, int64_t D, float *resid, hipStream_t s);
 int predict_grid(int64_t rows);
 hipError_t launch_predict(const DevBatch &bt, const float *w, unsigned long long *correct, double *ll_part,
                           double *ll_out, hipStream_t s);

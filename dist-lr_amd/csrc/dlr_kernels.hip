@@ -174,6 +174,25 @@ __device__ __forceinline__ float ordered_segment_dot(int64_t e0, int64_t e1, int
         const int64_t hi = b < ws + kWin ? b : ws + kWin;
         int o = (int)(lo - ws);
         const int oe = (int)(hi - ws);
+        if (oe - o >= 64) {
+            // a long run (a column of a small-D full batch: C1's 123 columns
+            // hold ~900 entries each): 16-byte reads, 32 products per LDS
+            // wait, same order.  Rows of a margin never get here (their
+            // runs are the row lengths, well under 64 at every config).
+            for (; o & 3; ++o) acc = acc + lds[o];
+            for (; o + 32 <= oe; o += 32) {
+                float4 q[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) q[u] = *reinterpret_cast<const float4 *>(lds + o + 4 * u);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    acc = acc + q[u].x;
+                    acc = acc + q[u].y;
+                    acc = acc + q[u].z;
+                    acc = acc + q[u].w;
+                }
+            }
+        }
         for (; o + 8 <= oe; o += 8) {
             const float x0 = lds[o], x1 = lds[o + 1], x2 = lds[o + 2], x3 = lds[o + 3];
             const float x4 = lds[o + 4], x5 = lds[o + 5], x6 = lds[o + 6], x7 = lds[o + 7];
@@ -1344,7 +1363,7 @@ hipError_t launch_mh(const DevBatch &bt, const float *w, float *resid, unsigned 
     return hipGetLastError();
 }
 
-hipError_t launch_margin_hot(const DevBatch &bt, const float *w, float *resid, hipStream_t s) {
+hipError_t launch_margin_hot(const DevBatch &bt, const float *w, int64_t D, float *resid, hipStream_t s) {
     if (bt.rows <= 0) return hipSuccess;
     static const int ncu = [] {
         int dev = 0, n = 0;
@@ -1352,9 +1371,19 @@ hipError_t launch_margin_hot(const DevBatch &bt, const float *w, float *resid, h
             n = 256;
         return n > 0 ? n : 256;
     }();
-    // 8,192 hot weights x 8 waves, 2 workgroups per CU: measured on C3
-    // against 4,096 x 8 (3/CU: margin 2.04 vs 1.78 ms), 2,048 x 8 (4/CU:
-    // 1.87), 8,192 x 4 (3/CU: 1.79) and 4,096 x 4 (5/CU: 2.22)
+    // 16,384 hot weights x 16 waves, one workgroup per CU, when D allows (C3
+    // margin 1.749 ms), else 8,192 x 8, two per CU (1.779 ms).  Also
+    // measured on C3: 16,384 x 8 (2.01 ms), 24,576 x 8 (2.00), 4,096 x 8
+    // (2.04), 2,048 x 8 (1.87), 8,192 x 4 (1.79), 4,096 x 4 (2.22).
+    // DLR_MARGIN_HOT_SHAPE (A/B only): 1 = 8,192 x 8, 2 = 16,384 x 8,
+    // 3 = 24,576 x 8 (each only when D >= its hot count).
+    static const int shape = [] {
+        const char *e = getenv("DLR_MARGIN_HOT_SHAPE");
+        return e ? atoi(e) : 0;
+    }();
+    if (shape == 0 && D >= 16384) return launch_mh<16384, 16>(bt, w, resid, (unsigned)ncu, s);
+    if (shape == 2 && D >= 16384) return launch_mh<16384, 8>(bt, w, resid, (unsigned)ncu, s);
+    if (shape == 3 && D >= 24576) return launch_mh<24576, 8>(bt, w, resid, (unsigned)ncu, s);
     return launch_mh<kMarginHot, kMarginHotWaves>(bt, w, resid, (unsigned)ncu * 2, s);
 }
 
