@@ -11,7 +11,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-me
 echo "== smoke" && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" && \
 echo "== bench c2" && timeout -k 10 400 python -u bench.py > gpurun_out/rp/bench_c2.json 2> gpurun_out/rp/bench_c2.err && \
 tail -c 400 gpurun_out/rp/bench_c2.json && echo && \
-for cfg in c2 c3 c4 c5 c4s; do
+for cfg in c1 c2 c3 c4 c5 c4s; do
   extra=""; [ $cfg = c4s ] && extra="--steps 12 --warmup 2"
   echo "== rocprofv3 $cfg" && ( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
       -d "$R/gpurun_out/rp/prof_$cfg" -o run -- python3 "$R/bench.py" --config $cfg $extra --no-cpu-baseline \
