@@ -142,9 +142,9 @@ def cpu_baseline(args, D: int) -> dict:
         oracle.server_update(w, [g], args.lr)
         done += 1
         el = time.perf_counter() - t0
-        if el >= args.cpu_seconds or done >= 5000:
+        if el >= args.cpu_seconds or done >= 200_000:
             break
-    return {"value": round(done * B / el, 1), "unit": "samples/s", "cores": 1, "kind": "port",
+    return {"value": round(done * B / el, 1), "unit": "samples/s", "cores": 1, "host_cpus": os.cpu_count(), "kind": "port",
             "sample": f"{done} steps of B={B}, D={D}, {args.nnz} nnz/row (oracle "
                       f"{'dense' if args.kind == 'dense' else 'sparse'} port, 1 thread) in "
                       f"{el:.1f} s"}
