@@ -903,22 +903,50 @@ __global__ __launch_bounds__(kLPWaves *kWave) void k_long_phase(DevLPhase lp, co
 // After the bands (and the long columns' combine, RAW into gacc): lr.cc:40
 // and the update (FUSED) or the pushed gradient, for every column -- an
 // untouched column has G = +0 there, as in k_grad.
+// Four columns per thread (16-byte loads and stores; gacc, read once, with
+// non-temporal loads); a scalar tail when D % 4 != 0.  Per column the same
+// arithmetic as k_grad's epilogue.
+__device__ __forceinline__ float finalize_one(float G, float wj, float Bf, double Bd, float C) {
+    const float cw = C * wj;
+    const float l2 = cw / Bf;
+    return (float)((double)G / Bd + (double)l2);
+}
+
 template <bool FUSED>
 __global__ __launch_bounds__(256) void k_band_finalize(const float *__restrict__ gacc, float *__restrict__ w,
                                                        float *__restrict__ gout, int64_t D, float Bf, double Bd,
                                                        float lr, float C) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
     if (j >= D) return;
-    const float G = gacc[j];
-    const float wj = w[j];
-    const float cw = C * wj;
-    const float l2 = cw / Bf;
-    const float g = (float)((double)G / Bd + (double)l2);
-    if (FUSED) {
-        const float step = lr * g;
-        w[j] = wj - step;
-    } else {
-        gout[j] = g;
+    if (j + 4 <= D) {
+        const float4 G = load_stream(reinterpret_cast<const float4 *>(gacc + j));
+        const float4 wj = *reinterpret_cast<const float4 *>(w + j);
+        float4 g;
+        g.x = finalize_one(G.x, wj.x, Bf, Bd, C);
+        g.y = finalize_one(G.y, wj.y, Bf, Bd, C);
+        g.z = finalize_one(G.z, wj.z, Bf, Bd, C);
+        g.w = finalize_one(G.w, wj.w, Bf, Bd, C);
+        if (FUSED) {
+            float4 nw;
+            nw.x = wj.x - lr * g.x;
+            nw.y = wj.y - lr * g.y;
+            nw.z = wj.z - lr * g.z;
+            nw.w = wj.w - lr * g.w;
+            *reinterpret_cast<float4 *>(w + j) = nw;
+        } else {
+            *reinterpret_cast<float4 *>(gout + j) = g;
+        }
+        return;
+    }
+    for (int64_t k = j; k < D; ++k) {
+        const float wj = w[k];
+        const float g = finalize_one(gacc[k], wj, Bf, Bd, C);
+        if (FUSED) {
+            const float step = lr * g;
+            w[k] = wj - step;
+        } else {
+            gout[k] = g;
+        }
     }
 }
 
@@ -1619,10 +1647,10 @@ hipError_t launch_band_finalize(const float *gacc, float *w, float *gout, int64_
     const float Bf = (float)B;
     const double Bd = (double)B;
     if (fused)
-        hipLaunchKernelGGL(k_band_finalize<true>, dim3(grid_for(D, 256)), dim3(256), 0, s, gacc, w, gout, D, Bf, Bd,
+        hipLaunchKernelGGL(k_band_finalize<true>, dim3(grid_for((D + 3) / 4, 256)), dim3(256), 0, s, gacc, w, gout, D, Bf, Bd,
                            lr, C);
     else
-        hipLaunchKernelGGL(k_band_finalize<false>, dim3(grid_for(D, 256)), dim3(256), 0, s, gacc, w, gout, D, Bf, Bd,
+        hipLaunchKernelGGL(k_band_finalize<false>, dim3(grid_for((D + 3) / 4, 256)), dim3(256), 0, s, gacc, w, gout, D, Bf, Bd,
                            lr, C);
     return hipGetLastError();
 }
