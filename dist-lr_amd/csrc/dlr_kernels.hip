@@ -1224,24 +1224,48 @@ __global__ __launch_bounds__(256) void k_dense_grad_blocked(DevDense dd, int64_t
     }
 }
 
+// Chunk partials of 16 columns per workgroup: the 256 threads stage up to
+// 256 chunks x 16 columns in LDS with one round of 16-byte loads (every
+// workgroup's loads in flight at once: a single memory round trip per tile,
+// where a lane-per-column loop waited ~4), then lane t < 16 adds its column's
+// partials in chunk order from LDS.  Same order as before.
 template <bool FUSED>
 __global__ __launch_bounds__(256) void k_dense_combine(const float *__restrict__ part, int64_t nchunks, int64_t Dp,
                                                        int64_t D, float *__restrict__ w, float *__restrict__ gout,
                                                        float Bf, double Bd, float lr, float C) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= D) return;
-    // chunk order as before; the partials are loaded 16 at a time so the
-    // loads overlap (D threads only -- latency, not bandwidth, bounds this)
-    constexpr int U = 16;
+    constexpr int CT = 16, KT = 256;
+    __shared__ __attribute__((aligned(16))) float s_t[KT][CT];
+    const int t = threadIdx.x;
+    const int64_t j0 = (int64_t)blockIdx.x * CT;
+    const int64_t jq = j0 + 4 * (t % 4);  // this thread's column quad (Dp is a multiple of 4)
     float G = 0.0f;
-    for (int64_t k = 0; k < nchunks; k += U) {
-        float pv[U];
+    for (int64_t k0 = 0; k0 < nchunks; k0 += KT) {
+        float4 v[4];
 #pragma unroll
-        for (int u = 0; u < U; ++u) pv[u] = k + u < nchunks ? part[(k + u) * Dp + j] : 0.0f;
+        for (int u = 0; u < 4; ++u) {
+            const int64_t k = k0 + t / 4 + 64 * u;
+            v[u] = (k < nchunks && jq < Dp) ? *reinterpret_cast<const float4 *>(part + k * Dp + jq)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        __syncthreads();  // the previous tile is consumed
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (k + u < nchunks) G = G + pv[u];
+        for (int u = 0; u < 4; ++u) *reinterpret_cast<float4 *>(&s_t[t / 4 + 64 * u][4 * (t % 4)]) = v[u];
+        __syncthreads();
+        if (t < CT) {
+            const int kn = (int)min<int64_t>(KT, nchunks - k0);
+            int k = 0;
+            for (; k + 8 <= kn; k += 8) {
+                float x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = s_t[k + u][t];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) G = G + x[u];
+            }
+            for (; k < kn; ++k) G = G + s_t[k][t];
+        }
     }
+    const int64_t j = j0 + t;
+    if (t >= CT || j >= D) return;
     const float wj = w[j];
     const float cw = C * wj;
     const float l2 = cw / Bf;
@@ -1690,10 +1714,10 @@ hipError_t launch_dense_grad(const DevDense &dd, int64_t first, int64_t B, const
         hipLaunchKernelGGL(k_dense_grad_blocked<false>, dim3((unsigned)nch, grid_for(dd.D, 256)), dim3(256), 0, s,
                            dd, first, B, resid, Dp, part);
     if (fused)
-        hipLaunchKernelGGL(k_dense_combine<true>, dim3(grid_for(dd.D, 256)), dim3(256), 0, s, part, nch, Dp, dd.D, w,
+        hipLaunchKernelGGL(k_dense_combine<true>, dim3(grid_for(dd.D, 16)), dim3(256), 0, s, part, nch, Dp, dd.D, w,
                            gout, Bf, Bd, lr, C);
     else
-        hipLaunchKernelGGL(k_dense_combine<false>, dim3(grid_for(dd.D, 256)), dim3(256), 0, s, part, nch, Dp, dd.D,
+        hipLaunchKernelGGL(k_dense_combine<false>, dim3(grid_for(dd.D, 16)), dim3(256), 0, s, part, nch, Dp, dd.D,
                            w, gout, Bf, Bd, lr, C);
     return hipGetLastError();
 }
