@@ -531,7 +531,15 @@ __global__ __launch_bounds__(256) void k_long_combine(const uint32_t *__restrict
     const uint32_t s0 = cseg[l], s1 = cseg[l + 1];
     float G = 0.0f;
     uint32_t s = s0 + (uint32_t)lane;
-    // 8 partials in flight per lane, added in the same order
+    // 32 (then 8) partials in flight per lane, added in the same order: the
+    // hottest column's wave (C3: ~20K partials) is the kernel's critical path
+    for (; s + 31 * kWave < s1; s += 32 * kWave) {
+        float x[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) x[u] = part[s + u * kWave];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) G = G + x[u];
+    }
     for (; s + 7 * kWave < s1; s += 8 * kWave) {
         float x[8];
 #pragma unroll
