@@ -94,9 +94,13 @@ def parse_args():
     ap.add_argument("--lr", type=float, default=0.2)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per step (written by tools/pmc_traffic.py)")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC-derived HBM bytes per step (written by tools/pmc_traffic.py; default "
+                         "profiles/traffic.json for c2, profiles/traffic_<config>.json otherwise)")
     args = ap.parse_args()
+    if args.traffic_json is None:
+        args.traffic_json = os.path.join(ROOT, "profiles", "traffic.json" if args.config == "c2"
+                                         else f"traffic_{args.config}.json")
     cfg = CONFIGS[args.config]
     for k in ("rows", "features", "nnz", "batch", "steps", "warmup"):
         if getattr(args, k) is None:

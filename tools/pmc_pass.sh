@@ -6,17 +6,18 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
 export TMPDIR=/tmp
-mkdir -p gpurun_out/pmc
+PD=gpurun_out/pmc${CONFIG:+_$CONFIG}
+mkdir -p $PD
 STEPS=${STEPS:-40}
 cd /tmp
 for pass in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
   tag=$(echo $pass | tr ' ' '_')
   echo "== pass $tag (calibration)"
-  timeout -s KILL 120 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d "$R/gpurun_out/pmc/calib_$tag" -o run -- \
-      "$R/tools/kbench/kbench" 65536 1000000 50 40 calib > "$R/gpurun_out/pmc/calib_$tag.log" 2>&1 || exit 1
+  timeout -s KILL 120 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d "$R/$PD/calib_$tag" -o run -- \
+      "$R/tools/kbench/kbench" 65536 1000000 50 40 calib > "$R/$PD/calib_$tag.log" 2>&1 || exit 1
   echo "== pass $tag (bench)"
-  timeout -s KILL 400 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d "$R/gpurun_out/pmc/bench_$tag" -o run -- \
-      python3 "$R/bench.py" --steps $STEPS --warmup 5 --no-cpu-baseline > "$R/gpurun_out/pmc/bench_$tag.json" \
-      2> "$R/gpurun_out/pmc/bench_$tag.err" || exit 1
+  timeout -s KILL 400 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d "$R/$PD/bench_$tag" -o run -- \
+      python3 "$R/bench.py" ${CONFIG:+--config $CONFIG} --steps $STEPS --warmup ${WARMUP:-5} --no-cpu-baseline > "$R/$PD/bench_$tag.json" \
+      2> "$R/$PD/bench_$tag.err" || exit 1
 done
 echo "pmc passes done"

@@ -12,6 +12,8 @@ calibrated by that stream; the raw counters are reported beside the
 corrected figure.
 
     python tools/pmc_traffic.py gpurun_out/pmc  [--out profiles/traffic.json]
+    python tools/pmc_traffic.py gpurun_out/pmc_c3 --workload-key D16777216_nnz39_B-1 --layout classic \
+        --out profiles/traffic_c3.json
 """
 from __future__ import annotations
 
@@ -69,22 +71,29 @@ def main() -> int:
     bw = per_kernel(os.path.join(d, "bench_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE")
     hits = per_kernel(os.path.join(d, "bench_TCC_HIT_sum_TCC_MISS_sum", "run_counter_collection.csv"), "TCC_HIT_sum")
     miss = per_kernel(os.path.join(d, "bench_TCC_HIT_sum_TCC_MISS_sum", "run_counter_collection.csv"), "TCC_MISS_sum")
+    # Per train step: every dispatch of a stage's kernels summed, divided by
+    # the number of steps (= margin dispatches: bench.py runs the margin and
+    # the gradient stage equally often).  C2 has one kernel per stage; C3's
+    # gradient is 12 band launches + long phases + combine + finalize.
+    roles = [("margin", ["k_margin"]), ("grad", ["k_grad", "k_long_", "k_band_finalize"])]
+    steps = len(pick(bf, "k_margin")) or 1
     total = 0.0
-    for short, key in [("margin", "k_margin_residual"), ("grad", "k_grad")]:
-        f = pick(bf, key)
-        w = pick(bw, key)
-        h = pick(hits, key)
-        m = pick(miss, key)
+    for short, keys in roles:
+        f = [x for k in keys for x in pick(bf, k)]
+        w = [x for k in keys for x in pick(bw, k)]
+        h = [x for k in keys for x in pick(hits, k)]
+        m = [x for k in keys for x in pick(miss, k)]
         if not f:
             continue
-        fk, wk = statistics.mean(f), statistics.mean(w) if w else 0.0
+        fk, wk = sum(f) / steps, (sum(w) / steps if w else 0.0)
         rd = fk * 1024.0 * read_factor
         wr = wk * 1024.0 * write_factor
         total += rd + wr
         res["kernels"][short] = {
-            "dispatches": len(f), "FETCH_SIZE_kB": round(fk, 1), "WRITE_SIZE_kB": round(wk, 1),
+            "dispatches": len(f), "dispatches_per_step": round(len(f) / steps, 2),
+            "FETCH_SIZE_kB": round(fk, 1), "WRITE_SIZE_kB": round(wk, 1),
             "read_bytes": round(rd), "write_bytes": round(wr),
-            "l2_hit_rate": round(statistics.mean(h) / (statistics.mean(h) + statistics.mean(m)), 4) if h and m else None,
+            "l2_hit_rate": round(sum(h) / (sum(h) + sum(m)), 4) if h and m else None,
         }
     res["hbm_bytes_per_step"] = round(total)
     js = json.dumps(res, indent=1)
