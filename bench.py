@@ -8,32 +8,32 @@ C = 1.  One step = one LR::Train batch: margin + sigmoid + residual, Xᵀr
 gradient + L2, (exchange), SGD update.  Weak scaling: every rank trains its
 own 10M-row shard (rank r = part-00{r+1}, like main.cc:158).
 
-  python bench.py [--gpus N --steps K --warmup W]
-  (N > 1: launched by torch.distributed.run, one process per GPU.)
+  python bench.py [--gpus N --steps K --warmup W] [--config c1|c2|c3|c4|c4s|c5]
+
+N > 1: one process per GPU (rank r on GPU r, its own shard), RCCL over
+xGMI for the exchange.  Launched either by torch.distributed.run (RANK /
+LOCAL_RANK / WORLD_SIZE / MASTER_* in the environment) or, without those,
+by this script itself: the parent starts N rank processes with that
+environment and never touches the GPU (or imports torch); `--spawn` takes
+the same launcher path at N = 1.
 
 Prints ONE JSON line on rank 0 (stdout); progress goes to stderr.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
-
-try:
-    import torch  # noqa: F401  -- loaded first: the library binds to torch's HIP runtime
-    import torch.distributed as dist
-except Exception:  # pragma: no cover
-    torch = None
-    dist = None
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "dist-lr_amd"))
 
-import distlr_amd as dlr  # noqa: E402
+torch = dist = dlr = np = None  # imported in the rank processes only (see main)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -94,6 +94,13 @@ def parse_args():
     ap.add_argument("--lr", type=float, default=0.2)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", choices=["mean", "last", "async"], default="mean",
+                    help="server update rule (main.cc:57-84): sync mean (default), sync last push, async")
+    ap.add_argument("--spawn", action="store_true", help="use the process launcher even at --gpus 1")
+    ap.add_argument("--launcher-check", action="store_true",
+                    help="ranks rendezvous over gloo and rank 0 prints the ranks it saw, no GPU work (CPU tests)")
+    ap.add_argument("--dump-weights", default=None,
+                    help="write each rank's weights after the timed passes to PATH.rank<r> (tests)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC-derived HBM bytes per step (written by tools/pmc_traffic.py; default "
                          "profiles/traffic.json for c2, profiles/traffic_<config>.json otherwise)")
@@ -154,20 +161,81 @@ def cpu_baseline(args, D: int) -> dict:
                       f"{el:.1f} s"}
 
 
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch(n: int) -> int:
+    """Starts n rank processes of this script (rank r -> GPU r), each with
+    the torch.distributed.run environment, and waits for them.  The parent
+    never imports torch or the engine: it only forks + execs fresh
+    interpreters, before anything has touched a GPU.  Rank 0 writes the JSON
+    line to the inherited stdout.  If a rank fails, the others are stopped."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLR_BENCH_LAUNCHER="bench.py")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                log(f"bench launcher: rank {procs.index(p)} exited with {code}; stopping the others")
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     args = parse_args()
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.spawn):
+        sys.exit(launch(args.gpus))
+    run_rank(args)
+
+
+def run_rank(args):
+    global torch, dist, dlr, np
+    import numpy as np  # noqa: F811
+    try:
+        import torch  # noqa: F811  -- loaded first: the library binds to torch's HIP runtime
+        import torch.distributed as dist  # noqa: F811
+    except Exception:  # pragma: no cover
+        torch = dist = None
+    import distlr_amd as dlr  # noqa: F811
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            sys.exit("--gpus N > 1 needs torch.distributed.run (one process per GPU)")
+        sys.exit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     distributed = world > 1
-    if torch is not None and torch.cuda.is_available():
+    if torch is not None and not args.launcher_check and torch.cuda.is_available():
         torch.cuda.set_device(local)  # torch.cuda.synchronize() below then waits on this rank's GPU only
     if distributed:
         dist.init_process_group("gloo")   # control plane only; data path is RCCL inside the library
+    if args.launcher_check:
+        seen = [None] * world
+        if distributed:
+            dist.all_gather_object(seen, {"rank": rank, "local_rank": local, "pid": os.getpid()})
+        else:
+            seen = [{"rank": rank, "local_rank": local, "pid": os.getpid()}]
+        if rank == 0:
+            print(json.dumps({"launcher_check": seen, "world": world}), flush=True)
+        if distributed:
+            dist.destroy_process_group()
+        return
     D, B = args.features, args.batch
+    mode = {"mean": dlr.MODE_SYNC_MEAN, "last": dlr.MODE_SYNC_LAST, "async": dlr.MODE_ASYNC}[args.mode]
 
     uid = None
     if distributed:
@@ -201,7 +269,7 @@ def main():
 
     def run(k0, k):
         for i in range(k0, k0 + k):
-            eng.train_step(i % nb, args.lr, 1.0, dlr.MODE_SYNC_MEAN)
+            eng.train_step(i % nb, args.lr, 1.0, mode)
 
     run(0, args.warmup)
     eng.sync()
@@ -240,6 +308,18 @@ def main():
           [("margin", dlr.TIMER_MARGIN), ("grad_update", dlr.TIMER_GRAD), ("merge", dlr.TIMER_UPDATE),
            ("exchange", dlr.TIMER_EXCHANGE), ("step", dlr.TIMER_STEP)]}
     eng.timing(False)
+    # Every rank holds the replicated weights after the same 2K (+W) steps:
+    # their checksums must agree (and, with --dump-weights, the tests compare
+    # them with the oracle's W-worker run).
+    w_fin = eng.get_weights()
+    digest = hashlib.sha1(w_fin.tobytes()).hexdigest()
+    if args.dump_weights:
+        w_fin.tofile(f"{args.dump_weights}.rank{rank}")
+    digests = [digest]
+    if distributed:
+        digests = [None] * world
+        dist.all_gather_object(digests, digest)
+    nranks, transport = eng.comm_info()
     # Pass 3 (the roofline): each kernel stage over K consecutive batches
     # between ONE event pair (no per-launch event overhead, comparable with
     # rocprofv3's kernel durations).  Runs after the measured passes: the
@@ -331,6 +411,21 @@ def main():
                        "rows_per_gpu": args.rows, "num_feature_dim": D, "nnz_per_row": args.nnz,
                        "batch_size": B, "parallelism": f"dp{world}"},
             "roofline": roofline,
+            "exchange": {
+                "transport": {dlr.TRANSPORT_NONE: "none (1 rank)", dlr.TRANSPORT_RCCL: "rccl",
+                              dlr.TRANSPORT_LOOPBACK: "loopback"}[transport],
+                "rccl_nranks": nranks if transport == dlr.TRANSPORT_RCCL else 0,
+                "launcher": os.environ.get("DLR_BENCH_LAUNCHER") or
+                            ("torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else
+                             ("external" if distributed else "single process")),
+                "us_per_step": round(avg_us["exchange"], 3),
+                "merge_us_per_step": round(avg_us["merge"], 3) if world > 1 else 0.0,
+                "protocol": ("touched-list all-gather + rank-ordered merge" if layout == "touched" else
+                             "key-range all-to-all + rank-ordered merge + in-place all-gather") if world > 1 else
+                            "none",
+                "weights_sha1": digest,
+                "ranks_agree": len(set(digests)) == 1,
+            },
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -1,0 +1,212 @@
+// dlr_comm.cpp -- RCCL and in-process loopback transports (dlr_comm.h).
+#include "dlr_comm.h"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+namespace dlr {
+
+namespace {
+
+bool hip_ok(hipError_t e, const char *what, std::string &err) {
+    if (e == hipSuccess) return true;
+    err = std::string(what) + ": " + hipGetErrorString(e);
+    return false;
+}
+
+bool nccl_ok(ncclResult_t r, const char *what, std::string &err) {
+    if (r == ncclSuccess) return true;
+    err = std::string(what) + ": " + ncclGetErrorString(r);
+    return false;
+}
+
+// ------------------------------------------------------------------ RCCL
+
+class RcclComm final : public Comm {
+public:
+    RcclComm(ncclComm_t c, int world, int rank) : comm_(c), world_(world), rank_(rank) {}
+    ~RcclComm() override { ncclCommDestroy(comm_); }
+    int world() const override { return world_; }
+    int rank() const override { return rank_; }
+    const char *kind() const override { return "rccl"; }
+    bool all_reduce_i64(int64_t *d, size_t n, bool max, hipStream_t s, std::string &err) override {
+        return nccl_ok(ncclAllReduce(d, d, n, ncclInt64, max ? ncclMax : ncclSum, comm_, s), "ncclAllReduce", err);
+    }
+    bool all_gather(const void *send, void *recv, size_t words, hipStream_t s, std::string &err) override {
+        return nccl_ok(ncclAllGather(send, recv, words, ncclUint32, comm_, s), "ncclAllGather", err);
+    }
+    bool all_to_all(const void *send, void *recv, size_t words, hipStream_t s, std::string &err) override {
+        return nccl_ok(ncclAllToAll(send, recv, words, ncclUint32, comm_, s), "ncclAllToAll", err);
+    }
+    int count() const {
+        int n = 0;
+        return ncclCommCount(comm_, &n) == ncclSuccess ? n : -1;
+    }
+
+private:
+    ncclComm_t comm_;
+    int world_, rank_;
+};
+
+}  // namespace
+
+bool rccl_unique_id(void *out, std::string &err) {
+    ncclUniqueId id;
+    if (!nccl_ok(ncclGetUniqueId(&id), "ncclGetUniqueId", err)) return false;
+    static_assert(sizeof(id) <= 128, "DLR_UNIQUE_ID_BYTES");
+    memcpy(out, &id, sizeof(id));
+    return true;
+}
+
+Comm *make_rccl_comm(int world, int rank, const void *unique_id, std::string &err) {
+    ncclUniqueId id;
+    if (world > 1) {
+        memcpy(&id, unique_id, sizeof(id));
+    } else if (!nccl_ok(ncclGetUniqueId(&id), "ncclGetUniqueId", err)) {
+        return nullptr;
+    }
+    ncclComm_t c = nullptr;
+    if (!nccl_ok(ncclCommInitRank(&c, world, id, rank), "ncclCommInitRank", err)) return nullptr;
+    auto *rc = new RcclComm(c, world, rank);
+    // the communicator's own rank count (reported by bench.py as rccl_nranks)
+    if (rc->count() != world) {
+        err = "ncclCommCount disagrees with the world size";
+        delete rc;
+        return nullptr;
+    }
+    return rc;
+}
+
+// ------------------------------------------------------------------ loopback
+
+struct LoopGroup {
+    explicit LoopGroup(int w) : W(w), send((size_t)w, nullptr), recv((size_t)w, nullptr) {}
+    const int W;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    bool broken = false;  // a rank timed out: every later barrier fails at once
+    std::vector<const void *> send;
+    std::vector<void *> recv;
+    std::atomic<int> refs{0};
+
+    // Generation barrier over the W ranks (each rank is one host thread).
+    bool barrier(std::string &err) {
+        std::unique_lock<std::mutex> lk(mu);
+        if (broken) {
+            err = "loopback group: a peer failed earlier";
+            return false;
+        }
+        const uint64_t g = gen;
+        if (++arrived == W) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+            return true;
+        }
+        if (!cv.wait_for(lk, std::chrono::seconds(300), [&] { return gen != g || broken; }) || broken) {
+            broken = true;
+            cv.notify_all();
+            err = "loopback group: peers did not reach the collective within 300 s";
+            return false;
+        }
+        return true;
+    }
+};
+
+namespace {
+
+class LoopbackComm final : public Comm {
+public:
+    LoopbackComm(LoopGroup *g, int rank) : g_(g), rank_(rank) { g_->refs.fetch_add(1); }
+    ~LoopbackComm() override {
+        if (g_->refs.fetch_sub(1) == 1) delete g_;
+    }
+    int world() const override { return g_->W; }
+    int rank() const override { return rank_; }
+    const char *kind() const override { return "loopback"; }
+
+    bool all_reduce_i64(int64_t *d, size_t n, bool max, hipStream_t s, std::string &err) override {
+        const int W = g_->W;
+        if (!publish(d, d, s, err)) return false;
+        std::vector<int64_t> all((size_t)W * n);
+        bool ok = true;
+        for (int q = 0; q < W && ok; ++q)
+            ok = hip_ok(hipMemcpyAsync(all.data() + (size_t)q * n, g_->send[(size_t)q], n * 8, hipMemcpyDeviceToHost, s),
+                        "loopback all_reduce (gather)", err);
+        ok = ok && hip_ok(hipStreamSynchronize(s), "loopback all_reduce", err);
+        if (!g_->barrier(err) || !ok) return false;  // every rank has read every buffer
+        std::vector<int64_t> r(all.begin(), all.begin() + (ptrdiff_t)n);
+        for (int q = 1; q < W; ++q)  // rank order
+            for (size_t i = 0; i < n; ++i) {
+                const int64_t v = all[(size_t)q * n + i];
+                r[i] = max ? std::max(r[i], v) : r[i] + v;
+            }
+        return hip_ok(hipMemcpyAsync(d, r.data(), n * 8, hipMemcpyHostToDevice, s), "loopback all_reduce (scatter)",
+                      err) &&
+               hip_ok(hipStreamSynchronize(s), "loopback all_reduce", err);
+    }
+
+    bool all_gather(const void *send, void *recv, size_t words, hipStream_t s, std::string &err) override {
+        const size_t bytes = words * 4;
+        if (!publish(send, recv, s, err)) return false;
+        bool ok = true;
+        for (int q = 0; q < g_->W && ok; ++q) {
+            char *dst = static_cast<char *>(recv) + (size_t)q * bytes;
+            if (dst == g_->send[(size_t)q] || bytes == 0) continue;  // in place
+            ok = hip_ok(hipMemcpyAsync(dst, g_->send[(size_t)q], bytes, hipMemcpyDeviceToDevice, s),
+                        "loopback all_gather", err);
+        }
+        return finish(ok, s, err);
+    }
+
+    bool all_to_all(const void *send, void *recv, size_t words, hipStream_t s, std::string &err) override {
+        const size_t bytes = words * 4;
+        if (!publish(send, recv, s, err)) return false;
+        bool ok = true;
+        for (int q = 0; q < g_->W && ok && bytes; ++q)
+            ok = hip_ok(hipMemcpyAsync(static_cast<char *>(recv) + (size_t)q * bytes,
+                                       static_cast<const char *>(g_->send[(size_t)q]) + (size_t)rank_ * bytes, bytes,
+                                       hipMemcpyDeviceToDevice, s),
+                        "loopback all_to_all", err);
+        return finish(ok, s, err);
+    }
+
+private:
+    // This rank's buffers are complete (stream drained) and visible to the
+    // peers once every rank has passed the barrier.
+    bool publish(const void *send, void *recv, hipStream_t s, std::string &err) {
+        if (!hip_ok(hipStreamSynchronize(s), "loopback collective", err)) return false;
+        g_->send[(size_t)rank_] = send;
+        g_->recv[(size_t)rank_] = recv;
+        return g_->barrier(err);
+    }
+    // The copies out of the peers' buffers are done before any rank reuses
+    // its send buffer.
+    bool finish(bool ok, hipStream_t s, std::string &err) {
+        ok = ok && hip_ok(hipStreamSynchronize(s), "loopback collective", err);
+        std::string berr;
+        const bool b = g_->barrier(berr);
+        if (ok && !b) err = berr;
+        return ok && b;
+    }
+
+    LoopGroup *g_;
+    int rank_;
+};
+
+}  // namespace
+
+LoopGroup *make_loop_group(int world) { return new LoopGroup(world); }
+
+Comm *make_loopback_comm(LoopGroup *g, int rank) { return new LoopbackComm(g, rank); }
+
+}  // namespace dlr

@@ -1,0 +1,58 @@
+// dlr_comm.h -- the exchange transport of one rank (internal, not ABI).
+//
+// Replaces ps-lite's KVWorker::Push/Pull + Postoffice::Barrier
+// (src/lr.cc:116-132, src/main.cc:150) for the data-parallel exchange.
+// Two transports behind one interface, both driving the SAME engine code
+// (key-range all-to-all, rank-ordered merge, in-place all-gather, touched
+// lists):
+//   * RcclComm     -- RCCL over xGMI, one process (or thread) per GPU: the
+//                     product path;
+//   * LoopbackComm -- W contexts of ONE process on ONE device linked by an
+//                     in-process group: device-to-device copies between the
+//                     contexts' buffers behind host barriers.  RCCL refuses
+//                     two ranks on one device, so this is what runs the
+//                     world > 1 engine path on a single GPU (tests, and
+//                     bin/distlr's DISTLR_TOPOLOGY=group).
+// Every call is collective: all ranks call it in the same order.  Buffers
+// are device pointers; `words` counts 4-byte words (floats / uint32) per
+// rank (all_gather) or per peer (all_to_all).  On failure the call returns
+// false and sets err.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+namespace dlr {
+
+class Comm {
+public:
+    virtual ~Comm() = default;
+    virtual int world() const = 0;
+    virtual int rank() const = 0;
+    virtual const char *kind() const = 0;
+    // In-place all-reduce of n int64 (max or sum).
+    virtual bool all_reduce_i64(int64_t *d, size_t n, bool max, hipStream_t s, std::string &err) = 0;
+    // recv[q * words ..] = rank q's send[0 .. words); send may alias
+    // recv + rank * words (in place).
+    virtual bool all_gather(const void *send, void *recv, size_t words, hipStream_t s, std::string &err) = 0;
+    // recv[q * words ..] = rank q's send[rank * words ..).
+    virtual bool all_to_all(const void *send, void *recv, size_t words, hipStream_t s, std::string &err) = 0;
+};
+
+// RCCL communicator for rank `rank` of `world` (unique_id: the 128-byte
+// ncclUniqueId from rank 0; ignored and generated locally when world == 1).
+Comm *make_rccl_comm(int world, int rank, const void *unique_id, std::string &err);
+
+// ncclGetUniqueId into out (DLR_UNIQUE_ID_BYTES).
+bool rccl_unique_id(void *out, std::string &err);
+
+// In-process group of `world` loopback ranks; make_loopback_comm(g, r) is
+// rank r's endpoint.  The group is reference-counted by its endpoints.
+struct LoopGroup;
+LoopGroup *make_loop_group(int world);
+Comm *make_loopback_comm(LoopGroup *g, int rank);
+
+}  // namespace dlr

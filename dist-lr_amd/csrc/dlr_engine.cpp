@@ -9,7 +9,6 @@
 // rank's slice of its range), rank-ordered merge + SGD on the range, then
 // an in-place all-gather of the updated weights (the "pull").
 #include <hip/hip_runtime_api.h>
-#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -21,6 +20,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "dlr_comm.h"
 #include "dlr_internal.h"
 #include "dlr_kernels.h"
 
@@ -149,7 +149,7 @@ struct dlr_ctx {
     int device = 0, rank = 0, world = 1;
     int64_t D = 0, chunk = 0, Dpad = 0;
     hipStream_t stream = nullptr;
-    ncclComm_t comm = nullptr;
+    dlr::Comm *comm = nullptr;  // exchange transport (RCCL, or an in-process loopback group); null: none
     float *w = nullptr;      // Dpad (replicated weights)
     float *g = nullptr;      // Dpad (this rank's pushed gradient), world > 1
     float *recv = nullptr;   // world x chunk, world > 1
@@ -206,10 +206,11 @@ int fail(dlr_ctx *c, int code, const std::string &msg) {
             return fail((c), DLR_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));             \
     } while (0)
 
-#define NCCLC(c, expr)                                                                                  \
+// A collective of the context's transport (dlr_comm.h); bool result.
+#define COMMC(c, expr)                                                                                  \
     do {                                                                                                \
-        ncclResult_t r_ = (expr);                                                                       \
-        if (r_ != ncclSuccess) return fail((c), DLR_E_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+        std::string e_;                                                                                 \
+        if (!(c)->comm->expr) return fail((c), DLR_E_RCCL, std::string((c)->comm->kind()) + " " + e_);  \
     } while (0)
 
 int dev_alloc(dlr_ctx *c, void **p, size_t bytes) {
@@ -315,22 +316,28 @@ void harvest(dlr_ctx *c) {
 
 // Load-time collectives (all ranks call dlr_load_train together): max of
 // an int64 over ranks, and an all-gather of one float per rank.
-int coll_max_i64(dlr_ctx *c, int64_t *v) {
-    if (!c->comm) return DLR_OK;
+// In-place max or sum of an int64 vector over the ranks (through a device
+// buffer: both transports reduce device memory).
+int coll_reduce_i64(dlr_ctx *c, int64_t *v, size_t n, bool max) {
+    if (!c->comm || n == 0) return DLR_OK;
     int64_t *d = nullptr;
-    int rc = dev_alloc(c, (void **)&d, 16);
+    int rc = dev_alloc(c, (void **)&d, n * 8);
     if (rc) return rc;
-    int64_t h = *v;
-    hipError_t e = hipMemcpyAsync(d, &h, 8, hipMemcpyHostToDevice, c->stream);
-    ncclResult_t r = e == hipSuccess ? ncclAllReduce(d, d, 1, ncclInt64, ncclMax, c->comm, c->stream) : ncclSuccess;
-    if (e == hipSuccess && r == ncclSuccess) e = hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, c->stream);
+    std::string err;
+    hipError_t e = hipMemcpyAsync(d, v, n * 8, hipMemcpyHostToDevice, c->stream);
+    const bool ok = e == hipSuccess && c->comm->all_reduce_i64(d, n, max, c->stream, err);
+    if (ok) e = hipMemcpyAsync(v, d, n * 8, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     dev_free(c, d);
-    if (r != ncclSuccess) return fail(c, DLR_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
-    if (e != hipSuccess) return fail(c, DLR_E_HIP, std::string("coll_max_i64: ") + hipGetErrorString(e));
-    *v = h;
+    if (e != hipSuccess) return fail(c, DLR_E_HIP, std::string("coll_reduce_i64: ") + hipGetErrorString(e));
+    if (!ok) return fail(c, DLR_E_RCCL, std::string(c->comm->kind()) + " " + err);
     return DLR_OK;
 }
+
+int coll_max_i64(dlr_ctx *c, int64_t *v) { return coll_reduce_i64(c, v, 1, true); }
+
+// Sum of an int64 vector over the ranks, in place.
+int coll_sum_i64(dlr_ctx *c, std::vector<int64_t> &v) { return coll_reduce_i64(c, v.data(), v.size(), false); }
 
 int coll_gather_f32(dlr_ctx *c, float v, std::vector<float> &out) {
     const int W = c->comm ? c->world : 1;
@@ -339,30 +346,34 @@ int coll_gather_f32(dlr_ctx *c, float v, std::vector<float> &out) {
     float *d = nullptr;
     int rc = dev_alloc(c, (void **)&d, (size_t)(W + 1) * 4);
     if (rc) return rc;
+    std::string err;
     hipError_t e = hipMemcpyAsync(d + W, &v, 4, hipMemcpyHostToDevice, c->stream);
-    ncclResult_t r = e == hipSuccess ? ncclAllGather(d + W, d, 1, ncclFloat32, c->comm, c->stream) : ncclSuccess;
-    if (e == hipSuccess && r == ncclSuccess) e = hipMemcpyAsync(out.data(), d, (size_t)W * 4, hipMemcpyDeviceToHost, c->stream);
+    const bool ok = e == hipSuccess && c->comm->all_gather(d + W, d, 1, c->stream, err);
+    if (ok) e = hipMemcpyAsync(out.data(), d, (size_t)W * 4, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     dev_free(c, d);
-    if (r != ncclSuccess) return fail(c, DLR_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(r));
     if (e != hipSuccess) return fail(c, DLR_E_HIP, std::string("coll_gather_f32: ") + hipGetErrorString(e));
+    if (!ok) return fail(c, DLR_E_RCCL, std::string(c->comm->kind()) + " " + err);
     return DLR_OK;
 }
 
-// Sum of an int64 vector over the ranks (RCCL), in place.
-int coll_sum_i64(dlr_ctx *c, std::vector<int64_t> &v) {
-    if (!c->comm || v.empty()) return DLR_OK;
-    int64_t *d = nullptr;
-    int rc = dev_alloc(c, (void **)&d, v.size() * 8);
+// Load-time agreement: every rank runs the same number of steps
+// with the same collectives, so a rank whose own arguments are bad, or
+// whose batch count differs from its peers', must not leave the others
+// waiting in a collective.  Each rank contributes its local error flag and
+// batch count; all ranks fail together.  Called by every rank exactly once
+// per load, before any other load-time collective.
+int coll_agree_load(dlr_ctx *c, const char *who, int local_rc, const std::string &local_msg, int64_t nb) {
+    if (!c->comm) return local_rc ? fail(c, local_rc, local_msg) : DLR_OK;
+    int64_t v[3] = {local_rc ? 1 : 0, nb, -nb};
+    int rc = coll_reduce_i64(c, v, 3, true);
     if (rc) return rc;
-    hipError_t e = hipMemcpyAsync(d, v.data(), v.size() * 8, hipMemcpyHostToDevice, c->stream);
-    ncclResult_t r =
-        e == hipSuccess ? ncclAllReduce(d, d, v.size(), ncclInt64, ncclSum, c->comm, c->stream) : ncclSuccess;
-    if (e == hipSuccess && r == ncclSuccess) e = hipMemcpyAsync(v.data(), d, v.size() * 8, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    dev_free(c, d);
-    if (r != ncclSuccess) return fail(c, DLR_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
-    if (e != hipSuccess) return fail(c, DLR_E_HIP, std::string("coll_sum_i64: ") + hipGetErrorString(e));
+    if (local_rc) return fail(c, local_rc, local_msg);
+    if (v[0]) return fail(c, DLR_E_ARG, std::string(who) + ": another rank rejected its shard");
+    if (v[1] != -v[2])
+        return fail(c, DLR_E_ARG, std::string(who) + ": ranks have different batch counts per epoch (" +
+                                      std::to_string(-v[2]) + " .. " + std::to_string(v[1]) +
+                                      "); synchronous data parallelism needs equal shards (INTEGRATION.md)");
     return DLR_OK;
 }
 
@@ -1101,16 +1112,15 @@ const char *dlr_last_error(const dlr_ctx *ctx) { return ctx ? ctx->err.c_str() :
 
 int dlr_get_unique_id(void *id_out) {
     if (!id_out) return DLR_E_ARG;
-    ncclUniqueId id;
-    ncclResult_t r = ncclGetUniqueId(&id);
-    if (r != ncclSuccess) return fail(nullptr, DLR_E_RCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
-    memcpy(id_out, &id, sizeof(id));
+    std::string err;
+    if (!dlr::rccl_unique_id(id_out, err)) return fail(nullptr, DLR_E_RCCL, err);
     return DLR_OK;
 }
 
-int dlr_create(int device, int rank, int world, const void *unique_id, int64_t D, dlr_ctx **out) {
-    if (!out || D <= 0 || world <= 0 || rank < 0 || rank >= world || (world > 1 && !unique_id))
-        return fail(nullptr, DLR_E_ARG, "dlr_create: bad argument");
+namespace {
+// One rank's context on `device`; takes ownership of `comm` (may be null).
+int create_ctx(int device, int rank, int world, int64_t D, dlr::Comm *comm, dlr_ctx **out) {
+    std::unique_ptr<dlr::Comm> own(comm);
     *out = nullptr;
     auto c = std::make_unique<dlr_ctx>();
     c->device = device;
@@ -1131,23 +1141,66 @@ int dlr_create(int device, int rank, int world, const void *unique_id, int64_t D
     if ((rc = dev_alloc(c.get(), (void **)&c->correct, 64))) return rc;
     HIPC(c.get(), hipHostMalloc((void **)&c->h_correct, 64, hipHostMallocDefault));
     HIPC(c.get(), hipHostMalloc((void **)&c->h_ll, 64, hipHostMallocDefault));
-    // Gradient + receive buffers serve both the RCCL exchange and the
+    // Gradient + receive buffers serve both the exchange and the
     // host-exchange (worker/server) entry points.
     if ((rc = dev_alloc(c.get(), (void **)&c->g, (size_t)c->Dpad * 4))) return rc;
     if ((rc = dev_alloc(c.get(), (void **)&c->recv, (size_t)c->Dpad * 4))) return rc;
     HIPC(c.get(), hipMemsetAsync(c->g, 0, (size_t)c->Dpad * 4, c->stream));
     HIPC(c.get(), hipStreamSynchronize(c->stream));
+    c->comm = own.release();
+    *out = c.release();
+    return DLR_OK;
+}
+}  // namespace
+
+int dlr_create(int device, int rank, int world, const void *unique_id, int64_t D, dlr_ctx **out) {
+    if (!out || D <= 0 || world <= 0 || rank < 0 || rank >= world || (world > 1 && !unique_id))
+        return fail(nullptr, DLR_E_ARG, "dlr_create: bad argument");
+    *out = nullptr;
+    if (hipSetDevice(device) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(nullptr, DLR_E_HIP, "dlr_create: hipSetDevice(" + std::to_string(device) + ") failed");
+    }
+    dlr::Comm *comm = nullptr;
     const char *force = getenv("DLR_FORCE_COLLECTIVES");
     if (world > 1 || (force && strcmp(force, "1") == 0)) {
-        ncclUniqueId id;
-        if (world > 1) {
-            memcpy(&id, unique_id, sizeof(id));
-        } else {
-            NCCLC(c.get(), ncclGetUniqueId(&id));
-        }
-        NCCLC(c.get(), ncclCommInitRank(&c->comm, world, id, rank));
+        std::string err;
+        comm = dlr::make_rccl_comm(world, rank, unique_id, err);
+        if (!comm) return fail(nullptr, DLR_E_RCCL, err);
     }
-    *out = c.release();
+    return create_ctx(device, rank, world, D, comm, out);
+}
+
+int dlr_create_group(int device, int world, int64_t D, dlr_ctx **out) {
+    if (!out || D <= 0 || world <= 0 || world > dlr::kMaxRanks)
+        return fail(nullptr, DLR_E_ARG, "dlr_create_group: bad argument");
+    for (int r = 0; r < world; ++r) out[r] = nullptr;
+    dlr::LoopGroup *g = dlr::make_loop_group(world);
+    std::vector<dlr::Comm *> comms((size_t)world);
+    for (int r = 0; r < world; ++r) comms[(size_t)r] = dlr::make_loopback_comm(g, r);  // endpoints own g
+    for (int r = 0; r < world; ++r) {
+        dlr::Comm *cm = comms[(size_t)r];
+        comms[(size_t)r] = nullptr;
+        const int rc = create_ctx(device, r, world, D, cm, &out[r]);
+        if (rc) {
+            for (auto *x : comms) delete x;
+            for (int q = 0; q < r; ++q) {
+                dlr_destroy(out[q]);
+                out[q] = nullptr;
+            }
+            return rc;
+        }
+    }
+    return DLR_OK;
+}
+
+int dlr_comm_info(const dlr_ctx *c, int *nranks, int *transport) {
+    if (!c) return DLR_E_ARG;
+    if (nranks) *nranks = c->comm ? c->comm->world() : 0;
+    if (transport)
+        *transport = !c->comm ? DLR_TRANSPORT_NONE
+                     : strcmp(c->comm->kind(), "rccl") == 0 ? DLR_TRANSPORT_RCCL
+                                                            : DLR_TRANSPORT_LOOPBACK;
     return DLR_OK;
 }
 
@@ -1157,7 +1210,7 @@ void dlr_destroy(dlr_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->cstream) (void)hipStreamSynchronize(ctx->cstream);
     free_train(ctx);  // unregisters a streamed shard's host rows
-    if (ctx->comm) ncclCommDestroy(ctx->comm);
+    delete ctx->comm;  // RCCL: ncclCommDestroy; loopback: drops the group reference
     for (void *p : ctx->allocs) (void)hipFree(p);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->h_correct) (void)hipHostFree(ctx->h_correct);
@@ -1201,11 +1254,22 @@ int dlr_get_weights(dlr_ctx *c, float *w, int64_t D) {
 }
 
 int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_t *n_batches) {
-    if (!c || !ds) return fail(c, DLR_E_ARG, "dlr_load_train: bad argument");
-    if (ds->D != c->D) return fail(c, DLR_E_ARG, "dlr_load_train: dataset D != context D");
-    if (batch_size == 0) return fail(c, DLR_E_ARG, "dlr_load_train: batch_size 0 (reference never terminates)");
-    if (ds->n_rows <= 0) return fail(c, DLR_E_ARG, "dlr_load_train: empty shard (reference never terminates)");
+    if (!c) return fail(c, DLR_E_ARG, "dlr_load_train: bad argument");
     HIPC(c, hipSetDevice(c->device));
+    {
+        std::string msg;
+        if (!ds)
+            msg = "dlr_load_train: bad argument";
+        else if (ds->D != c->D)
+            msg = "dlr_load_train: dataset D != context D";
+        else if (batch_size == 0)
+            msg = "dlr_load_train: batch_size 0 (reference never terminates)";
+        else if (ds->n_rows <= 0)
+            msg = "dlr_load_train: empty shard (reference never terminates)";
+        const int64_t nb = msg.empty() ? dlr_num_batches(ds->n_rows, batch_size) : 0;
+        int rc = coll_agree_load(c, "dlr_load_train", msg.empty() ? DLR_OK : DLR_E_ARG, msg, nb);
+        if (rc) return rc;
+    }
     HIPC(c, hipStreamSynchronize(c->stream));
     free_train(c);
     TrainShard &t = c->train;
@@ -1626,11 +1690,22 @@ int dlr_load_test(dlr_ctx *c, const dlr_dataset *ds) {
 }
 
 int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, int64_t *n_batches) {
-    if (!c || !ds) return fail(c, DLR_E_ARG, "dlr_load_train_dense: bad argument");
-    if (ds->D != c->D) return fail(c, DLR_E_ARG, "dlr_load_train_dense: dataset D != context D");
-    if (batch_size == 0) return fail(c, DLR_E_ARG, "dlr_load_train_dense: batch_size 0 (reference never terminates)");
-    if (ds->n_rows <= 0) return fail(c, DLR_E_ARG, "dlr_load_train_dense: empty shard (reference never terminates)");
+    if (!c) return fail(c, DLR_E_ARG, "dlr_load_train_dense: bad argument");
     HIPC(c, hipSetDevice(c->device));
+    {
+        std::string msg;
+        if (!ds)
+            msg = "dlr_load_train_dense: bad argument";
+        else if (ds->D != c->D)
+            msg = "dlr_load_train_dense: dataset D != context D";
+        else if (batch_size == 0)
+            msg = "dlr_load_train_dense: batch_size 0 (reference never terminates)";
+        else if (ds->n_rows <= 0)
+            msg = "dlr_load_train_dense: empty shard (reference never terminates)";
+        const int64_t nb = msg.empty() ? dlr_num_batches(ds->n_rows, batch_size) : 0;
+        int rc = coll_agree_load(c, "dlr_load_train_dense", msg.empty() ? DLR_OK : DLR_E_ARG, msg, nb);
+        if (rc) return rc;
+    }
     HIPC(c, hipStreamSynchronize(c->stream));
     free_train(c);
     free_touched_bufs(c);
@@ -1766,7 +1841,7 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
             HIPC(c, hipMemsetD32Async(c->xsend, (int)n, 1, c->stream));
             HIPC(c, hipMemcpyAsync(c->xsend + 1, cols, (size_t)n * 4, hipMemcpyDeviceToDevice, c->stream));
             time_begin(c, &t0);
-            NCCLC(c, ncclAllGather(c->xsend, c->xrecv, (size_t)stride, ncclUint32, c->comm, c->stream));
+            COMMC(c, all_gather(c->xsend, c->xrecv, (size_t)stride, c->stream, e_));
             time_end(c, 3, t0);
             time_begin(c, &t0);
             HIPC(c, dlr::launch_sparse_merge(c->xrecv, cap, stride, c->w, c->rs, lr, C, mode, c->xcols, c->xnewv,
@@ -1784,7 +1859,7 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
         HIPC(c, launch_gradient(c, b, bt.rows, c->g, lr, C, false));
         time_end(c, 1, t0);
         time_begin(c, &t0);
-        NCCLC(c, ncclAllToAll(c->g, c->recv, (size_t)c->chunk, ncclFloat32, c->comm, c->stream));
+        COMMC(c, all_to_all(c->g, c->recv, (size_t)c->chunk, c->stream, e_));
         time_end(c, 3, t0);
         int64_t kb, ke;
         dlr_key_range(c->D, c->world, c->rank, &kb, &ke);
@@ -1792,8 +1867,7 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
         HIPC(c, dlr::launch_merge_update(c->recv, c->world, c->chunk, ke - kb, c->w + kb, lr, mode, c->stream));
         time_end(c, 2, t0);
         time_begin(c, &t0);
-        NCCLC(c, ncclAllGather(c->w + (int64_t)c->rank * c->chunk, c->w, (size_t)c->chunk, ncclFloat32, c->comm,
-                               c->stream));
+        COMMC(c, all_gather(c->w + (int64_t)c->rank * c->chunk, c->w, (size_t)c->chunk, c->stream, e_));
         time_end(c, 3, t0);
     }
     time_end(c, 4, t_step);

@@ -25,6 +25,7 @@ UNIQUE_ID_BYTES = 128
 LAYOUT_CLASSIC, LAYOUT_LDS, LAYOUT_TOUCHED = 0, 1, 2
 RESIDENCY_AUTO, RESIDENCY_DEVICE, RESIDENCY_STREAM = 0, 1, 2
 STAGE_MARGIN, STAGE_GRADIENT, STAGE_UPDATE = 0, 1, 2
+TRANSPORT_NONE, TRANSPORT_RCCL, TRANSPORT_LOOPBACK = 0, 1, 2
 
 # Exported symbols, in include/distlr_amd.h order (tests check the .so
 # exports every one of them).
@@ -37,7 +38,7 @@ SYMBOLS = [
     "dlr_dense_free",
     "dlr_num_batches", "dlr_batch_rows",
     "dlr_init_weight", "dlr_format_model", "dlr_key_range",
-    "dlr_get_unique_id", "dlr_create", "dlr_destroy", "dlr_last_error",
+    "dlr_get_unique_id", "dlr_create", "dlr_create_group", "dlr_comm_info", "dlr_destroy", "dlr_last_error",
     "dlr_set_weights", "dlr_get_weights", "dlr_load_train", "dlr_load_test", "dlr_load_train_dense",
     "dlr_load_test_dense", "dlr_set_residency", "dlr_train_residency",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
@@ -133,6 +134,8 @@ _sig("dlr_format_model", C.c_int, P, i64, C.c_char_p, i64, C.POINTER(i64))
 _sig("dlr_key_range", C.c_int, i64, C.c_int, C.c_int, C.POINTER(i64), C.POINTER(i64))
 _sig("dlr_get_unique_id", C.c_int, P)
 _sig("dlr_create", C.c_int, C.c_int, C.c_int, C.c_int, P, i64, C.POINTER(P))
+_sig("dlr_create_group", C.c_int, C.c_int, C.c_int, i64, P)
+_sig("dlr_comm_info", C.c_int, P, C.POINTER(C.c_int), C.POINTER(C.c_int))
 _sig("dlr_destroy", None, P)
 _sig("dlr_last_error", C.c_char_p, P)
 _sig("dlr_set_weights", C.c_int, P, P, i64)
@@ -423,13 +426,32 @@ class Engine:
     """One GPU context = one rank (dlr_ctx)."""
 
     def __init__(self, num_feature_dim: int, device: int = 0, rank: int = 0, world: int = 1,
-                 unique_id: Optional[bytes] = None):
+                 unique_id: Optional[bytes] = None, _handle=None):
         self.D = num_feature_dim
-        h = P()
-        uid = C.create_string_buffer(unique_id, UNIQUE_ID_BYTES) if unique_id is not None else None
-        _check(lib.dlr_create(device, rank, world, uid, num_feature_dim, C.byref(h)))
-        self._h = h
+        self.rank, self.world = rank, world
+        if _handle is None:
+            h = P()
+            uid = C.create_string_buffer(unique_id, UNIQUE_ID_BYTES) if unique_id is not None else None
+            _check(lib.dlr_create(device, rank, world, uid, num_feature_dim, C.byref(h)))
+            _handle = h
+        self._h = _handle
         self.n_batches = 0
+
+    @classmethod
+    def create_group(cls, num_feature_dim: int, world: int, device: int = 0) -> list:
+        """`world` ranks on ONE device linked by the in-process loopback
+        transport (dlr_create_group): the world > 1 engine path without
+        RCCL.  Drive each engine from its own thread (collectives block until
+        every rank arrives)."""
+        hs = (P * world)()
+        _check(lib.dlr_create_group(device, world, num_feature_dim, hs))
+        return [cls(num_feature_dim, device, r, world, _handle=P(hs[r])) for r in range(world)]
+
+    def comm_info(self) -> Tuple[int, int]:
+        """(ranks of the communicator, TRANSPORT_*) -- dlr_comm_info."""
+        n, t = C.c_int(), C.c_int()
+        self._c(lib.dlr_comm_info(self._h, C.byref(n), C.byref(t)))
+        return n.value, t.value
 
     def _c(self, rc):
         return _check(rc, self._h)

@@ -40,6 +40,7 @@ struct ParamServer::State {
     int arrived = 0;
     uint64_t generation = 0;
     bool initialised = false;
+    std::string failure;  // set once a step failed (or a worker aborted): every Push then throws
 };
 
 ParamServer::ParamServer(int device, int num_workers, float learning_rate, bool sync_mode, int64_t D)
@@ -74,17 +75,28 @@ void ParamServer::Pull(std::vector<float> &w) {
 
 void ParamServer::Push(int rank, const std::vector<float> &grad) {
     std::unique_lock<std::mutex> lk(st_->mu);
+    if (!st_->failure.empty()) throw std::runtime_error(st_->failure);
     std::copy(grad.begin(), grad.end(), st_->grads.begin() + (size_t)rank * (size_t)st_->D);
     const uint64_t gen = st_->generation;
     if (++st_->arrived == num_workers_) {
-        check(dlr_server_apply(st_->ctx, st_->grads.data(), num_workers_, st_->D, st_->lr, st_->mode), st_->ctx,
-              "ParamServer::Push");
+        // The last arrival applies the step.  On failure every waiting
+        // worker is released with the same error instead of blocking forever
+        // (the reference's server CHECK-aborts the process, main.cc:49).
+        const int rc = dlr_server_apply(st_->ctx, st_->grads.data(), num_workers_, st_->D, st_->lr, st_->mode);
+        if (rc < 0) st_->failure = std::string("ParamServer::Push: ") + dlr_last_error(st_->ctx);
         st_->arrived = 0;
         ++st_->generation;
         st_->cv.notify_all();
     } else {
-        st_->cv.wait(lk, [&] { return st_->generation != gen; });
+        st_->cv.wait(lk, [&] { return st_->generation != gen || !st_->failure.empty(); });
     }
+    if (!st_->failure.empty()) throw std::runtime_error(st_->failure);
+}
+
+void ParamServer::Abort(const std::string &why) {
+    std::lock_guard<std::mutex> g(st_->mu);
+    if (st_->failure.empty()) st_->failure = why;
+    st_->cv.notify_all();
 }
 
 // ------------------------------------------------------------------ KVWorker
@@ -99,6 +111,18 @@ KVWorker::KVWorker(int device, int rank, int world, const void *unique_id, float
                    int64_t num_feature_dim)
     : rank_(rank), world_(world), learning_rate_(learning_rate), sync_mode_(sync_mode) {
     check(dlr_create(device, rank, world, unique_id, num_feature_dim, &ctx_), nullptr, "dlr_create");
+}
+
+KVWorker::KVWorker(dlr_ctx *ctx, int rank, int world, float learning_rate, bool sync_mode)
+    : ctx_(ctx), rank_(rank), world_(world), learning_rate_(learning_rate), sync_mode_(sync_mode) {}
+
+std::vector<KVWorker *> KVWorker::Group(int device, int world, float learning_rate, bool sync_mode,
+                                        int64_t num_feature_dim) {
+    std::vector<dlr_ctx *> ctx((size_t)world, nullptr);
+    check(dlr_create_group(device, world, num_feature_dim, ctx.data()), nullptr, "dlr_create_group");
+    std::vector<KVWorker *> out;
+    for (int r = 0; r < world; ++r) out.push_back(new KVWorker(ctx[(size_t)r], r, world, learning_rate, sync_mode));
+    return out;
 }
 
 KVWorker::~KVWorker() { dlr_destroy(ctx_); }

@@ -10,12 +10,25 @@
 //
 // Topology: one process, one thread per worker (rank).  With at least as
 // many GPUs as workers each rank owns a GPU and gradients are exchanged
-// over RCCL (all-to-all of key ranges + rank-ordered merge + all-gather);
-// with more workers than GPUs (e.g. local.sh's 2 workers on one GPU) the
-// workers share GPUs and exchange through the in-process ParamServer.
-// Optional: DISTLR_GPUS (GPUs to use), DISTLR_TOPOLOGY=ps|rccl,
+// over RCCL (all-to-all of key ranges + rank-ordered merge + all-gather).
+// With more workers than GPUs (e.g. local.sh's 2 workers on one GPU) and a
+// single GPU, the ranks share it as a loopback group (dlr_create_group:
+// the same engine step, the collectives become device-to-device copies);
+// with several GPUs but more workers than GPUs, the workers share GPUs and
+// exchange through the in-process ParamServer.
+// Optional: DISTLR_GPUS (GPUs to use), DISTLR_TOPOLOGY=rccl|group|ps,
 // DISTLR_SYNC_MERGE=last (main.cc:71 as written instead of the mean).
 // Missing variables are reported (the reference dereferences NULL).
+//
+// Roles (DMLC_ROLE, examples/local.sh:30-49; main.cc:172-181 dispatches
+// on it through ps::IsServer / ps::IsWorker): local.sh starts one
+// scheduler, S servers and W workers of this binary.  Here the scheduler
+// process runs the whole W-rank job (the ranks are threads of it, so it is
+// also where the collectives and the server update happen); a server
+// process prints its mode line (main.cc:30) and exits; a worker process
+// exits at once.  So local.sh's launch pattern produces exactly one
+// training run, one set of accuracy lines and one set of model files.
+// Without DMLC_ROLE the binary runs the job standalone.
 #include <hip/hip_runtime_api.h>
 
 #include <cstdlib>
@@ -54,17 +67,20 @@ struct Config {
 };
 
 // main.cc:124-170 for one rank.
-void run_worker(const Config &cfg, int rank, distlr::KVWorker *kv, std::vector<int> *failed) {
+void run_worker(const Config &cfg, int rank, distlr::KVWorker *kv, distlr::ParamServer *ps,
+                std::vector<int> *failed) {
     try {
         {
             std::lock_guard<std::mutex> g(g_out);
-            std::cout << 0 << "I got a rank " << rank << std::endl;
+            std::cout << 0 << "I got a rank " << rank << std::endl;  // main.cc:134 (customer id 0)
         }
         distlr::LR lr = distlr::LR(cfg.num_feature_dim);
         lr.SetKVWorker(kv);
         lr.SetRank(rank);
         {
             std::lock_guard<std::mutex> g(g_out);
+            std::cout << 0 << "I'm going to push " << rank << std::endl;  // main.cc:140
+            std::cout << 0 << "I'm here " << rank << std::endl;           // main.cc:149
             std::cout << "Worker[" << rank << "]: start working..." << std::endl;
         }
         for (int i = 0; i < cfg.num_iteration; ++i) {
@@ -81,6 +97,7 @@ void run_worker(const Config &cfg, int rank, distlr::KVWorker *kv, std::vector<i
         std::string modelfile = cfg.root + "/models/part-00" + std::to_string(rank + 1);
         lr.SaveModel(modelfile);
     } catch (const std::exception &e) {
+        if (ps) ps->Abort(std::string("worker ") + std::to_string(rank) + " failed");  // release its peers
         std::lock_guard<std::mutex> g(g_out);
         std::cerr << "distlr: worker " << rank << ": " << e.what() << std::endl;
         (*failed)[(size_t)rank] = 1;
@@ -106,7 +123,21 @@ int main(int argc, char **argv) {
         std::cerr << "distlr: bad configuration" << std::endl;
         return 2;
     }
-    std::cout << "Server mode: " << (cfg.sync_mode ? "sync" : "async") << std::endl;
+    const char *role_env = getenv("DMLC_ROLE");
+    const std::string role = role_env ? role_env : "";
+    if (!role.empty() && role != "scheduler" && role != "server" && role != "worker") {
+        std::cerr << "distlr: unknown DMLC_ROLE '" << role << "'" << std::endl;
+        return 2;
+    }
+    if (role == "worker") {
+        std::cerr << "distlr: DMLC_ROLE=worker: the worker ranks run as threads of the scheduler process"
+                  << std::endl;
+        return 0;
+    }
+    // main.cc:30, printed by each server (KVStoreDistServer's constructor)
+    if (role.empty() || role == "server")
+        std::cout << "Server mode: " << (cfg.sync_mode ? "sync" : "async") << std::endl;
+    if (role == "server") return 0;
 
     int ngpu = 0;
     if (hipGetDeviceCount(&ngpu) != hipSuccess || ngpu < 1) {
@@ -115,9 +146,17 @@ int main(int argc, char **argv) {
     }
     if (const char *g = getenv("DISTLR_GPUS")) ngpu = std::max(1, std::min(ngpu, atoi(g)));
     std::string topo = getenv("DISTLR_TOPOLOGY") ? getenv("DISTLR_TOPOLOGY") : "";
-    const bool use_rccl = topo == "rccl" || (topo != "ps" && cfg.workers <= ngpu);
-    if (use_rccl && cfg.workers > ngpu) {
+    if (topo.empty()) topo = cfg.workers <= ngpu ? "rccl" : ngpu == 1 ? "group" : "ps";
+    if (topo != "rccl" && topo != "group" && topo != "ps") {
+        std::cerr << "distlr: DISTLR_TOPOLOGY must be rccl, group or ps" << std::endl;
+        return 2;
+    }
+    if (topo == "rccl" && cfg.workers > ngpu) {
         std::cerr << "distlr: DISTLR_TOPOLOGY=rccl needs one GPU per worker" << std::endl;
+        return 2;
+    }
+    if (topo == "group" && cfg.workers > 16) {
+        std::cerr << "distlr: DISTLR_TOPOLOGY=group supports at most 16 workers" << std::endl;
         return 2;
     }
 
@@ -126,7 +165,11 @@ int main(int argc, char **argv) {
     std::unique_ptr<distlr::ParamServer> ps;
     std::vector<distlr::KVWorker *> kvs((size_t)cfg.workers, nullptr);
     try {
-        if (use_rccl) {
+        if (topo == "group") {
+            std::vector<distlr::KVWorker *> g =
+                distlr::KVWorker::Group(0, cfg.workers, cfg.learning_rate, cfg.sync_mode, cfg.num_feature_dim);
+            for (int r = 0; r < cfg.workers; ++r) kvs[(size_t)r] = g[(size_t)r];
+        } else if (topo == "rccl") {
             char uid[DLR_UNIQUE_ID_BYTES] = {0};
             if (cfg.workers > 1 && dlr_get_unique_id(uid) != DLR_OK) {
                 std::cerr << "distlr: " << dlr_last_error(nullptr) << std::endl;
@@ -159,7 +202,8 @@ int main(int argc, char **argv) {
         std::cerr << "distlr: " << e.what() << std::endl;
         return 4;
     }
-    for (int r = 0; r < cfg.workers; ++r) th.emplace_back(run_worker, std::cref(cfg), r, kvs[(size_t)r], &failed);
+    for (int r = 0; r < cfg.workers; ++r)
+        th.emplace_back(run_worker, std::cref(cfg), r, kvs[(size_t)r], ps.get(), &failed);
     for (auto &t : th) t.join();
     for (int f : failed)
         if (f) return 1;

@@ -36,7 +36,11 @@ class ParamServer {
     void Init(const std::vector<float> &w);
     void Pull(std::vector<float> &w);
     // Blocks until the step of all W pushes has been applied.
+    // Throws if the step failed; then every later Push throws too.
     void Push(int rank, const std::vector<float> &grad);
+    // Releases the workers waiting in Push with an error (a worker that
+    // cannot push any more, e.g. it threw, calls this so its peers stop).
+    void Abort(const std::string &why);
     int num_workers() const { return num_workers_; }
 
    private:
@@ -54,6 +58,12 @@ class KVWorker {
     // Parameter-server topology: this worker's own context on `device`,
     // exchanging through `ps` (not owned).
     KVWorker(int device, int rank, ParamServer *ps, float learning_rate, bool sync_mode, int64_t num_feature_dim);
+    // Loopback-group topology: the `world` ranks of one device linked
+    // in-process (dlr_create_group) -- the same world > 1 engine step as
+    // over RCCL when there are more workers than GPUs.  Drive each
+    // returned worker from its own thread.
+    static std::vector<KVWorker *> Group(int device, int world, float learning_rate, bool sync_mode,
+                                         int64_t num_feature_dim);
     ParamServer *ps() const { return ps_; }
     ~KVWorker();
     KVWorker(const KVWorker &) = delete;
@@ -73,6 +83,7 @@ class KVWorker {
     std::shared_ptr<Shard> train_keep, test_keep;
 
    private:
+    KVWorker(dlr_ctx *ctx, int rank, int world, float learning_rate, bool sync_mode);  // adopts ctx
     dlr_ctx *ctx_ = nullptr;
     ParamServer *ps_ = nullptr;
     int rank_, world_;

@@ -191,6 +191,25 @@ int dlr_get_unique_id(void *id_out);
  * (main.cc:135-138: KVWorker + LR) and the server (main.cc:116-122): with
  * replicated weights each rank also serves its key range. */
 int dlr_create(int device, int rank, int world, const void *unique_id, int64_t num_feature_dim, dlr_ctx **out);
+/* Creates `world` ranks' contexts, out[0..world), all on HIP device `device`
+ * and linked by an in-process LOOPBACK group instead of RCCL (RCCL refuses
+ * two ranks on one device): the collectives of dlr_load_train* and
+ * dlr_train_step become device-to-device copies between the contexts'
+ * buffers behind host barriers.  Everything else -- key ranges, the
+ * rank-ordered merge, the in-place all-gather, the touched-list exchange --
+ * is the same engine code as over RCCL.  Replaces ps-lite's W workers + 1
+ * server sharing one machine (examples/local.sh:34-49) when there are more
+ * workers than GPUs.  Each context must be driven by its own host thread
+ * (every collective blocks until all ranks arrive; a rank missing for 300 s
+ * fails the group).  world <= 16. */
+int dlr_create_group(int device, int world, int64_t num_feature_dim, dlr_ctx **out);
+/* The context's exchange transport: *nranks = ranks of its communicator (the
+ * RCCL communicator's own count, ncclCommCount) or 0 without one;
+ * *transport = DLR_TRANSPORT_*. */
+#define DLR_TRANSPORT_NONE 0
+#define DLR_TRANSPORT_RCCL 1
+#define DLR_TRANSPORT_LOOPBACK 2
+int dlr_comm_info(const dlr_ctx *ctx, int *nranks, int *transport);
 void dlr_destroy(dlr_ctx *ctx);
 const char *dlr_last_error(const dlr_ctx *ctx);
 

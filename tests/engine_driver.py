@@ -96,3 +96,65 @@ def run_engine(shards: Sequence[dlr.Dataset], D: int, num_iteration: int, batch_
     finally:
         for e in workers + [server]:
             e.close()
+
+
+def run_group(shards: Sequence, D: int, num_iteration: int, batch_size: int, learning_rate: float,
+              test=None, test_interval: int = 10, mode: int = dlr.MODE_SYNC_MEAN, C_: float = 1.0,
+              random_state: int = 0, dense: bool = False, device: int = 0) -> EngineRun:
+    """RunWorker (main.cc:124-170) with W = len(shards) ranks of ONE device
+    linked by the loopback transport (dlr_create_group): the product's
+    world > 1 step -- key-range all-to-all, rank-ordered merge, in-place
+    all-gather (or the touched-list exchange) -- with one host thread per
+    rank, as bin/distlr drives its ranks."""
+    import threading
+
+    W = len(shards)
+    w0 = dlr.init_weight(D, random_state)
+    if dense:
+        shards = [s if isinstance(s, dlr.DenseDataset) else dlr.DenseDataset.from_dataset(s) for s in shards]
+        if test is not None and not isinstance(test, dlr.DenseDataset):
+            test = dlr.DenseDataset.from_dataset(test)
+    engines = dlr.Engine.create_group(D, W, device)
+    pulled: List[Optional[np.ndarray]] = [None] * W
+    finals: List[Optional[np.ndarray]] = [None] * W
+    tests: List[Tuple[int, int, int, float]] = []
+    errors: List[Optional[BaseException]] = [None] * W
+
+    def rank_main(r: int):
+        eng = engines[r]
+        try:
+            eng.set_weights(w0)                      # every rank holds InitWeight_'s result (main.cc:141-148)
+            nb = eng.load_train_dense(shards[r], batch_size) if dense else eng.load_train(shards[r], batch_size)
+            if r == 0 and test is not None:
+                eng.load_test_dense(test) if dense else eng.load_test(test)
+            p = w0.copy()
+            for it in range(num_iteration):
+                for b in range(nb):
+                    if it == num_iteration - 1 and b == nb - 1:
+                        p = eng.get_weights()        # the last PullWeight_ of Train (lr.cc:32)
+                    eng.train_step(b, learning_rate, C_, mode)
+                if r == 0 and test is not None and (it + 1) % test_interval == 0:
+                    c, n, ll = eng.predict()
+                    tests.append((it + 1, c, n, ll))
+                    if it == num_iteration - 1:
+                        p = eng.get_weights()
+            pulled[r] = p
+            finals[r] = eng.get_weights()
+        except BaseException as e:  # noqa: BLE001 -- re-raised in the caller
+            errors[r] = e
+
+    try:
+        th = [threading.Thread(target=rank_main, args=(r,)) for r in range(W)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    finally:
+        for e in engines:
+            e.close()
+    for e in errors:
+        if e is not None:
+            raise e
+    for r in range(1, W):  # replicated weights: every rank ends with the same bits
+        assert np.array_equal(finals[r].view(np.uint32), finals[0].view(np.uint32)), f"rank {r} weights differ"
+    return EngineRun(w=finals[0], pulled=pulled, tests=tests)

@@ -39,11 +39,15 @@ def run_distlr(tmp_path, dataset, meta, workers, extra_env=None):
     return out, lines, models
 
 
-@pytest.mark.parametrize("name,workers", [("c1_W1_Bfull_mean", 1), ("c1_W1_B7_mean", 1),
-                                          ("c1_W2_Bfull_mean", 2), ("real_W2_B50_mean", 2)])
-def test_distlr_matches_oracle(tmp_path, name, workers):
+@pytest.mark.parametrize("name,workers,topo", [("c1_W1_Bfull_mean", 1, None), ("c1_W1_B7_mean", 1, None),
+                                               ("c1_W2_Bfull_mean", 2, "group"), ("real_W2_B50_mean", 2, "group"),
+                                               ("c1_W2_Bfull_mean", 2, "ps"), ("real_W2_B50_mean", 2, "ps")])
+def test_distlr_matches_oracle(tmp_path, name, workers, topo):
+    # W = 2 on one GPU: the loopback group (default there) and the
+    # parameter-server topology
     meta = read_golden_json("trajectories.json")[name]
-    out, lines, models = run_distlr(tmp_path, meta["dataset"], meta, workers)
+    out, lines, models = run_distlr(tmp_path, meta["dataset"], meta, workers,
+                                    {"DISTLR_TOPOLOGY": topo} if topo else None)
     assert "Server mode: sync" in out
     lr_env = repr(meta["learning_rate"])
     if np.float32(oracle.to_float(lr_env)) == np.float32(meta["learning_rate"]):
@@ -82,3 +86,47 @@ def test_distlr_forced_rccl_single_worker(tmp_path):
 def test_distlr_missing_env_is_reported(tmp_path):
     r = subprocess.run([BIN], env={"PATH": os.environ.get("PATH", "")}, capture_output=True, timeout=60)
     assert r.returncode == 2 and b"DATA_DIR" in r.stderr
+
+
+LOCAL_SH_PATTERN = """#!/bin/bash
+# local.sh's launch pattern (examples/local.sh:11-51): env, then one
+# scheduler, $1 servers and $2 workers of the same binary in the background
+export DATA_DIR="$3" NUM_FEATURE_DIM=123 LEARNING_RATE=0.2 TEST_INTERVAL=10 SYNC_MODE=1
+export NUM_ITERATION=100 BATCH_SIZE=-1 RANDOM_SEED=10
+export DMLC_NUM_SERVER=$1 DMLC_NUM_WORKER=$2 DMLC_PS_ROOT_URI=127.0.0.1 DMLC_PS_ROOT_PORT=8001
+bin="$4"
+export DMLC_ROLE=scheduler; $bin &
+export DMLC_ROLE=server; for ((i=0; i<DMLC_NUM_SERVER; ++i)); do $bin & done
+export DMLC_ROLE=worker; for ((i=0; i<DMLC_NUM_WORKER; ++i)); do $bin & done
+wait
+"""
+
+
+def test_local_sh_roles(tmp_path):
+    # local.sh 1 2 bin/distlr: exactly one training run (in the scheduler
+    # process), one set of accuracy lines, one server mode line, and the
+    # model files of the 2-worker mean run
+    meta = read_golden_json("trajectories.json")["c1_W2_Bfull_mean"]
+    assert (meta["num_iteration"], meta["batch_size"], meta["test_interval"], meta["learning_rate"]) == (100, -1, 10, 0.2)
+    data = tmp_path / "data"
+    shutil.copytree(os.path.join(GOLDEN, meta["dataset"]), data)
+    script = tmp_path / "local_pattern.sh"
+    script.write_text(LOCAL_SH_PATTERN)
+    r = subprocess.run(["bash", str(script), "1", "2", str(data), BIN], capture_output=True, timeout=300)
+    assert r.returncode == 0, r.stderr.decode()
+    out = r.stdout.decode()
+    lines = [l[l.index("Iteration "):] for l in out.splitlines() if " Iteration " in l]
+    assert lines == meta["accuracy_lines"]
+    assert out.count("Server mode: sync") == 1
+    assert out.count("Worker[0]: start working...") == 1 and out.count("Worker[1]: start working...") == 1
+    pulled = [np.frombuffer(bytes.fromhex(h), dtype="<f4") for h in meta["pulled"]]
+    for rk in range(2):
+        assert (data / "models" / f"part-00{rk + 1}").read_text() == dlr.format_model(pulled[rk])
+
+
+def test_unknown_role_is_reported(tmp_path):
+    env = {"PATH": os.environ.get("PATH", ""), "DATA_DIR": str(tmp_path), "NUM_FEATURE_DIM": "10",
+           "NUM_ITERATION": "1", "BATCH_SIZE": "-1", "TEST_INTERVAL": "1", "SYNC_MODE": "1", "LEARNING_RATE": "0.1",
+           "DMLC_ROLE": "bogus"}
+    r = subprocess.run([BIN], env=env, capture_output=True, timeout=60)
+    assert r.returncode == 2 and b"DMLC_ROLE" in r.stderr
