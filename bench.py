@@ -130,35 +130,75 @@ def alg_bytes_per_step(B: int, nnz: float, D: int, dense: bool = False, unit: bo
 
 
 def cpu_baseline(args, D: int) -> dict:
-    """The oracle's sparse port (oracle/lr_oracle.c, bitwise equal to the
-    reference arithmetic) on host cores, same batch shape; a bounded sample."""
+    """the reference's CPU path with its own cost structure
+    (oracle/ref_loop.cc: local.sh's worker threads + in-process server,
+    per-epoch re-parse into dense samples, lr.cc:35-39's O(B*D^2) loop with
+    by-value copies; its weights are bitwise the oracle's).  Calibrated in
+    the build container against the verbatim reference (BASELINE.md 2:
+    52.9k samples/s at W = 1; this restatement 52.3k).
+    c1: local.sh's job itself (W = 2 threads, B = -1, test every 10 epochs)
+    for a bounded number of epochs.  Other configs cannot run it (a dense
+    sample is D floats, a step O(B*D^2)): the lr.cc:35-39 loop body is
+    timed at the config's D and the per-sample cost (D of them) reported."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle  # checker only: timed as the CPU baseline, never as the product
+    import cpu_baselines as cb  # baseline only, never the product
+    if args.config == "c1":
+        import tempfile
+        with tempfile.TemporaryDirectory() as d:
+            for sub in ("train", "test", "models"):
+                os.makedirs(os.path.join(d, sub))
+            for p in range(2):
+                make_shard(args, args.rows, p + 1).write_libsvm(os.path.join(d, "train", f"part-00{p + 1}"))
+            make_shard(args, 16281, 100).write_libsvm(os.path.join(d, "test", "part-001"))
+            epochs = 60
+            _, steps, sec, _, _ = cb.reference_local_run(d, 2, D, epochs, -1, 10, args.lr, 0)
+        return {"value": round(steps / sec, 1), "unit": "samples/s", "cores": 2, "host_cpus": os.cpu_count(),
+                "kind": "port",
+                "sample": f"local.sh topology (2 worker threads + in-process server, examples/local.sh:12-19): "
+                          f"{epochs} epochs of 2 x {args.rows} rows, B = -1, per-epoch re-parse, test every 10 "
+                          f"epochs on 16,281 rows; {steps} sample-steps in {sec:.1f} s (oracle/ref_loop.cc: "
+                          f"lr.cc/main.cc loop structure, weights bitwise the oracle's)"}
+    iters = 8
+    while True:
+        t = cb.reference_inner_cost(D, 4, iters)
+        if t * iters >= 2.0 or iters >= 1 << 30:
+            break
+        iters *= 4
+    per_sample = t * D  # lr.cc:35-39 runs the body D times per sample (one per column j)
+    return {"value": float(f"{1.0 / per_sample:.4g}"), "unit": "samples/s", "cores": 1, "host_cpus": os.cpu_count(),
+            "kind": "port",
+            "sample": f"extrapolated: {iters} iterations of lr.cc:35-39's loop body at D = {D} (two by-value "
+                      f"copies of a {D}-float sample + the O(D) margin) took {t * 1e6:.3g} us each; a "
+                      f"sample-step is D = {D} of them ({per_sample:.3g} s); one worker thread "
+                      f"(oracle/ref_loop.cc; the reference cannot hold this config: dense samples)"}
 
-    B = args.batch if args.batch > 0 else min(args.rows, 200_000)  # full-shard configs: B = -1 over <=200k rows
+
+def cpu_baseline_build(args, D: int) -> dict:
+    """BASELINE.md 3.2 -- "build CPU path, not reference": an efficient
+    OpenMP trainer (oracle/lr_cpu_omp.c) on the host's CPU share
+    (OMP_NUM_THREADS), over a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpu_baselines as cb  # baseline only, never the product
+    B = args.batch if args.batch > 0 else min(args.rows, 200_000)  # full-shard configs: B = -1 over <= 200k rows
     n_rows = 4 * B if args.batch > 0 else B
     ds = make_shard(args, n_rows, 1)
+    w = dlr.init_weight(D)
+    done, el = 0, 0.0
     if args.kind == "dense":
         X, lab = ds.arrays()
-        grad = lambda rr, ww: oracle.grad_dense(X, lab, rr, ww)       # noqa: E731
+        step = lambda k: cb.omp_train_dense(X, lab, B, w, args.lr, 1.0, k, 1)  # noqa: E731
     else:
         rp, col, val, lab = ds.csr()
-        grad = lambda rr, ww: oracle.grad_csr((rp, col, val), lab, rr, ww)  # noqa: E731
-    w = dlr.init_weight(D)
-    bb = args.batch if args.batch > 0 else -1
-    rows = [oracle.batch_rows(n_rows, bb, b % oracle.num_batches(n_rows, bb)) for b in range(4)]
-    done, t0 = 0, time.perf_counter()
-    while True:
-        g = grad(rows[done % 4], w)
-        oracle.server_update(w, [g], args.lr)
+        unit = bool(np.all(val == 1.0))
+        step = lambda k: cb.omp_train_csr(rp, col, None if unit else val, lab, D, B, w, args.lr, 1.0, k, 1)  # noqa: E731
+    step(0)  # first touch of the working set
+    while el < args.cpu_seconds and done < 100_000:
+        el += step(done)
         done += 1
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds or done >= 200_000:
-            break
-    return {"value": round(done * B / el, 1), "unit": "samples/s", "cores": 1, "host_cpus": os.cpu_count(), "kind": "port",
-            "sample": f"{done} steps of B={B}, D={D}, {args.nnz} nnz/row (oracle "
-                      f"{'dense' if args.kind == 'dense' else 'sparse'} port, 1 thread) in "
-                      f"{el:.1f} s"}
+    return {"value": round(done * B / el, 1), "unit": "samples/s", "cores": cb.omp_threads(),
+            "host_cpus": os.cpu_count(), "kind": "build CPU path, not reference",
+            "sample": f"{done} steps of B = {B} over {n_rows} rows (D = {D}, {args.nnz} nnz/row) in {el:.1f} s, "
+                      f"OpenMP {cb.omp_threads()} threads (oracle/lr_cpu_omp.c)"}
 
 
 def free_port() -> int:
@@ -380,12 +420,16 @@ def run_rank(args):
         roofline["timing"] = "value and achieved: K un-instrumented steps (copy-bound); step_breakdown_us: " \
                              "the event pass (the margin interval includes the wait for the batch copy)"
 
-    cpu = None
+    cpu = cpu_build = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             cpu = cpu_baseline(args, D)
         except Exception as e:  # the baseline is a report, never the product
             log(f"cpu baseline failed: {e}")
+        try:
+            cpu_build = cpu_baseline_build(args, D)
+        except Exception as e:
+            log(f"cpu build baseline failed: {e}")
     eng.close()
 
     if rank == 0:
@@ -427,6 +471,7 @@ def run_rank(args):
                 "ranks_agree": len(set(digests)) == 1,
             },
             "cpu_baseline": cpu,
+            "cpu_baseline_build": cpu_build,
         }
         print(json.dumps(line), flush=True)
     if distributed:

@@ -1480,8 +1480,6 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         t.row16 = t.B <= 65536;
         const int64_t total = t.coff[(size_t)nb];
         if (total >= (int64_t)1 << 31) return fail(c, DLR_E_ARG, "dlr_load_train: a batch has >= 2^31 entries");
-        const char *lm = getenv("DLR_LONG_COLUMN");
-        const int64_t long_min = lm ? atoll(lm) : 4096;
         std::vector<uint32_t> cptr((size_t)nb * (size_t)(D + 1));
         std::vector<float> cval(t.unit ? 0 : (size_t)total);
         // Row bands for the short columns of large batches (DLR_BAND_ROWS:
@@ -1493,6 +1491,14 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         int shift = 0;
         while (band_rows > 0 && ((int64_t)2 << shift) <= band_rows) ++shift;
         const bool band = band_rows > 0 && shift > 0 && (brs ? t.B > ((int64_t)1 << shift) : t.B >= ((int64_t)2 << shift));
+        // Long columns (DLR_LONG_COLUMN entries in a batch; 0 = none) are
+        // summed in a fixed chunked order instead of the reference's single
+        // sequential chain.  Default: 4,096 in band mode only
+        // (C3's 2^21+-row batches, ~10^6-entry chains); otherwise 2^17, far
+        // above anything a local.sh-sized shard holds (8,140 rows), so a
+        // skewed a9a-like shard (columns in > 50% of the rows) stays bitwise.
+        const char *lm = getenv("DLR_LONG_COLUMN");
+        const int64_t long_min = lm ? atoll(lm) : band ? 4096 : ((int64_t)1 << 17);
         int64_t lbytes = 0;
         auto finish_long = [&](auto &lb) -> int {
             // concatenate the batches' long columns

@@ -1,0 +1,85 @@
+"""BASELINE C3 at its real per-GPU size: a 12.5M-row
+Criteo-shaped shard (2^24 hashed features, 39 Zipf fields, unit values),
+B = -1 (the full shard per step, as local.sh), the DEFAULT engine choices:
+frequency relabeling, 2^20-row bands, long columns (> 4,096 entries) in
+16,384-row phases combined by a fixed tree, hot weights in LDS for the
+margin.  Two steps against the oracle (lr.cc:35-40 + main.cc:70-72).
+
+Bars (north_star: weights within 1e-5 relative): weights within
+1e-5*|b| + 1e-7 after each step; the pushed gradient of the short columns
+(<= 4,096 entries: one sequential sum each, carried across bands) bitwise,
+of the long columns (~10^5-10^6-entry chains) within 1e-5 relative; a rerun
+bitwise identical.
+
+Two initial weight vectors: the reference's own InitWeight_ (lr.cc:92-98,
+w in [0,1]: with 39 such weights per row every margin is ~20, sigma rounds
+to exactly 1.0f and the residuals are exactly 1 - y, so the sums are of
+small integers and come out exact -- bitwise whatever the order), and a
+centred init (w - 0.5) / 5 whose margins spread around 0, so the
+residuals are general fp32 values and the long-column sums really round
+differently from the reference's single chain."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import distlr_amd as dlr
+import oracle
+from test_gpu_parity import assert_same_weights
+
+pytestmark = pytest.mark.gpu
+
+D, ROWS, LR = 1 << 24, 12_500_000, 0.2
+
+
+@pytest.fixture(scope="module")
+def c3_shard():
+    ds = dlr.Dataset.generate_hashed(ROWS, D, 39, seed=10, stream=1)
+    rp, col, val, lab = ds.csr()
+    return ds, (rp, col, val), lab
+
+
+@pytest.mark.parametrize("init", ["reference", "centred"])
+def test_c3_full_size_two_steps(c3_shard, init):
+    ds, csr, lab = c3_shard
+    rows = oracle.batch_rows(ROWS, -1, 0)
+    w0 = dlr.init_weight(D)
+    if init == "centred":
+        w0 = ((w0 - np.float32(0.5)) / np.float32(5.0)).astype(np.float32)
+    counts = np.bincount(csr[1], minlength=D)
+    long_cols = counts > 4096
+    assert long_cols.sum() > 100 and counts.max() > 500_000      # the ~10^6-entry chains are there
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(w0)
+        assert eng.load_train(ds, -1) == 1
+        assert eng.train_band_rows() == 1 << 20 and eng.train_relabeled() and eng.train_unit_values()
+        # the pushed gradient of step 0 (the N > 1 path's finalize)
+        g_eng = eng.worker_gradient(0, 1.0)
+        g_orc = oracle.grad_csr(csr, lab, rows, w0)
+        assert_same_weights(g_eng[~long_cols], g_orc[~long_cols], "short-column gradient")
+        a, b = g_eng[long_cols].astype(np.float64), g_orc[long_cols].astype(np.float64)
+        rel = np.abs(a - b) / np.abs(b)
+        assert np.all(np.abs(a - b) <= 1e-5 * np.abs(b) + 1e-9), f"long-column gradient max rel {rel.max():.3g}"
+        # two fused steps (single rank: margin, banded gradient + update)
+        eng.set_weights(w0)
+        w = w0.copy()
+        traj = []
+        for step in range(2):
+            eng.train_step(0, LR, 1.0)
+            g = g_orc if step == 0 else oracle.grad_csr(csr, lab, rows, w)
+            oracle.server_update(w, [g], LR)
+            got = eng.get_weights()
+            traj.append(got)
+            x, y = got.astype(np.float64), w.astype(np.float64)
+            assert np.all(np.abs(x - y) <= 1e-5 * np.abs(y) + 1e-7), f"step {step}"
+            print(f"\nC3 full size ({init} init) step {step}: max rel weight diff vs oracle "
+                  f"{np.max(np.abs(x - y) / np.maximum(np.abs(y), 1e-30)):.3g}; long-column gradient max rel "
+                  f"{rel.max():.3g}")
+        # deterministic: the same two steps again
+        eng.set_weights(w0)
+        for step in range(2):
+            eng.train_step(0, LR, 1.0)
+            assert_same_weights(eng.get_weights(), traj[step], f"rerun step {step}")
+    finally:
+        eng.close()

@@ -192,3 +192,36 @@ def test_residency_reporting():
             eng.set_residency(7)
     finally:
         eng.close()
+
+
+def test_c4_blocked_gradient_full_epoch():
+    # the C4 blocked gradient over a FULL epoch at B = 65,536
+    # (1M rows = 16 batches, the last one wrapping to row 0), against the
+    # oracle's sequential sums step by step.  Bar: |a-b| <= 1e-5*|b| + 1e-6
+    # (the 1e-6 absolute floor: see test_c4_shape_dense_steps -- the
+    # reference's own fp32 gradient moves a weight ~3e-7 per step away from
+    # exact arithmetic).  Prints the max relative difference of the epoch.
+    D, B, lr = 4096, 65536, 0.05
+    dd = dlr.DenseDataset.generate(1_000_000, D, seed=10, stream=2)
+    X, y = dd.arrays()
+    w0 = dlr.init_weight(D)
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(w0)
+        nb = eng.load_train_dense(dd, B)
+        assert nb == 16
+        w = w0.copy()
+        worst = worst_abs = 0.0
+        for b in range(nb):
+            eng.train_step(b, lr, 1.0)
+            g = oracle.grad_dense(X, y, oracle.batch_rows(len(y), B, b), w)
+            oracle.server_update(w, [g], lr)
+            a, bb = eng.get_weights().astype(np.float64), w.astype(np.float64)
+            big = np.abs(bb) >= 1e-2
+            worst = max(worst, float(np.max(np.abs(a - bb)[big] / np.abs(bb)[big])))
+            worst_abs = max(worst_abs, float(np.max(np.abs(a - bb))))
+            assert np.all(np.abs(a - bb) <= 1e-5 * np.abs(bb) + 1e-6), f"step {b}"
+        print(f"\nC4 blocked gradient, 1 epoch (16 x 65,536 rows, D 4,096): vs oracle max rel weight diff "
+              f"{worst:.3g} (weights >= 1e-2), max abs diff {worst_abs:.3g}")
+    finally:
+        eng.close()

@@ -106,22 +106,24 @@ def test_local_sh_roles(tmp_path):
     # local.sh 1 2 bin/distlr: exactly one training run (in the scheduler
     # process), one set of accuracy lines, one server mode line, and the
     # model files of the 2-worker mean run
-    meta = read_golden_json("trajectories.json")["c1_W2_Bfull_mean"]
-    assert (meta["num_iteration"], meta["batch_size"], meta["test_interval"], meta["learning_rate"]) == (100, -1, 10, 0.2)
     data = tmp_path / "data"
-    shutil.copytree(os.path.join(GOLDEN, meta["dataset"]), data)
+    shutil.copytree(os.path.join(GOLDEN, "c1_tiny"), data)
+    # local.sh's own settings (100 epochs, B = -1, test every 10, lr 0.2)
+    D = 123
+    shards = [oracle.load_dense(str(data / "train" / f"part-00{p + 1}"), D) for p in range(2)]
+    test = oracle.load_dense(str(data / "test" / "part-001"), D)
+    orc = oracle.run_worker(shards, D, 100, -1, oracle.to_float("0.2"), test=test, test_interval=10)
     script = tmp_path / "local_pattern.sh"
     script.write_text(LOCAL_SH_PATTERN)
     r = subprocess.run(["bash", str(script), "1", "2", str(data), BIN], capture_output=True, timeout=300)
     assert r.returncode == 0, r.stderr.decode()
     out = r.stdout.decode()
     lines = [l[l.index("Iteration "):] for l in out.splitlines() if " Iteration " in l]
-    assert lines == meta["accuracy_lines"]
+    assert lines == orc.accuracy_lines() and len(lines) == 10
     assert out.count("Server mode: sync") == 1
     assert out.count("Worker[0]: start working...") == 1 and out.count("Worker[1]: start working...") == 1
-    pulled = [np.frombuffer(bytes.fromhex(h), dtype="<f4") for h in meta["pulled"]]
     for rk in range(2):
-        assert (data / "models" / f"part-00{rk + 1}").read_text() == dlr.format_model(pulled[rk])
+        assert (data / "models" / f"part-00{rk + 1}").read_text() == dlr.format_model(orc.pulled[rk])
 
 
 def test_unknown_role_is_reported(tmp_path):

@@ -178,10 +178,12 @@ def test_c3_hot_columns_bitwise_without_chunking(monkeypatch):
 
 
 @pytest.mark.parametrize("W", [1, 2])
-def test_c3_long_column_chunking_within_tolerance(W):
-    # default: columns with > 4,096 entries are summed in 512-entry chunks
+def test_c3_long_column_chunking_within_tolerance(W, monkeypatch):
+    # columns with > 4,096 entries summed in chunks (the band-mode default
+    # threshold, forced here without bands)
     # (deterministic); weights stay within the north-star bar of the
     # reference's single sequential sum: |a-b| <= 1e-5*|b| + 1e-7
+    monkeypatch.setenv("DLR_LONG_COLUMN", "4096")
     D = 1 << 24
     shards = _c3_shards(W)
     eng = run_engine(shards, D, 3, -1, 0.2)
@@ -196,6 +198,7 @@ def test_c3_long_column_chunking_within_tolerance(W):
 
 def test_c3_long_columns_forced_collectives(monkeypatch):
     # long columns through the key-range all-to-all exchange (1-rank comm)
+    monkeypatch.setenv("DLR_LONG_COLUMN", "4096")
     monkeypatch.setenv("DLR_FORCE_COLLECTIVES", "1")
     D = 1 << 24
     shards = _c3_shards(1)
@@ -206,9 +209,10 @@ def test_c3_long_columns_forced_collectives(monkeypatch):
     assert_same_weights(got.w, ref.w)
 
 
-def test_c3_long_column_gradient_tolerance():
+def test_c3_long_column_gradient_tolerance(monkeypatch):
     # the pushed gradient itself (lr.cc:40's g): hot columns summed in
     # chunks differ from the single sequential sum by rounding only
+    monkeypatch.setenv("DLR_LONG_COLUMN", "4096")
     D = 1 << 24
     ds = _c3_shards(1, rows=120_000)[0]
     rp, col, val, lab = ds.csr()

@@ -239,8 +239,8 @@ def test_sparse_layouts_two_ranks_valued(monkeypatch, layout, B):
     # a sparse valued shard that fits the LDS layout (the golden C1 shards
     # are too dense for it), per layout, wrapping batches included
     monkeypatch.setenv("DLR_GRAD_KERNEL", layout)
-    D = 3000
+    D = 30000  # sparse enough for the LDS layout's <= 255 entries per 64-column block and phase
     shards = [dlr.Dataset.generate(1000, D, 20, value_mode=1, seed=3, stream=r + 1) for r in range(2)]
     got = run_group(shards, D, 2, B, 0.1, mode=dlr.MODE_SYNC_MEAN)
-    orc = oracle.run_worker([oracle_shard(s, D) for s in shards], D, 2, B, 0.1)
+    orc = oracle.run_worker([_csr(s) for s in shards], D, 2, B, 0.1)
     compare_runs(got, orc)

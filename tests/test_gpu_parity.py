@@ -222,3 +222,36 @@ def test_errors_are_loud():
             eng.load_train(ds, 4)                       # D mismatch
     finally:
         eng.close()
+
+
+def _skewed_a9a_shard(seed, n=8140, D=123, k=14):
+    """a9a-like skew: a few columns (sex, race, native-country, capital-gain
+    bins...) appear in most rows -- >4,096 entries each in an 8,140-row
+    full-shard batch -- the rest fill each row up to k columns."""
+    rng = np.random.default_rng(seed)
+    hot = np.array([2, 9, 37, 60, 71, 95, 110, 119])
+    p_hot = np.array([0.92, 0.85, 0.67, 0.6, 0.55, 0.51, 0.8, 0.7])
+    rows = []
+    for _ in range(n):
+        cols = set(hot[rng.random(len(hot)) < p_hot].tolist())
+        while len(cols) < k:
+            cols.add(int(rng.integers(0, D)))
+        rows.append(sorted(cols))
+    rp = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int64)
+    col = np.concatenate(rows).astype(np.int32)
+    val = np.ones(len(col), np.float32)
+    lab = (rng.random(n) < 0.24).astype(np.int32)
+    return dlr.Dataset.from_csr(rp, col, val, lab, D)
+
+
+@pytest.mark.parametrize("W", [1, 2])
+def test_skewed_a9a_full_shard_bitwise(W):
+    # ADVICE r1: local.sh's shape (B = -1 over 8,140 rows) with columns in
+    # more than half of the rows must stay bitwise (no chunked long-column
+    # sums outside band mode)
+    D = 123
+    shards = [_skewed_a9a_shard(40 + r) for r in range(W)]
+    assert int(np.bincount(shards[0].csr()[1], minlength=D).max()) > 4096
+    eng = run_engine(shards, D, 100, -1, 0.2)
+    orc = oracle.run_worker([oracle_shard(s, D) for s in shards], D, 100, -1, 0.2)
+    compare_runs(eng, orc)
