@@ -1581,12 +1581,13 @@ hipError_t launch_margin_hot(const DevBatch &bt, const float *w, int64_t D, floa
         const char *e = getenv("DLR_MARGIN_HOT_SHAPE");
         return e ? atoi(e) : 0;
     }();
-    // Unit-valued shards: the compacted-cold-gather variant
-    // (DLR_MARGIN_COMPACT=0 turns it off; DLR_MARGIN_NT=<id>: columns >= id
-    // gathered non-temporally, default none).
+    // DLR_MARGIN_COMPACT=1 (A/B only): the compacted-cold-gather variant for
+    // unit-valued shards (C3: margin 1.90 ms against 1.76 ms for the plain
+    // hot margin, profiles/r02_c3_margin_ab.txt); DLR_MARGIN_NT=<id> there:
+    // columns >= id gathered non-temporally (2^19 / 2^20 / 2^21: no change).
     static const bool compact = [] {
         const char *e = getenv("DLR_MARGIN_COMPACT");
-        return !e || atoi(e) != 0;
+        return e && atoi(e) != 0;
     }();
     static const unsigned nt_from = [] {
         const char *e = getenv("DLR_MARGIN_NT");
