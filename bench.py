@@ -69,6 +69,11 @@ CONFIGS = {
     # (the rate is per batch and does not depend on the shard's length)
     "c4s": dict(rows=2_500_000, features=4096, nnz=4096, batch=65536, value_mode=1, steps=40, warmup=4,
                 label="C4 dense LR, streamed from host", kind="dense", residency="stream"),
+    # C2 with the sparse shard kept in page-locked host memory and every
+    # batch's CSR + column-major slices staged over PCIe (K1 streaming: what
+    # a shard larger than HBM runs as; forced here on a shard that fits)
+    "c2s": dict(rows=10_000_000, features=1_000_000, nnz=50, batch=65536, value_mode=1, steps=200, warmup=10,
+                label="C2 sparse LR, streamed from host", residency="stream"),
 }
 PCIE_PEAK_GBS = 63.0  # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s (spec)
 
@@ -295,10 +300,10 @@ def run_rank(args):
     if args.residency != "auto":
         eng.set_residency({"device": dlr.RESIDENCY_DEVICE, "stream": dlr.RESIDENCY_STREAM}[args.residency])
     nb = eng.load_train_dense(ds, B) if args.kind == "dense" else eng.load_train(ds, B)
-    streamed = args.kind == "dense" and eng.train_residency() == dlr.RESIDENCY_STREAM
+    streamed = eng.train_residency() == dlr.RESIDENCY_STREAM
     train_bytes, _ = eng.memory_info()
-    if not streamed:
-        ds.free()   # a streamed shard reads these host rows every step
+    if not (streamed and args.kind == "dense"):
+        ds.free()   # a streamed DENSE shard reads these host rows in place every step
     t_load = time.perf_counter() - t_setup - t_gen
     layout = "dense" if args.kind == "dense" else \
         {dlr.LAYOUT_CLASSIC: "classic", dlr.LAYOUT_LDS: "lds", dlr.LAYOUT_TOUCHED: "touched"}[eng.train_layout()]
@@ -410,8 +415,10 @@ def run_rank(args):
         "instrumented_ms_per_step": round(el_instr / args.steps * 1000.0, 5),
     }
     if streamed:
-        # bound by the host->device batch copies (B rows x D fp32 + labels per step)
-        h2d = B_eff * (4 * D + 4)
+        # bound by the host->device batch copies: dense, B rows x D fp32 +
+        # labels per step; sparse, the batch's CSR + column-major slices (at
+        # most one of the two device slots, train_bytes / 2)
+        h2d = B_eff * (4 * D + 4) if args.kind == "dense" else train_bytes // 2
         pcie = h2d / (el / args.steps) / 1e9
         roofline.update({"bound": "pcie", "kernel": "per-batch host->device staging (copy stream) overlapped "
                                                       "with the margin/gradient kernels of the previous batch",

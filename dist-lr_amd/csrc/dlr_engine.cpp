@@ -14,6 +14,7 @@
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <string>
 #include <thread>
@@ -32,6 +33,24 @@ constexpr int64_t kPad = 64;  // padding entries after col/val (16-B tail loads)
 struct DeviceBuf {
     void *p = nullptr;
     size_t bytes = 0;
+};
+
+// One array of a STREAMED sparse shard (DLR_RESIDENCY_STREAM: the shard and
+// its column-major copies stay in page-locked host memory; each batch's
+// slice of every array is copied into one of two device slots on the copy
+// stream).  beg/end: the batch's element range; pad: elements copied past
+// it (the kernels' padded tail loads).  Before batch b runs, the shard's
+// pointer field is bound to slot - beg[b] (element-wise), so the views the
+// kernels get (field + the batch's own offset) land in the slot.
+struct StreamArr {
+    void **field = nullptr;
+    size_t es = 0, pad = 0;
+    std::vector<int64_t> beg, end;
+    std::shared_ptr<void> keep;  // the host array, page-locked
+    const char *host = nullptr;
+    bool registered = false;
+    void *slot[2] = {nullptr, nullptr};
+    size_t cap = 0;  // elements per slot
 };
 
 struct TrainShard {
@@ -86,7 +105,10 @@ struct TrainShard {
     bool streamed = false, host_registered = false;
     const float *hX = nullptr;
     float *sx[2] = {nullptr, nullptr}, *sl[2] = {nullptr, nullptr};
-    int64_t sb[2] = {-1, -1};  // batch held by each slot
+    int64_t sb[2] = {-1, -1};  // batch held by each slot (dense or sparse streaming)
+    // streamed sparse shard: every per-batch array (StreamArr)
+    bool sparse_stream = false;
+    std::vector<StreamArr> sarr;
     bool row16 = false;
     uint32_t *cptr = nullptr;   // n_batches x (D+1)
     void *crow = nullptr;
@@ -246,8 +268,25 @@ int upload(dlr_ctx *c, T **dst, const T *src, size_t n, size_t pad = 0) {
     return DLR_OK;
 }
 
+// A shard array: uploaded (resident), or -- for a streamed sparse shard --
+// kept page-locked in host memory with its per-batch element ranges
+// rng(b) = [beg, end) and two device slots (StreamArr).  The host copy is
+// made here, so src may be freed on return.
+using RangeFn = std::function<std::pair<int64_t, int64_t>(int64_t)>;
+template <typename T>
+int place(dlr_ctx *c, T **field, const T *src, size_t n, size_t pad, const RangeFn &rng);
+
 void free_train(dlr_ctx *c) {
     TrainShard &t = c->train;
+    if (t.sparse_stream) {
+        if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+        for (StreamArr &a : t.sarr) {
+            if (a.registered) (void)hipHostUnregister(const_cast<char *>(a.host));
+            dev_free(c, a.slot[0]);
+            dev_free(c, a.slot[1]);
+            *a.field = nullptr;  // the bound view pointed into a slot
+        }
+    }
     if (t.streamed) {
         if (c->cstream) (void)hipStreamSynchronize(c->cstream);
         if (t.host_registered) (void)hipHostUnregister(const_cast<float *>(t.hX));
@@ -262,6 +301,46 @@ void free_train(dlr_ctx *c) {
                     (void *)t.lpslot, (void *)t.lpws, (void *)t.lprow, (void *)t.lpval})
         dev_free(c, p);
     t = TrainShard();
+}
+
+template <typename T>
+int place(dlr_ctx *c, T **field, const T *src, size_t n, size_t pad, const RangeFn &rng) {
+    TrainShard &t = c->train;
+    if (!t.sparse_stream) return upload(c, field, src, n, pad);
+    const int64_t nb = (int64_t)t.plan.size();
+    StreamArr a;
+    a.field = reinterpret_cast<void **>(field);
+    a.es = sizeof(T);
+    a.pad = pad;
+    a.beg.resize((size_t)nb);
+    a.end.resize((size_t)nb);
+    size_t cap = 1;
+    for (int64_t b = 0; b < nb; ++b) {
+        const std::pair<int64_t, int64_t> r = rng(b);
+        a.beg[(size_t)b] = r.first;
+        a.end[(size_t)b] = std::max(r.first, r.second);
+        if (a.end[(size_t)b] > a.beg[(size_t)b]) cap = std::max(cap, (size_t)(a.end[(size_t)b] - a.beg[(size_t)b]) + pad);
+    }
+    auto *hv = new std::vector<T>(n + pad);  // zero tail: the padded reads of the last batch
+    if (n) std::copy(src, src + n, hv->begin());
+    a.keep = std::shared_ptr<void>(hv, [](void *p) { delete static_cast<std::vector<T> *>(p); });
+    a.host = reinterpret_cast<const char *>(hv->data());
+    hipError_t e = hipHostRegister(const_cast<char *>(a.host), (n + pad) * sizeof(T), hipHostRegisterDefault);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(c, DLR_E_HIP, std::string("dlr_load_train: hipHostRegister (streamed shard): ") + hipGetErrorString(e));
+    }
+    a.registered = true;
+    a.cap = cap;
+    *field = nullptr;
+    t.sarr.push_back(std::move(a));
+    StreamArr &sa = t.sarr.back();
+    for (int k = 0; k < 2; ++k) {
+        const int rc = dev_alloc(c, &sa.slot[k], cap * sizeof(T));
+        if (rc) return rc;
+    }
+    t.bytes += (int64_t)(2 * cap * sizeof(T));
+    return DLR_OK;
 }
 
 void free_touched_bufs(dlr_ctx *c) {
@@ -991,6 +1070,53 @@ hipError_t stage_dense(dlr_ctx *c, int64_t b, int s) {
     return e;
 }
 
+// Streamed sparse shard: copy batch b's slice of every array into slot s
+// after the kernels that last read the slot are done (ev_free[s]).
+hipError_t stage_sparse(dlr_ctx *c, int64_t b, int s) {
+    TrainShard &t = c->train;
+    hipError_t e = hipStreamWaitEvent(c->cstream, c->ev_free[s], 0);
+    for (StreamArr &a : t.sarr) {
+        if (e != hipSuccess) break;
+        const int64_t beg = a.beg[(size_t)b], end = a.end[(size_t)b];
+        if (end <= beg) continue;
+        e = hipMemcpyAsync(a.slot[s], a.host + (size_t)beg * a.es, ((size_t)(end - beg) + a.pad) * a.es,
+                           hipMemcpyHostToDevice, c->cstream);
+    }
+    if (e == hipSuccess) e = hipEventRecord(c->ev_ready[s], c->cstream);
+    t.sb[s] = e == hipSuccess ? b : -1;
+    return e;
+}
+
+// Before batch b's kernels: its slices are (being) staged, the engine
+// stream waits for them, and every streamed array's pointer is bound to
+// the slot (slot - beg[b] elements: the views add the batch's offsets).
+hipError_t sparse_batch(dlr_ctx *c, int64_t b) {
+    TrainShard &t = c->train;
+    int s = t.sb[0] == b ? 0 : t.sb[1] == b ? 1 : -1;
+    hipError_t e = hipSuccess;
+    if (s < 0) {
+        s = (int)(b & 1);
+        e = stage_sparse(c, b, s);
+    }
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_ready[s], 0);
+    for (StreamArr &a : t.sarr) {
+        void *p = static_cast<char *>(a.slot[s]) - (ptrdiff_t)((size_t)a.beg[(size_t)b] * a.es);
+        memcpy(a.field, &p, sizeof p);
+    }
+    return e;
+}
+
+// After batch b's last kernel: release its slot and start staging the next
+// batch into the other one (it overlaps this step's remaining work).
+hipError_t sparse_batch_done(dlr_ctx *c, int64_t b) {
+    TrainShard &t = c->train;
+    const int s = t.sb[0] == b ? 0 : 1;
+    hipError_t e = hipEventRecord(c->ev_free[s], c->stream);
+    const int64_t nx = (b + 1) % (int64_t)t.plan.size();
+    if (e == hipSuccess && t.sb[0] != nx && t.sb[1] != nx) e = stage_sparse(c, nx, s ^ 1);
+    return e;
+}
+
 // Batch b's rows as the dense kernels see them: the resident shard (rows
 // from plan.first_row, wrapping), or the slot b is staged in (rows 0..B-1;
 // the engine stream waits for its copy).
@@ -1341,14 +1467,64 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
     }
     const CsrView src{ds->n_rows, ds->row_ptr.data(), c->perm.empty() ? ds->col.data() : mapped.data(),
                       ds->val.data()};
-    // Shard CSR (no value array for a unit-valued shard).
     t.unit = unit_values(ds->val);
-    if ((rc = upload(c, &t.row_ptr, ds->row_ptr.data(), (size_t)t.n_rows + 1))) return rc;
-    if ((rc = upload(c, &t.col, src.col, (size_t)t.nnz, kPad))) return rc;
-    if (!t.unit && (rc = upload(c, &t.val, ds->val.data(), (size_t)t.nnz, kPad))) return rc;
+    // Row bands (classic layout, DLR_BAND_ROWS: rows per band, rounded down
+    // to a power of two; 0 = off; default 2^20 rows, a 4 MB residual slice,
+    // for batches of >= 2 bands); the long columns then go in row phases.
+    const char *brs = getenv("DLR_BAND_ROWS");
+    const int64_t band_rows = brs ? atoll(brs) : (int64_t)1 << 20;
+    int shift = 0;
+    while (band_rows > 0 && ((int64_t)2 << shift) <= band_rows) ++shift;
+    const bool band = !t.touched && band_rows > 0 && shift > 0 &&
+                      (brs ? t.B > ((int64_t)1 << shift) : t.B >= ((int64_t)2 << shift));
+    // Residency (K1, data_iter.h:40-55's batches): resident in HBM, or --
+    // DLR_RESIDENCY_STREAM, or AUTO when the shard would not leave 8 GiB of
+    // HBM free -- kept in page-locked host memory and staged batch by batch
+    // into two device slots on the copy stream (every array below goes
+    // through place()).  A band-mode batch (>= 2^21 rows) is one huge step:
+    // streaming it per batch buys nothing, so it stays resident.
+    {
+        const double est = (double)t.nnz * (t.unit ? 10.0 : 16.0) + (double)t.n_rows * 16.0 +
+                           (t.touched ? 0.0 : (double)nb * (double)(D + 1) * 4.0);
+        bool stream = c->residency == DLR_RESIDENCY_STREAM;
+        if (c->residency == DLR_RESIDENCY_AUTO) {
+            size_t fr = 0, tot = 0;
+            HIPC(c, hipMemGetInfo(&fr, &tot));
+            stream = est + (double)((size_t)8 << 30) > (double)fr;
+        }
+        if (stream && band)
+            return fail(c, DLR_E_ARG, "dlr_load_train: a band-mode batch (>= 2^21 rows) cannot be streamed per batch");
+        t.sparse_stream = stream;
+        if (stream) {
+            if (!c->cstream) HIPC(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+            for (int k = 0; k < 2; ++k) {
+                if (!c->ev_ready[k]) HIPC(c, hipEventCreateWithFlags(&c->ev_ready[k], hipEventDisableTiming));
+                if (!c->ev_free[k]) HIPC(c, hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming));
+                HIPC(c, hipEventRecord(c->ev_free[k], c->stream));
+            }
+        }
+    }
+    // Shard CSR (no value array for a unit-valued shard).  Streamed: batch
+    // b's rows [first, first + B) (the wrapping batch is materialised below
+    // and stays resident).
+    auto csr_rows = [&](int64_t extra) -> RangeFn {
+        return [&, extra](int64_t b) -> std::pair<int64_t, int64_t> {
+            const dlr::BatchSpan &sp = t.plan[(size_t)b];
+            if (!sp.contiguous) return {0, 0};
+            return {sp.first_row, sp.first_row + sp.rows + extra};
+        };
+    };
+    const RangeFn csr_entries = [&](int64_t b) -> std::pair<int64_t, int64_t> {
+        const dlr::BatchSpan &sp = t.plan[(size_t)b];
+        if (!sp.contiguous) return {0, 0};
+        return {ds->row_ptr[(size_t)sp.first_row] & ~int64_t(3), ds->row_ptr[(size_t)(sp.first_row + sp.rows)]};
+    };
+    if ((rc = place(c, &t.row_ptr, ds->row_ptr.data(), (size_t)t.n_rows + 1, 0, csr_rows(1)))) return rc;
+    if ((rc = place(c, &t.col, src.col, (size_t)t.nnz, kPad, csr_entries))) return rc;
+    if (!t.unit && (rc = place(c, &t.val, ds->val.data(), (size_t)t.nnz, kPad, csr_entries))) return rc;
     {
         std::vector<float> lab(ds->label.begin(), ds->label.end());
-        if ((rc = upload(c, &t.label, lab.data(), lab.size()))) return rc;
+        if ((rc = place(c, &t.label, lab.data(), lab.size(), 0, csr_rows(0)))) return rc;
     }
     // Materialise the (at most one) wrapping batch.
     for (int64_t b = 0; b < nb; ++b) {
@@ -1405,10 +1581,14 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         std::vector<uint16_t> prow((size_t)total, 0);
         std::vector<float> pval((size_t)total, 0.0f);
         pcsc_fill(src, t.plan, D, pb, t.poff, base, ends, prow, pval, nthreads);
-        if ((rc = upload(c, &t.pbase, base.data(), base.size()))) return rc;
-        if ((rc = upload(c, &t.pends, ends.data(), ends.size()))) return rc;
-        if ((rc = upload(c, &t.prow, prow.data(), prow.size(), 256))) return rc;
-        if ((rc = upload(c, &t.pval, pval.data(), pval.size(), 256))) return rc;
+        const int64_t pbk = pb.pblocks;
+        const RangeFn r_base = [&](int64_t b) { return std::make_pair(b * (pbk + 1), (b + 1) * (pbk + 1)); };
+        const RangeFn r_ends = [&](int64_t b) { return std::make_pair(b * pbk * 64, (b + 1) * pbk * 64); };
+        const RangeFn r_ent = [&](int64_t b) { return std::make_pair(t.poff[(size_t)b], t.poff[(size_t)b + 1]); };
+        if ((rc = place(c, &t.pbase, base.data(), base.size(), 0, r_base))) return rc;
+        if ((rc = place(c, &t.pends, ends.data(), ends.size(), 0, r_ends))) return rc;
+        if ((rc = place(c, &t.prow, prow.data(), prow.size(), 256, r_ent))) return rc;
+        if ((rc = place(c, &t.pval, pval.data(), pval.size(), 256, r_ent))) return rc;
         csc_bytes = (int64_t)(base.size() * 4 + ends.size() + (total + 256) * 6);
         resid_need = (int64_t)pb.P * pb.R;  // the fills read whole phases
     } else if (t.touched) {
@@ -1451,14 +1631,17 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             }
         }
         tbs.clear();
-        if ((rc = upload(c, &t.tcols, tcols.data(), tcols.size(), 64))) return rc;
-        if ((rc = upload(c, &t.cptr, tptr.data(), tptr.size()))) return rc;
+        const RangeFn r_cols = [&](int64_t b) { return std::make_pair(t.tcoff[(size_t)b], t.tcoff[(size_t)b + 1]); };
+        const RangeFn r_ptr = [&](int64_t b) { return std::make_pair(t.tpoff[(size_t)b], t.tpoff[(size_t)b + 1]); };
+        const RangeFn r_ent = [&](int64_t b) { return std::make_pair(t.coff[(size_t)b], t.coff[(size_t)b + 1]); };
+        if ((rc = place(c, &t.tcols, tcols.data(), tcols.size(), 64, r_cols))) return rc;
+        if ((rc = place(c, &t.cptr, tptr.data(), tptr.size(), 0, r_ptr))) return rc;
         if (t.row16) {
-            if ((rc = upload(c, (uint16_t **)&t.crow, crow16.data(), crow16.size(), kPad))) return rc;
+            if ((rc = place(c, (uint16_t **)&t.crow, crow16.data(), crow16.size(), kPad, r_ent))) return rc;
         } else {
-            if ((rc = upload(c, (uint32_t **)&t.crow, crow32.data(), crow32.size(), kPad))) return rc;
+            if ((rc = place(c, (uint32_t **)&t.crow, crow32.data(), crow32.size(), kPad, r_ent))) return rc;
         }
-        if (!t.unit && (rc = upload(c, &t.cval, cval.data(), cval.size(), kPad))) return rc;
+        if (!t.unit && (rc = place(c, &t.cval, cval.data(), cval.size(), kPad, r_ent))) return rc;
         csc_bytes = (int64_t)(tcols.size() * 4 + tptr.size() * 4 +
                               (total + kPad) * ((t.row16 ? 2 : 4) + (t.unit ? 0 : 4)));
         // step buffers and every rank's batch size (L2 term of its pushes)
@@ -1482,15 +1665,6 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         if (total >= (int64_t)1 << 31) return fail(c, DLR_E_ARG, "dlr_load_train: a batch has >= 2^31 entries");
         std::vector<uint32_t> cptr((size_t)nb * (size_t)(D + 1));
         std::vector<float> cval(t.unit ? 0 : (size_t)total);
-        // Row bands for the short columns of large batches (DLR_BAND_ROWS:
-        // rows per band, rounded down to a power of two; 0 = off; default
-        // 2^20 rows, a 4 MB residual slice, for batches of >= 2 bands); the
-        // long columns then go in row phases (build_long_phases)
-        const char *brs = getenv("DLR_BAND_ROWS");
-        const int64_t band_rows = brs ? atoll(brs) : (int64_t)1 << 20;
-        int shift = 0;
-        while (band_rows > 0 && ((int64_t)2 << shift) <= band_rows) ++shift;
-        const bool band = band_rows > 0 && shift > 0 && (brs ? t.B > ((int64_t)1 << shift) : t.B >= ((int64_t)2 << shift));
         // Long columns (DLR_LONG_COLUMN entries in a batch; 0 = none) are
         // summed in a fixed chunked order instead of the reference's single
         // sequential chain.  Default: 4,096 in band mode only
@@ -1561,14 +1735,20 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 L = {};
             }
             int r;
-            if ((r = upload(c, &t.lcols, cols.data(), cols.size()))) return r;
-            if ((r = upload(c, &t.lcseg, cseg.data(), cseg.size()))) return r;
-            if ((r = upload(c, &t.lsptr, sptr.data(), sptr.size()))) return r;
+            const RangeFn r_cols = [&](int64_t b) { return std::make_pair(t.lcoff[(size_t)b], t.lcoff[(size_t)b + 1]); };
+            const RangeFn r_cseg = [&](int64_t b) {
+                return std::make_pair(t.lcoff[(size_t)b] + b, t.lcoff[(size_t)b + 1] + b + 1);
+            };
+            const RangeFn r_seg = [&](int64_t b) { return std::make_pair(t.lsoff[(size_t)b], t.lsoff[(size_t)b + 1]); };
+            const RangeFn r_ent = [&](int64_t b) { return std::make_pair(t.leoff[(size_t)b], t.leoff[(size_t)b + 1]); };
+            if ((r = place(c, &t.lcols, cols.data(), cols.size(), 0, r_cols))) return r;
+            if ((r = place(c, &t.lcseg, cseg.data(), cseg.size(), 0, r_cseg))) return r;
+            if ((r = place(c, &t.lsptr, sptr.data(), sptr.size(), 0, r_seg))) return r;
             if (!(getenv("DLR_LONG_SCHED") && strcmp(getenv("DLR_LONG_SCHED"), "0") == 0) &&
-                (r = upload(c, &t.lsched, sched.data(), sched.size())))
+                (r = place(c, &t.lsched, sched.data(), sched.size(), 0, r_seg)))
                 return r;
-            if ((r = upload(c, (RowT **)&t.lrow, row.data(), row.size(), dlr::kLongChunk))) return r;
-            if (!t.unit && (r = upload(c, &t.lval, val.data(), val.size(), dlr::kLongChunk))) return r;
+            if ((r = place(c, (RowT **)&t.lrow, row.data(), row.size(), dlr::kLongChunk, r_ent))) return r;
+            if (!t.unit && (r = place(c, &t.lval, val.data(), val.size(), dlr::kLongChunk, r_ent))) return r;
             if ((r = dev_alloc(c, (void **)&t.lpart, (size_t)maxseg * 4))) return r;
             lbytes = (int64_t)(cols.size() * 4 + cseg.size() * 4 + sptr.size() * 4 + row.size() * sizeof(RowT) +
                                val.size() * 4);
@@ -1580,7 +1760,8 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             int r;
             if ((r = finish_long(lb))) return r;
             if (!band) {
-                if ((r = upload(c, (RowT **)&t.crow, crow.data(), crow.size(), kPad))) return r;
+                const RangeFn r_ent = [&](int64_t b) { return std::make_pair(t.coff[(size_t)b], t.coff[(size_t)b + 1]); };
+                if ((r = place(c, (RowT **)&t.crow, crow.data(), crow.size(), kPad, r_ent))) return r;
                 return DLR_OK;
             }
             BandBuild<RowT> bb;
@@ -1608,8 +1789,10 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             if ((rc = classic(crow, lb))) return rc;
         }
         if (!band) {
-            if ((rc = upload(c, &t.cptr, cptr.data(), cptr.size()))) return rc;
-            if (!t.unit && (rc = upload(c, &t.cval, cval.data(), cval.size(), kPad))) return rc;
+            const RangeFn r_ptr = [&](int64_t b) { return std::make_pair(b * (D + 1), (b + 1) * (D + 1)); };
+            const RangeFn r_ent = [&](int64_t b) { return std::make_pair(t.coff[(size_t)b], t.coff[(size_t)b + 1]); };
+            if ((rc = place(c, &t.cptr, cptr.data(), cptr.size(), 0, r_ptr))) return rc;
+            if (!t.unit && (rc = place(c, &t.cval, cval.data(), cval.size(), kPad, r_ent))) return rc;
         }
         // Entry-balanced wave schedule: a wave takes consecutive columns until
         // it has 64 or about one window (kWin entries) of them -- a column
@@ -1641,7 +1824,8 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             std::vector<uint32_t> all;
             all.reserve((size_t)t.wsoff[(size_t)nb]);
             for (auto &v : ws) all.insert(all.end(), v.begin(), v.end());
-            if ((rc = upload(c, &t.wsched, all.data(), all.size()))) return rc;
+            const RangeFn r_ws = [&](int64_t b) { return std::make_pair(t.wsoff[(size_t)b], t.wsoff[(size_t)b + 1]); };
+            if ((rc = place(c, &t.wsched, all.data(), all.size(), 0, r_ws))) return rc;
             csc_bytes += (int64_t)all.size() * 4;
         }
         if (!band)
@@ -1657,7 +1841,9 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         HIPC(c, hipStreamSynchronize(c->stream));
         c->resid_cap = resid_need;
     }
-    t.bytes = (int64_t)((t.n_rows + 1) * 8 + (t.nnz + kPad) * (t.unit ? 4 : 8) + t.n_rows * 4) + csc_bytes;
+    // streamed: the slots (counted by place()); resident: the shard arrays
+    if (!t.sparse_stream)
+        t.bytes = (int64_t)((t.n_rows + 1) * 8 + (t.nnz + kPad) * (t.unit ? 4 : 8) + t.n_rows * 4) + csc_bytes;
     t.loaded = true;
     if (n_batches) *n_batches = nb;
     return DLR_OK;
@@ -1818,6 +2004,7 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
     if (bt.rows > c->resid_cap) return fail(c, DLR_E_STATE, "dlr_train_step: residual buffer too small");
     hipEvent_t t_step, t0;
     time_begin(c, &t_step);
+    if (c->train.sparse_stream) HIPC(c, sparse_batch(c, b));  // binds the batch's slot (the views below)
     time_begin(c, &t0);
     HIPC(c, launch_margin(c, b));
     time_end(c, 0, t0);
@@ -1876,6 +2063,7 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
         COMMC(c, all_gather(c->w + (int64_t)c->rank * c->chunk, c->w, (size_t)c->chunk, c->stream, e_));
         time_end(c, 3, t0);
     }
+    if (c->train.sparse_stream) HIPC(c, sparse_batch_done(c, b));
     time_end(c, 4, t_step);
     return DLR_OK;
 }
@@ -1899,6 +2087,7 @@ int dlr_worker_gradient(dlr_ctx *c, int64_t b, float C, float *grad_out, int64_t
     struct {
         int64_t rows;
     } const bt{c->train.plan[(size_t)b].rows};
+    if (c->train.sparse_stream) HIPC(c, sparse_batch(c, b));
     HIPC(c, launch_margin(c, b));
     if (c->train.touched) {
         // full pushed vector: the L2 term everywhere, the touched columns' g
@@ -1912,6 +2101,7 @@ int dlr_worker_gradient(dlr_ctx *c, int64_t b, float C, float *grad_out, int64_t
     } else {
         HIPC(c, launch_gradient(c, b, bt.rows, c->g, 0.0f, C, false));
     }
+    if (c->train.sparse_stream) HIPC(c, sparse_batch_done(c, b));
     if (c->perm.empty()) {
         HIPC(c, hipMemcpyAsync(grad_out, c->g, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
         HIPC(c, hipStreamSynchronize(c->stream));
@@ -2010,7 +2200,8 @@ int dlr_stage_time(dlr_ctx *c, int stage, int64_t first, int64_t count, float lr
     const TrainShard &t = c->train;
     if (stage == DLR_STAGE_UPDATE && !t.touched)
         return fail(c, DLR_E_ARG, "dlr_stage_time: the update stage is separate only in the touched layout");
-    if (t.streamed) return fail(c, DLR_E_STATE, "dlr_stage_time: streamed shard (kernel stages wait on batch copies)");
+    if (t.streamed || t.sparse_stream)
+        return fail(c, DLR_E_STATE, "dlr_stage_time: streamed shard (kernel stages wait on batch copies)");
     HIPC(c, hipSetDevice(c->device));
     harvest(c);
     const bool was = c->timing;
@@ -2061,7 +2252,7 @@ int dlr_set_residency(dlr_ctx *c, int mode) {
 int dlr_train_residency(dlr_ctx *c) {
     if (!c) return DLR_E_ARG;
     if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_residency: no training shard loaded");
-    return c->train.streamed ? DLR_RESIDENCY_STREAM : DLR_RESIDENCY_DEVICE;
+    return c->train.streamed || c->train.sparse_stream ? DLR_RESIDENCY_STREAM : DLR_RESIDENCY_DEVICE;
 }
 
 int dlr_train_relabeled(dlr_ctx *c) {

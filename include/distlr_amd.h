@@ -234,13 +234,17 @@ int dlr_load_test(dlr_ctx *ctx, const dlr_dataset *ds);
 int dlr_load_train_dense(dlr_ctx *ctx, const dlr_dense *ds, int64_t batch_size, int64_t *n_batches);
 int dlr_load_test_dense(dlr_ctx *ctx, const dlr_dense *ds);
 
-/* Residency of the next dense training shard (20M x 4096
- * fp32 is 328 GB, more than one GPU's HBM).  DEVICE uploads the rows once;
- * STREAM keeps them in the caller's host memory (registered in place, so
- * the dlr_dense must outlive the loaded shard) and copies each batch into
- * one of two device slots on a copy stream while the previous batch
- * computes -- PCIe-bound; AUTO (default) streams only when the rows would
- * not fit in free HBM.  Results are identical either way.
+/* K1 -- residency of the next training shard (replaces DataIter's
+ * per-batch copies, data_iter.h:40-55; SURVEY 8(d) C4: 20M x 4096 fp32 is
+ * 328 GB, more than one GPU's HBM).  DEVICE uploads the shard once; STREAM
+ * keeps it in page-locked host memory and copies each batch into one of two
+ * device slots on a copy stream while the previous batch computes --
+ * PCIe-bound.  Dense shards stream the caller's rows in place (registered:
+ * the dlr_dense must outlive the loaded shard); sparse shards stream a
+ * page-locked copy of their CSR and per-batch column-major slices (every
+ * layout except band mode, whose one >= 2^21-row batch is not worth
+ * streaming: DLR_E_ARG).  AUTO (default) streams only when the shard would
+ * not leave 8 GiB of HBM free.  Results are bitwise identical either way.
  * dlr_train_residency reports what the loaded shard uses. */
 #define DLR_RESIDENCY_AUTO 0
 #define DLR_RESIDENCY_DEVICE 1
