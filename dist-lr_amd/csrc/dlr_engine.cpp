@@ -97,7 +97,7 @@ struct TrainShard {
     float *lval = nullptr, *lpart = nullptr;
     std::vector<int64_t> lcoff, lsoff, leoff;
     // dense shard (dlr_load_train_dense): X row-major n_rows x D
-    bool dense = false, dblocked = false;
+    bool dense = false, dblocked = false, dfused = false;
     float *dX = nullptr, *dpart = nullptr;
     // streamed dense shard (DLR_RESIDENCY_STREAM): X stays in the caller's
     // host memory (registered, pinned in place); each batch's rows and labels
@@ -1159,6 +1159,7 @@ hipError_t launch_margin(dlr_ctx *c, int64_t b) {
         int64_t first;
         hipError_t e = dense_batch(c, b, &dd, &first);
         if (e != hipSuccess) return e;
+        if (t.dfused) return dlr::launch_dense_fused(dd, first, t.plan[(size_t)b].rows, c->w, t.dpart, c->stream);
         return dlr::launch_dense_margin(dd, first, t.plan[(size_t)b].rows, c->w, c->resid, c->stream);
     }
     if (t.margin_hot) return dlr::launch_margin_hot(batch_view(c, b), c->w, c->D, c->resid, c->stream);
@@ -1191,7 +1192,9 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
         int64_t first;
         hipError_t e = dense_batch(c, b, &dd, &first);
         if (e == hipSuccess)
-            e = dlr::launch_dense_grad(dd, first, B, c->resid, c->w, gout, t.dpart, t.dblocked, lr, C, fused, c->stream);
+            e = t.dfused ? dlr::launch_dense_combine(t.dpart, c->D, B, c->w, gout, lr, C, fused, c->stream)
+                         : dlr::launch_dense_grad(dd, first, B, c->resid, c->w, gout, t.dpart, t.dblocked, lr, C, fused,
+                                                  c->stream);
         if (e == hipSuccess) e = dense_batch_done(c, b);
         return e;
     }
@@ -1910,7 +1913,10 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
     t.plan = dlr::plan_batches(ds->n_rows, batch_size);
     const int64_t D = c->D;
     const char *dg = getenv("DLR_DENSE_GRAD");
-    t.dblocked = dg ? strcmp(dg, "blocked") == 0 : (t.B * D > ((int64_t)1 << 24));
+    t.dfused = dg && strcmp(dg, "fused") == 0;
+    if (t.dfused && !dlr::dense_fused_ok(D))
+        return fail(c, DLR_E_ARG, "dlr_load_train_dense: DLR_DENSE_GRAD=fused needs D in {512, 1024, 2048, 4096}");
+    t.dblocked = t.dfused || (dg ? strcmp(dg, "blocked") == 0 : (t.B * D > ((int64_t)1 << 24)));
     // Residency: device-resident unless asked to stream, or (auto) the rows
     // would not leave room in HBM (20M x 4096 fp32 = 328 GB
     // on one 288 GB GPU).  Streamed rows are staged per batch over PCIe.

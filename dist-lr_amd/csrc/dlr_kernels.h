@@ -171,6 +171,13 @@ hipError_t launch_dense_margin(const DevDense &dd, int64_t first, int64_t B, con
 int64_t dense_chunks(int64_t B);  // row chunks of the blocked gradient (part: chunks x roundup4(D) floats)
 hipError_t launch_dense_grad(const DevDense &dd, int64_t first, int64_t B, const float *resid, float *w, float *gout,
                              float *part, bool blocked, float lr, float C, bool fused, hipStream_t s);
+// K6 fused (DLR_DENSE_GRAD=fused): margin + blocked gradient partials in
+// one pass over X (part: dense_chunks(B) x D), then the combine + update.
+bool dense_fused_ok(int64_t D);  // D in {512, 1024, 2048, 4096}
+hipError_t launch_dense_fused(const DevDense &dd, int64_t first, int64_t B, const float *w, float *part,
+                              hipStream_t s);
+hipError_t launch_dense_combine(const float *part, int64_t D, int64_t B, float *w, float *gout, float lr, float C,
+                                bool fused, hipStream_t s);
 int predict_dense_grid(int64_t rows);
 hipError_t launch_dense_predict(const DevDense &dd, const float *w, unsigned long long *correct, double *ll_part,
                                 double *ll_out, hipStream_t s);

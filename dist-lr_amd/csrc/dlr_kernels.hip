@@ -1372,6 +1372,166 @@ __global__ __launch_bounds__(256) void k_dense_grad_blocked(DevDense dd, int64_t
     }
 }
 
+// K6 fused (DLR_DENSE_GRAD=fused): margin AND the blocked gradient partials
+// in ONE pass over X.  The two-kernel path reads every batch row twice from
+// HBM (the gradient needs a row's residual, which exists only after the
+// whole row is summed); here workgroup k owns the same 256-row chunk as
+// k_dense_grad_blocked and streams it through LDS two rows at a time, so
+// each row is read from HBM once and used twice from LDS.  Staging: every
+// thread holds the next two sub-chunks in registers (16-byte loads, 64 KiB
+// per CU in flight) and writes one into the free LDS buffer per step
+// (register staging: the compiler's waits are per register, where LDS-DMA
+// pieces would make it drain every load before each LDS read).
+//   margin   wave 0: lane (i, q) -- row i of the sub-chunk, q < 32 -- sums
+//            the columns 128t + 4q .. +3 for t = 0, 1, ... in order (LDS
+//            reads conflict-free), then lane 32i adds the 32 partials in q
+//            order: z is a fixed blocked order, not lr.cc:108-112's single
+//            chain (same tolerance regime as the blocked gradient);
+//   gradient all 256 threads: column quad g sums r_i * x_i in row order,
+//            continuing across the chunk's sub-chunks -- exactly
+//            k_dense_grad_blocked's per-chunk order -- into part[k].
+// k_dense_combine then adds the chunk partials and applies the update.
+// Needs D % 256 == 0 and D <= 4096.
+typedef float v4f __attribute__((ext_vector_type(4)));  // staging registers (SROA-friendly)
+constexpr int kFuseRows = 2;   // rows per sub-chunk
+constexpr int kFuseMaxD = 4096;
+constexpr int kFuseRegs = kFuseRows * kFuseMaxD / 4 / 256;  // float4 per thread per sub-chunk (max)
+
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <int DQ>  // D / 4
+__global__ __launch_bounds__(256) void k_dense_fused(DevDense dd, int64_t first, int64_t B,
+                                                     const float *__restrict__ w, int64_t Dp,
+                                                     float *__restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) float fsm[];
+    constexpr int64_t D = 4 * DQ;
+    constexpr int d4 = DQ;                               // float4 per row
+    float *s_x = fsm;                                    // 2 buffers x kFuseRows x D
+    float *s_w = fsm + (size_t)2 * kFuseRows * D;        // D
+    float *s_zp = s_w + D;                               // kFuseRows x 32 margin partials
+    float *s_r = s_zp + kFuseRows * 32;                  // kFuseRows residuals
+    float *s_lab = s_r + kFuseRows;                      // the chunk's labels (kDenseChunk)
+    int64_t *s_roff = reinterpret_cast<int64_t *>(s_lab + kDenseChunk);  // row offsets (kDenseChunk + kFuseRows)
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wv = tid / kWave;
+    const int64_t k = blockIdx.x;
+    const int64_t i0 = k * kDenseChunk, i1 = min(i0 + kDenseChunk, B);
+    const int nsub = (int)((i1 - i0 + kFuseRows - 1) / kFuseRows);
+    constexpr int nreg = kFuseRows * d4 / 256;           // float4 per thread per sub-chunk
+    static_assert(nreg >= 1 && nreg <= kFuseRegs && kFuseRows * d4 % 256 == 0, "D % 512 == 0, D <= 4096");
+    // sub-chunk q's float4 f = p * 256 + tid (p < nreg) into registers RG;
+    // rows past the chunk end re-read its last row (never used)
+    // (sub-chunks past the last re-load the last one: never used, but every
+    // step issues the same loads, so the compiler's vmcnt waits stay exact)
+#define DLR_FUSE_LOAD(q, RG)                                                                                   \
+    {                                                                                                          \
+        const int qc_ = min((q), nsub - 1);                                                                    \
+        _Pragma("unroll") for (int p = 0; p < nreg; ++p)                                                       \
+            RG[p] = *reinterpret_cast<const v4f *>(dd.X + s_roff[qc_ * kFuseRows + fri[p]] + fc[p]);           \
+    }
+#define DLR_FUSE_STORE(q, RG)                                                                                  \
+    {                                                                                                          \
+        float *sbuf_ = s_x + (size_t)((q) & 1) * kFuseRows * D;                                                \
+        _Pragma("unroll") for (int p = 0; p < nreg; ++p)                                                       \
+            *reinterpret_cast<v4f *>(sbuf_ + (size_t)(p * 256 + tid) * 4) = RG[p];                             \
+    }
+    // this thread's column quads: g = tid, tid + 256, ... (D / 4 quads)
+    constexpr int kMaxQ = (d4 + 255) / 256;
+    const int nq = (d4 + 255 - tid) / 256;
+    float4 acc[kMaxQ];
+#pragma unroll
+    for (int u = 0; u < kMaxQ; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto compute = [&](int q) {
+        const float *buf = s_x + (size_t)(q & 1) * kFuseRows * D;
+        const int64_t r0 = i0 + (int64_t)q * kFuseRows;
+        if (wv == 0) {
+            const int i = lane / 32, qq = lane % 32;
+            const float *x = buf + (size_t)i * D + qq * 4;
+            const float *ww = s_w + qq * 4;
+            float z = 0.0f;
+            for (int64_t t = 0; t < D; t += 128) {
+                const float4 xv = *reinterpret_cast<const float4 *>(x + t);
+                const float4 wq = *reinterpret_cast<const float4 *>(ww + t);
+                z = z + wq.x * xv.x;
+                z = z + wq.y * xv.y;
+                z = z + wq.z * xv.z;
+                z = z + wq.w * xv.w;
+            }
+            s_zp[i * 32 + qq] = z;
+            wave_sync();
+            if (qq == 0 && r0 + i < i1) {
+                float zz = 0.0f;
+                for (int u = 0; u < 32; ++u) zz = zz + s_zp[i * 32 + u];
+                s_r[i] = sigmoid_ref(zz) - s_lab[q * kFuseRows + i];
+            }
+        }
+        lds_barrier();
+        const int nr = (int)min<int64_t>(kFuseRows, i1 - r0);
+        for (int i = 0; i < nr; ++i) {
+            const float r = s_r[i];
+            const float *x = buf + (size_t)i * D;
+#pragma unroll
+            for (int u = 0; u < kMaxQ; ++u) {
+                if (u < nq) {
+                    const float4 xv = *reinterpret_cast<const float4 *>(x + (size_t)(tid + 256 * u) * 4);
+                    acc[u].x = acc[u].x + r * xv.x;
+                    acc[u].y = acc[u].y + r * xv.y;
+                    acc[u].z = acc[u].z + r * xv.z;
+                    acc[u].w = acc[u].w + r * xv.w;
+                }
+            }
+        }
+    };
+    for (int64_t j = tid * 4; j < D; j += 1024) *reinterpret_cast<float4 *>(s_w + j) = *reinterpret_cast<const float4 *>(w + j);
+    if (i0 + tid < i1) s_lab[tid] = dd.label[wrap_row(first + i0 + tid, dd.N)];
+    // shard offset of each of the chunk's rows (NextBatch's wrap,
+    // data_iter.h:49-52; rows past the chunk end repeat its last row), and
+    // this thread's (row, column) of each staged float4
+    for (int ii = tid; ii < kDenseChunk + kFuseRows; ii += 256) {
+        const int64_t r = min(i0 + ii, i1 - 1);
+        s_roff[ii] = wrap_row(first + r, dd.N) * D;
+    }
+    int fri[nreg];
+    int64_t fc[nreg];
+#pragma unroll
+    for (int p = 0; p < nreg; ++p) {
+        const int f = p * 256 + tid;
+        fri[p] = f / d4;
+        fc[p] = (int64_t)(f - fri[p] * d4) * 4;
+    }
+    __syncthreads();
+    v4f ra[nreg], rb[nreg];
+    DLR_FUSE_LOAD(0, ra)
+    DLR_FUSE_LOAD(1, rb)
+    DLR_FUSE_STORE(0, ra)
+    DLR_FUSE_LOAD(2, ra)
+    __syncthreads();
+    // step q: compute sub-chunk q (buffer q & 1); store q + 1 (held in the
+    // other register set) into buffer (q + 1) & 1, refill that set with q + 3
+    for (int q = 0; q < nsub; q += 2) {
+        compute(q);
+        DLR_FUSE_STORE(q + 1, rb)  // buffer (q + 1) & 1 was last read in step q - 1
+        DLR_FUSE_LOAD(q + 3, rb)
+        lds_barrier();
+        if (q + 1 < nsub) {  // uniform
+            compute(q + 1);
+            DLR_FUSE_STORE(q + 2, ra)
+            DLR_FUSE_LOAD(q + 4, ra)
+            lds_barrier();
+        }
+    }
+#undef DLR_FUSE_LOAD
+#undef DLR_FUSE_STORE
+#pragma unroll
+    for (int u = 0; u < kMaxQ; ++u)
+        if (u < nq) *reinterpret_cast<float4 *>(part + k * Dp + (int64_t)(tid + 256 * u) * 4) = acc[u];
+}
+
 // Chunk partials of 16 columns per workgroup: the 256 threads stage up to
 // 256 chunks x 16 columns in LDS with one round of 16-byte loads (every
 // workgroup's loads in flight at once: a single memory round trip per tile,
@@ -1868,6 +2028,39 @@ hipError_t launch_dense_margin(const DevDense &dd, int64_t first, int64_t B, con
 }
 
 int64_t dense_chunks(int64_t B) { return (B + kDenseChunk - 1) / kDenseChunk; }
+
+bool dense_fused_ok(int64_t D) { return D == 512 || D == 1024 || D == 2048 || D == 4096; }
+
+hipError_t launch_dense_fused(const DevDense &dd, int64_t first, int64_t B, const float *w, float *part,
+                              hipStream_t s) {
+    if (B <= 0) return hipSuccess;
+    if (!dense_fused_ok(dd.D)) return hipErrorInvalidValue;
+    const size_t lds = ((size_t)2 * kFuseRows * dd.D + dd.D + kFuseRows * 33 + kDenseChunk) * 4 +
+                       (size_t)(kDenseChunk + kFuseRows) * 8 + 16;
+    const dim3 g((unsigned)dense_chunks(B)), blk(256);
+    switch (dd.D) {
+        case 512: hipLaunchKernelGGL(k_dense_fused<128>, g, blk, lds, s, dd, first, B, w, dd.D, part); break;
+        case 1024: hipLaunchKernelGGL(k_dense_fused<256>, g, blk, lds, s, dd, first, B, w, dd.D, part); break;
+        case 2048: hipLaunchKernelGGL(k_dense_fused<512>, g, blk, lds, s, dd, first, B, w, dd.D, part); break;
+        default: hipLaunchKernelGGL(k_dense_fused<1024>, g, blk, lds, s, dd, first, B, w, dd.D, part); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_dense_combine(const float *part, int64_t D, int64_t B, float *w, float *gout, float lr, float C,
+                                bool fused, hipStream_t s) {
+    const int64_t nch = dense_chunks(B);
+    const int64_t Dp = (D + 3) & ~int64_t(3);
+    const float Bf = (float)B;
+    const double Bd = (double)B;
+    if (fused)
+        hipLaunchKernelGGL(k_dense_combine<true>, dim3(grid_for(D, 16)), dim3(256), 0, s, part, nch, Dp, D, w, gout, Bf,
+                           Bd, lr, C);
+    else
+        hipLaunchKernelGGL(k_dense_combine<false>, dim3(grid_for(D, 16)), dim3(256), 0, s, part, nch, Dp, D, w, gout,
+                           Bf, Bd, lr, C);
+    return hipGetLastError();
+}
 
 hipError_t launch_dense_grad(const DevDense &dd, int64_t first, int64_t B, const float *resid, float *w, float *gout,
                              float *part, bool blocked, float lr, float C, bool fused, hipStream_t s) {

@@ -225,3 +225,48 @@ def test_c4_blocked_gradient_full_epoch():
               f"{worst:.3g} (weights >= 1e-2), max abs diff {worst_abs:.3g}")
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("D,B,N", [(512, 300, 1000), (1024, 256, 700), (2048, 1000, 1000), (4096, 600, 1500),
+                                   (4096, 2000, 1500)])
+def test_fused_dense_within_tolerance(monkeypatch, D, B, N):
+    # DLR_DENSE_GRAD=fused: margin + blocked gradient partials in one pass
+    # over X (LDS-staged); a blocked margin order -> tolerance, deterministic.
+    # Cases: chunks with a ragged tail (B % 256), wrapping batches, B > N.
+    monkeypatch.setenv("DLR_DENSE_GRAD", "fused")
+    dd = dlr.DenseDataset.generate(N, D, seed=31, stream=1)
+    got = run_engine([dd], D, 2, B, 0.05, dense=True)
+    orc = oracle.run_worker([dense_shard(dd)], D, 2, B, 0.05, sparse=False)
+    within_bar(got.w, orc.w)
+    again = run_engine([dd], D, 2, B, 0.05, dense=True)
+    assert_same_weights(again.w, got.w)
+
+
+def test_fused_dense_c4_epoch_and_streamed(monkeypatch):
+    # C4's shape (D = 4,096, B = 65,536) over a full epoch of 8 batches, the
+    # last wrapping; then the same shard streamed from host: bitwise equal
+    monkeypatch.setenv("DLR_DENSE_GRAD", "fused")
+    D, B, lr = 4096, 65536, 0.05
+    dd = dlr.DenseDataset.generate(500_000, D, seed=10, stream=3)
+    X, y = dd.arrays()
+    w0 = dlr.init_weight(D)
+    res = {}
+    for residency in ("device", "stream"):
+        monkeypatch.setenv("DLR_RESIDENCY", residency)
+        eng = dlr.Engine(D)
+        try:
+            eng.set_weights(w0)
+            nb = eng.load_train_dense(dd, B)
+            assert nb == 8
+            for b in range(nb):
+                eng.train_step(b, lr, 1.0)
+            res[residency] = eng.get_weights()
+        finally:
+            eng.close()
+    assert_same_weights(res["stream"], res["device"])
+    w = w0.copy()
+    for b in range(8):
+        g = oracle.grad_dense(X, y, oracle.batch_rows(len(y), B, b), w)
+        oracle.server_update(w, [g], lr)
+    a, bb = res["device"].astype(np.float64), w.astype(np.float64)
+    assert np.all(np.abs(a - bb) <= 1e-5 * np.abs(bb) + 1e-6)
