@@ -1376,15 +1376,15 @@ __global__ __launch_bounds__(256) void k_dense_grad_blocked(DevDense dd, int64_t
 // in ONE pass over X.  The two-kernel path reads every batch row twice from
 // HBM (the gradient needs a row's residual, which exists only after the
 // whole row is summed); here workgroup k owns the same 256-row chunk as
-// k_dense_grad_blocked and streams it through LDS two rows at a time, so
+// k_dense_grad_blocked and streams it through LDS four rows at a time, so
 // each row is read from HBM once and used twice from LDS.  Staging: every
 // thread holds the next two sub-chunks in registers (16-byte loads, 64 KiB
 // per CU in flight) and writes one into the free LDS buffer per step
 // (register staging: the compiler's waits are per register, where LDS-DMA
 // pieces would make it drain every load before each LDS read).
-//   margin   wave 0: lane (i, q) -- row i of the sub-chunk, q < 32 -- sums
-//            the columns 128t + 4q .. +3 for t = 0, 1, ... in order (LDS
-//            reads conflict-free), then lane 32i adds the 32 partials in q
+//   margin   wave i (row i of a 4-row sub-chunk): lane l sums the columns
+//            256t + 4l .. +3 for t = 0, 1, ... in order (LDS reads
+//            conflict-free), then lane 0 adds the 64 partials in lane
 //            order: z is a fixed blocked order, not lr.cc:108-112's single
 //            chain (same tolerance regime as the blocked gradient);
 //   gradient all 256 threads: column quad g sums r_i * x_i in row order,
@@ -1393,7 +1393,7 @@ __global__ __launch_bounds__(256) void k_dense_grad_blocked(DevDense dd, int64_t
 // k_dense_combine then adds the chunk partials and applies the update.
 // Needs D % 256 == 0 and D <= 4096.
 typedef float v4f __attribute__((ext_vector_type(4)));  // staging registers (SROA-friendly)
-constexpr int kFuseRows = 2;   // rows per sub-chunk
+constexpr int kFuseRows = 4;   // rows per sub-chunk: one wave's margin each
 constexpr int kFuseMaxD = 4096;
 constexpr int kFuseRegs = kFuseRows * kFuseMaxD / 4 / 256;  // float4 per thread per sub-chunk (max)
 
@@ -1412,8 +1412,8 @@ __global__ __launch_bounds__(256) void k_dense_fused(DevDense dd, int64_t first,
     constexpr int d4 = DQ;                               // float4 per row
     float *s_x = fsm;                                    // 2 buffers x kFuseRows x D
     float *s_w = fsm + (size_t)2 * kFuseRows * D;        // D
-    float *s_zp = s_w + D;                               // kFuseRows x 32 margin partials
-    float *s_r = s_zp + kFuseRows * 32;                  // kFuseRows residuals
+    float *s_zp = s_w + D;                               // kFuseRows x 64 margin partials
+    float *s_r = s_zp + kFuseRows * 64;                  // kFuseRows residuals
     float *s_lab = s_r + kFuseRows;                      // the chunk's labels (kDenseChunk)
     int64_t *s_roff = reinterpret_cast<int64_t *>(s_lab + kDenseChunk);  // row offsets (kDenseChunk + kFuseRows)
     const int tid = threadIdx.x;
@@ -1449,12 +1449,16 @@ __global__ __launch_bounds__(256) void k_dense_fused(DevDense dd, int64_t first,
     auto compute = [&](int q) {
         const float *buf = s_x + (size_t)(q & 1) * kFuseRows * D;
         const int64_t r0 = i0 + (int64_t)q * kFuseRows;
-        if (wv == 0) {
-            const int i = lane / 32, qq = lane % 32;
-            const float *x = buf + (size_t)i * D + qq * 4;
-            const float *ww = s_w + qq * 4;
+        {
+            // wave i: row i of the sub-chunk; lane l sums columns
+            // 256t + 4l .. +3 in order, then lane 0 adds the 64 partials in
+            // lane order
+            const int i = wv;
+            const float *x = buf + (size_t)i * D + lane * 4;
+            const float *ww = s_w + lane * 4;
             float z = 0.0f;
-            for (int64_t t = 0; t < D; t += 128) {
+#pragma unroll 4
+            for (int64_t t = 0; t < D; t += 256) {
                 const float4 xv = *reinterpret_cast<const float4 *>(x + t);
                 const float4 wq = *reinterpret_cast<const float4 *>(ww + t);
                 z = z + wq.x * xv.x;
@@ -1462,11 +1466,20 @@ __global__ __launch_bounds__(256) void k_dense_fused(DevDense dd, int64_t first,
                 z = z + wq.z * xv.z;
                 z = z + wq.w * xv.w;
             }
-            s_zp[i * 32 + qq] = z;
+            s_zp[i * 64 + lane] = z;
             wave_sync();
-            if (qq == 0 && r0 + i < i1) {
+            if (lane == 0 && r0 + i < i1) {
+                float4 pz[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) pz[u] = *reinterpret_cast<const float4 *>(s_zp + i * 64 + 4 * u);
                 float zz = 0.0f;
-                for (int u = 0; u < 32; ++u) zz = zz + s_zp[i * 32 + u];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    zz = zz + pz[u].x;
+                    zz = zz + pz[u].y;
+                    zz = zz + pz[u].z;
+                    zz = zz + pz[u].w;
+                }
                 s_r[i] = sigmoid_ref(zz) - s_lab[q * kFuseRows + i];
             }
         }
@@ -2035,7 +2048,7 @@ hipError_t launch_dense_fused(const DevDense &dd, int64_t first, int64_t B, cons
                               hipStream_t s) {
     if (B <= 0) return hipSuccess;
     if (!dense_fused_ok(dd.D)) return hipErrorInvalidValue;
-    const size_t lds = ((size_t)2 * kFuseRows * dd.D + dd.D + kFuseRows * 33 + kDenseChunk) * 4 +
+    const size_t lds = ((size_t)2 * kFuseRows * dd.D + dd.D + kFuseRows * 65 + kDenseChunk) * 4 +
                        (size_t)(kDenseChunk + kFuseRows) * 8 + 16;
     const dim3 g((unsigned)dense_chunks(B)), blk(256);
     switch (dd.D) {
