@@ -1912,11 +1912,16 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
     t.B = batch_size < 0 ? ds->n_rows : batch_size;
     t.plan = dlr::plan_batches(ds->n_rows, batch_size);
     const int64_t D = c->D;
+    // Gradient order: the reference's per-column sequential
+    // sums (seq) for small batches; for batch rows x D > 2^24 the fused
+    // one-pass kernel where D allows (C4), else the two-pass blocked sums.
+    // DLR_DENSE_GRAD=seq|blocked|fused forces one.
     const char *dg = getenv("DLR_DENSE_GRAD");
-    t.dfused = dg && strcmp(dg, "fused") == 0;
+    const bool big = t.B * D > ((int64_t)1 << 24);
+    t.dfused = dg ? strcmp(dg, "fused") == 0 : (big && dlr::dense_fused_ok(D));
     if (t.dfused && !dlr::dense_fused_ok(D))
         return fail(c, DLR_E_ARG, "dlr_load_train_dense: DLR_DENSE_GRAD=fused needs D in {512, 1024, 2048, 4096}");
-    t.dblocked = t.dfused || (dg ? strcmp(dg, "blocked") == 0 : (t.B * D > ((int64_t)1 << 24)));
+    t.dblocked = t.dfused || (dg ? strcmp(dg, "blocked") == 0 : big);
     // Residency: device-resident unless asked to stream, or (auto) the rows
     // would not leave room in HBM (20M x 4096 fp32 = 328 GB
     // on one 288 GB GPU).  Streamed rows are staged per batch over PCIe.

@@ -227,10 +227,13 @@ int dlr_load_train(dlr_ctx *ctx, const dlr_dataset *ds, int64_t batch_size, int6
 int dlr_load_test(dlr_ctx *ctx, const dlr_dataset *ds);
 /* The dense counterparts (K6: GEMV-shaped margin and gradient kernels,
  * HBM-bound, off MFMA).  The gradient is the reference's per-column
- * sequential sum when batch rows x D <= 2^24, else a blocked sum (per-column
- * sequential over 256-row chunks, chunk partials added in order:
- * deterministic, within the north-star tolerance); DLR_DENSE_GRAD=seq|blocked
- * forces one. */
+ * sequential sum when batch rows x D <= 2^24; above that, for D in {512,
+ * 1024, 2048, 4096} (C4), one FUSED pass over X (margin + per-256-row-chunk
+ * gradient partials from LDS, X read from HBM once; the margin summed in a
+ * fixed blocked order), else two passes with the blocked gradient
+ * (per-column sequential over 256-row chunks, chunk partials added in
+ * order).  Deterministic, within the north-star tolerance;
+ * DLR_DENSE_GRAD=seq|blocked|fused forces one. */
 int dlr_load_train_dense(dlr_ctx *ctx, const dlr_dense *ds, int64_t batch_size, int64_t *n_batches);
 int dlr_load_test_dense(dlr_ctx *ctx, const dlr_dense *ds);
 

@@ -80,7 +80,7 @@ def test_dense_blocked_gradient_within_bar(monkeypatch, W):
     assert_same_weights(eng2.w, eng.w)
 
 
-def test_c4_shape_dense_steps():
+def test_c4_shape_dense_steps(monkeypatch):
     # BASELINE C4: 4,096 dense features, B = 65,536 (blocked gradient by
     # default at this size); rows reduced to two batches.
     # At this size the reference's own sequential fp32 gradient is ~1.4e-5
@@ -89,6 +89,7 @@ def test_c4_shape_dense_steps():
     # a 1e-7 absolute floor.  The bar here: the engine's pushed gradient is at
     # least as close to the fp64-exact gradient as the reference's, and the
     # weights stay within 1e-5 relative + 1e-6 absolute of the reference.
+    monkeypatch.setenv("DLR_DENSE_GRAD", "blocked")  # the fused default: test_fused_dense_*
     D, B = 4096, 65536
     dd = dlr.DenseDataset.generate(2 * B, D, seed=10, stream=1)
     X, y = dd.arrays()
@@ -194,13 +195,14 @@ def test_residency_reporting():
         eng.close()
 
 
-def test_c4_blocked_gradient_full_epoch():
+def test_c4_blocked_gradient_full_epoch(monkeypatch):
     # the C4 blocked gradient over a FULL epoch at B = 65,536
     # (1M rows = 16 batches, the last one wrapping to row 0), against the
     # oracle's sequential sums step by step.  Bar: |a-b| <= 1e-5*|b| + 1e-6
     # (the 1e-6 absolute floor: see test_c4_shape_dense_steps -- the
     # reference's own fp32 gradient moves a weight ~3e-7 per step away from
     # exact arithmetic).  Prints the max relative difference of the epoch.
+    monkeypatch.setenv("DLR_DENSE_GRAD", "blocked")
     D, B, lr = 4096, 65536, 0.05
     dd = dlr.DenseDataset.generate(1_000_000, D, seed=10, stream=2)
     X, y = dd.arrays()
