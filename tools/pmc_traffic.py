@@ -12,6 +12,7 @@ calibrated by that stream; the raw counters are reported beside the
 corrected figure.
 
     python tools/pmc_traffic.py gpurun_out/pmc  [--out profiles/traffic.json]
+    python tools/pmc_traffic.py profiles/r02_pmc_c2      # the committed raw CSVs of profiles/traffic.json
     python tools/pmc_traffic.py gpurun_out/pmc_c3 --workload-key D16777216_nnz39_B-1 --layout classic \
         --out profiles/traffic_c3.json
 """
@@ -27,6 +28,10 @@ from collections import defaultdict
 
 
 def per_kernel(path: str, counter: str) -> dict[str, list[float]]:
+    # rocprofv3's layout (<pass>/run_counter_collection.csv) or the flat copy
+    # committed under profiles/ (<pass>.csv)
+    if not os.path.exists(path):
+        path = os.path.dirname(path) + ".csv"
     out: dict[str, list[float]] = defaultdict(list)
     with open(path) as f:
         for row in csv.DictReader(f):
