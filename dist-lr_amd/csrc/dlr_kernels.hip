@@ -1376,26 +1376,27 @@ __global__ __launch_bounds__(256) void k_dense_grad_blocked(DevDense dd, int64_t
 // in ONE pass over X.  The two-kernel path reads every batch row twice from
 // HBM (the gradient needs a row's residual, which exists only after the
 // whole row is summed); here workgroup k owns the same 256-row chunk as
-// k_dense_grad_blocked and streams it through LDS four rows at a time, so
-// each row is read from HBM once and used twice from LDS.  Staging: every
-// thread holds the next two sub-chunks in registers (16-byte loads, 64 KiB
-// per CU in flight) and writes one into the free LDS buffer per step
-// (register staging: the compiler's waits are per register, where LDS-DMA
-// pieces would make it drain every load before each LDS read).
-//   margin   wave i (row i of a 4-row sub-chunk): lane l sums the columns
-//            256t + 4l .. +3 for t = 0, 1, ... in order (LDS reads
+// k_dense_grad_blocked and streams it through LDS four rows (one
+// "sub-chunk") at a time, so each row is read from HBM once and used twice
+// from LDS.  Two wave roles, one sub-chunk apart, so the margin and the
+// gradient run side by side (one wave of each per SIMD):
+//   margin   waves 0-3, sub-chunk t: wave i takes row i; lane l sums the
+//            columns 256u + 4l .. +3, u = 0, 1, ..., in order (LDS reads
 //            conflict-free), then lane 0 adds the 64 partials in lane
 //            order: z is a fixed blocked order, not lr.cc:108-112's single
-//            chain (same tolerance regime as the blocked gradient);
-//   gradient all 256 threads: column quad g sums r_i * x_i in row order,
-//            continuing across the chunk's sub-chunks -- exactly
+//            chain (the same tolerance regime as the blocked gradient);
+//   gradient waves 4-7, sub-chunk t - 1: column quad g sums r_i * x_i in
+//            row order, continuing across the chunk's sub-chunks -- exactly
 //            k_dense_grad_blocked's per-chunk order -- into part[k].
-// k_dense_combine then adds the chunk partials and applies the update.
-// Needs D % 256 == 0 and D <= 4096.
+// Staging: every thread holds the next two sub-chunks in registers (16-byte
+// loads, 128 KiB per CU in flight) and writes one into the LDS buffer the
+// step has just freed (register staging: the compiler's waits are per
+// register, where LDS-DMA pieces make it drain every load before each LDS
+// read).  k_dense_combine then adds the chunk partials and applies the
+// update.  Instantiated for D = 512, 1,024, 2,048 and 4,096 (BASELINE C4).
 typedef float v4f __attribute__((ext_vector_type(4)));  // staging registers (SROA-friendly)
-constexpr int kFuseRows = 4;   // rows per sub-chunk: one wave's margin each
-constexpr int kFuseMaxD = 4096;
-constexpr int kFuseRegs = kFuseRows * kFuseMaxD / 4 / 256;  // float4 per thread per sub-chunk (max)
+constexpr int kFuseRows = 4;       // rows per sub-chunk: one margin wave each
+constexpr int kFuseThreads = 512;  // 4 margin + 4 gradient waves
 
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1404,30 +1405,30 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 template <int DQ>  // D / 4
-__global__ __launch_bounds__(256) void k_dense_fused(DevDense dd, int64_t first, int64_t B,
-                                                     const float *__restrict__ w, int64_t Dp,
-                                                     float *__restrict__ part) {
+__global__ __launch_bounds__(kFuseThreads) void k_dense_fused(DevDense dd, int64_t first, int64_t B,
+                                                              const float *__restrict__ w, int64_t Dp,
+                                                              float *__restrict__ part) {
     extern __shared__ __attribute__((aligned(16))) float fsm[];
     constexpr int64_t D = 4 * DQ;
-    constexpr int d4 = DQ;                               // float4 per row
-    float *s_x = fsm;                                    // 2 buffers x kFuseRows x D
-    float *s_w = fsm + (size_t)2 * kFuseRows * D;        // D
-    float *s_zp = s_w + D;                               // kFuseRows x 64 margin partials
-    float *s_r = s_zp + kFuseRows * 64;                  // kFuseRows residuals
-    float *s_lab = s_r + kFuseRows;                      // the chunk's labels (kDenseChunk)
+    constexpr int d4 = DQ;                                   // float4 per row
+    constexpr int nreg = kFuseRows * d4 / kFuseThreads;      // float4 per thread per sub-chunk
+    static_assert(nreg >= 1 && kFuseRows * d4 % kFuseThreads == 0, "D % 512 == 0");
+    float *s_x = fsm;                                        // 2 buffers x kFuseRows x D
+    float *s_w = fsm + (size_t)2 * kFuseRows * D;            // D
+    float *s_zp = s_w + D;                                   // kFuseRows x 64 margin partials
+    float *s_r = s_zp + kFuseRows * 64;                      // 2 x kFuseRows residuals
+    float *s_lab = s_r + 2 * kFuseRows;                      // the chunk's labels (kDenseChunk)
     int64_t *s_roff = reinterpret_cast<int64_t *>(s_lab + kDenseChunk);  // row offsets (kDenseChunk + kFuseRows)
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wv = tid / kWave;
+    const int gt = tid - 256;                                // gradient thread (waves 4-7)
     const int64_t k = blockIdx.x;
     const int64_t i0 = k * kDenseChunk, i1 = min(i0 + kDenseChunk, B);
     const int nsub = (int)((i1 - i0 + kFuseRows - 1) / kFuseRows);
-    constexpr int nreg = kFuseRows * d4 / 256;           // float4 per thread per sub-chunk
-    static_assert(nreg >= 1 && nreg <= kFuseRegs && kFuseRows * d4 % 256 == 0, "D % 512 == 0, D <= 4096");
-    // sub-chunk q's float4 f = p * 256 + tid (p < nreg) into registers RG;
-    // rows past the chunk end re-read its last row (never used)
-    // (sub-chunks past the last re-load the last one: never used, but every
-    // step issues the same loads, so the compiler's vmcnt waits stay exact)
+    // sub-chunk q's float4 f = p * kFuseThreads + tid into registers RG
+    // (past the last sub-chunk: the last one again, never used -- every step
+    // issues the same loads, so the compiler's vmcnt waits stay exact)
 #define DLR_FUSE_LOAD(q, RG)                                                                                   \
     {                                                                                                          \
         const int qc_ = min((q), nsub - 1);                                                                    \
@@ -1438,84 +1439,86 @@ __global__ __launch_bounds__(256) void k_dense_fused(DevDense dd, int64_t first,
     {                                                                                                          \
         float *sbuf_ = s_x + (size_t)((q) & 1) * kFuseRows * D;                                                \
         _Pragma("unroll") for (int p = 0; p < nreg; ++p)                                                       \
-            *reinterpret_cast<v4f *>(sbuf_ + (size_t)(p * 256 + tid) * 4) = RG[p];                             \
+            *reinterpret_cast<v4f *>(sbuf_ + (size_t)(p * kFuseThreads + tid) * 4) = RG[p];                    \
     }
-    // this thread's column quads: g = tid, tid + 256, ... (D / 4 quads)
+    // gradient threads: column quads g = gt, gt + 256, ...
     constexpr int kMaxQ = (d4 + 255) / 256;
-    const int nq = (d4 + 255 - tid) / 256;
+    const int nq = gt < 0 ? 0 : (d4 + 255 - gt) / 256;
     float4 acc[kMaxQ];
 #pragma unroll
     for (int u = 0; u < kMaxQ; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    auto compute = [&](int q) {
-        const float *buf = s_x + (size_t)(q & 1) * kFuseRows * D;
-        const int64_t r0 = i0 + (int64_t)q * kFuseRows;
-        {
-            // wave i: row i of the sub-chunk; lane l sums columns
-            // 256t + 4l .. +3 in order, then lane 0 adds the 64 partials in
-            // lane order
-            const int i = wv;
-            const float *x = buf + (size_t)i * D + lane * 4;
-            const float *ww = s_w + lane * 4;
-            float z = 0.0f;
+    // one step: margin of sub-chunk t (t < nsub) and gradient of t - 1 (t >= 1)
+    auto step = [&](int t) {
+        if (wv < kFuseRows) {
+            if (t < nsub) {
+                const float *buf = s_x + (size_t)(t & 1) * kFuseRows * D;
+                const int i = wv;
+                const float *x = buf + (size_t)i * D + lane * 4;
+                const float *ww = s_w + lane * 4;
+                float z = 0.0f;
 #pragma unroll 4
-            for (int64_t t = 0; t < D; t += 256) {
-                const float4 xv = *reinterpret_cast<const float4 *>(x + t);
-                const float4 wq = *reinterpret_cast<const float4 *>(ww + t);
-                z = z + wq.x * xv.x;
-                z = z + wq.y * xv.y;
-                z = z + wq.z * xv.z;
-                z = z + wq.w * xv.w;
-            }
-            s_zp[i * 64 + lane] = z;
-            wave_sync();
-            if (lane == 0 && r0 + i < i1) {
-                float4 pz[16];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) pz[u] = *reinterpret_cast<const float4 *>(s_zp + i * 64 + 4 * u);
-                float zz = 0.0f;
-#pragma unroll
-                for (int u = 0; u < 16; ++u) {
-                    zz = zz + pz[u].x;
-                    zz = zz + pz[u].y;
-                    zz = zz + pz[u].z;
-                    zz = zz + pz[u].w;
+                for (int64_t u = 0; u < D; u += 256) {
+                    const float4 xv = *reinterpret_cast<const float4 *>(x + u);
+                    const float4 wq = *reinterpret_cast<const float4 *>(ww + u);
+                    z = z + wq.x * xv.x;
+                    z = z + wq.y * xv.y;
+                    z = z + wq.z * xv.z;
+                    z = z + wq.w * xv.w;
                 }
-                s_r[i] = sigmoid_ref(zz) - s_lab[q * kFuseRows + i];
-            }
-        }
-        lds_barrier();
-        const int nr = (int)min<int64_t>(kFuseRows, i1 - r0);
-        for (int i = 0; i < nr; ++i) {
-            const float r = s_r[i];
-            const float *x = buf + (size_t)i * D;
+                s_zp[i * 64 + lane] = z;
+                wave_sync();
+                const int64_t row = i0 + (int64_t)t * kFuseRows + i;
+                if (lane == 0 && row < i1) {
+                    float4 pz[16];
 #pragma unroll
-            for (int u = 0; u < kMaxQ; ++u) {
-                if (u < nq) {
-                    const float4 xv = *reinterpret_cast<const float4 *>(x + (size_t)(tid + 256 * u) * 4);
-                    acc[u].x = acc[u].x + r * xv.x;
-                    acc[u].y = acc[u].y + r * xv.y;
-                    acc[u].z = acc[u].z + r * xv.z;
-                    acc[u].w = acc[u].w + r * xv.w;
+                    for (int u = 0; u < 16; ++u) pz[u] = *reinterpret_cast<const float4 *>(s_zp + i * 64 + 4 * u);
+                    float zz = 0.0f;
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) {
+                        zz = zz + pz[u].x;
+                        zz = zz + pz[u].y;
+                        zz = zz + pz[u].z;
+                        zz = zz + pz[u].w;
+                    }
+                    s_r[(t & 1) * kFuseRows + i] = sigmoid_ref(zz) - s_lab[t * kFuseRows + i];
+                }
+            }
+        } else if (t >= 1) {
+            const int q = t - 1;
+            const float *buf = s_x + (size_t)(q & 1) * kFuseRows * D;
+            const int nr = (int)min<int64_t>(kFuseRows, i1 - (i0 + (int64_t)q * kFuseRows));
+            for (int i = 0; i < nr; ++i) {
+                const float r = s_r[(q & 1) * kFuseRows + i];
+                const float *x = buf + (size_t)i * D;
+#pragma unroll
+                for (int u = 0; u < kMaxQ; ++u) {
+                    if (u < nq) {
+                        const float4 xv = *reinterpret_cast<const float4 *>(x + (size_t)(gt + 256 * u) * 4);
+                        acc[u].x = acc[u].x + r * xv.x;
+                        acc[u].y = acc[u].y + r * xv.y;
+                        acc[u].z = acc[u].z + r * xv.z;
+                        acc[u].w = acc[u].w + r * xv.w;
+                    }
                 }
             }
         }
     };
-    for (int64_t j = tid * 4; j < D; j += 1024) *reinterpret_cast<float4 *>(s_w + j) = *reinterpret_cast<const float4 *>(w + j);
-    if (i0 + tid < i1) s_lab[tid] = dd.label[wrap_row(first + i0 + tid, dd.N)];
+    for (int64_t j = tid * 4; j < D; j += 4 * kFuseThreads)
+        *reinterpret_cast<float4 *>(s_w + j) = *reinterpret_cast<const float4 *>(w + j);
+    if (tid < kDenseChunk && i0 + tid < i1) s_lab[tid] = dd.label[wrap_row(first + i0 + tid, dd.N)];
     // shard offset of each of the chunk's rows (NextBatch's wrap,
     // data_iter.h:49-52; rows past the chunk end repeat its last row), and
     // this thread's (row, column) of each staged float4
-    for (int ii = tid; ii < kDenseChunk + kFuseRows; ii += 256) {
+    for (int ii = tid; ii < kDenseChunk + kFuseRows; ii += kFuseThreads) {
         const int64_t r = min(i0 + ii, i1 - 1);
         s_roff[ii] = wrap_row(first + r, dd.N) * D;
     }
-    int fri[nreg];
-    int64_t fc[nreg];
+    int fri[nreg], fc[nreg];
 #pragma unroll
     for (int p = 0; p < nreg; ++p) {
-        const int f = p * 256 + tid;
+        const int f = p * kFuseThreads + tid;
         fri[p] = f / d4;
-        fc[p] = (int64_t)(f - fri[p] * d4) * 4;
+        fc[p] = (f - fri[p] * d4) * 4;
     }
     __syncthreads();
     v4f ra[nreg], rb[nreg];
@@ -1524,17 +1527,20 @@ __global__ __launch_bounds__(256) void k_dense_fused(DevDense dd, int64_t first,
     DLR_FUSE_STORE(0, ra)
     DLR_FUSE_LOAD(2, ra)
     __syncthreads();
-    // step q: compute sub-chunk q (buffer q & 1); store q + 1 (held in the
-    // other register set) into buffer (q + 1) & 1, refill that set with q + 3
-    for (int q = 0; q < nsub; q += 2) {
-        compute(q);
-        DLR_FUSE_STORE(q + 1, rb)  // buffer (q + 1) & 1 was last read in step q - 1
-        DLR_FUSE_LOAD(q + 3, rb)
+    // step t reads buffers t & 1 (margin) and (t - 1) & 1 (gradient); then
+    // sub-chunk t + 1 goes into buffer (t + 1) & 1 -- the gradient's, now
+    // free -- and its register set is refilled with t + 3
+    for (int t = 0; t <= nsub; t += 2) {
+        step(t);
         lds_barrier();
-        if (q + 1 < nsub) {  // uniform
-            compute(q + 1);
-            DLR_FUSE_STORE(q + 2, ra)
-            DLR_FUSE_LOAD(q + 4, ra)
+        DLR_FUSE_STORE(t + 1, rb)
+        DLR_FUSE_LOAD(t + 3, rb)
+        lds_barrier();
+        if (t + 1 <= nsub) {  // uniform
+            step(t + 1);
+            lds_barrier();
+            DLR_FUSE_STORE(t + 2, ra)
+            DLR_FUSE_LOAD(t + 4, ra)
             lds_barrier();
         }
     }
@@ -1542,7 +1548,7 @@ __global__ __launch_bounds__(256) void k_dense_fused(DevDense dd, int64_t first,
 #undef DLR_FUSE_STORE
 #pragma unroll
     for (int u = 0; u < kMaxQ; ++u)
-        if (u < nq) *reinterpret_cast<float4 *>(part + k * Dp + (int64_t)(tid + 256 * u) * 4) = acc[u];
+        if (u < nq) *reinterpret_cast<float4 *>(part + k * Dp + (int64_t)(gt + 256 * u) * 4) = acc[u];
 }
 
 // Chunk partials of 16 columns per workgroup: the 256 threads stage up to
@@ -2048,9 +2054,9 @@ hipError_t launch_dense_fused(const DevDense &dd, int64_t first, int64_t B, cons
                               hipStream_t s) {
     if (B <= 0) return hipSuccess;
     if (!dense_fused_ok(dd.D)) return hipErrorInvalidValue;
-    const size_t lds = ((size_t)2 * kFuseRows * dd.D + dd.D + kFuseRows * 65 + kDenseChunk) * 4 +
+    const size_t lds = ((size_t)2 * kFuseRows * dd.D + dd.D + kFuseRows * 66 + kDenseChunk) * 4 +
                        (size_t)(kDenseChunk + kFuseRows) * 8 + 16;
-    const dim3 g((unsigned)dense_chunks(B)), blk(256);
+    const dim3 g((unsigned)dense_chunks(B)), blk(kFuseThreads);
     switch (dd.D) {
         case 512: hipLaunchKernelGGL(k_dense_fused<128>, g, blk, lds, s, dd, first, B, w, dd.D, part); break;
         case 1024: hipLaunchKernelGGL(k_dense_fused<256>, g, blk, lds, s, dd, first, B, w, dd.D, part); break;
