@@ -137,6 +137,7 @@ struct TrainShard {
     // b's phases are lpdesc[b * lnph ..], its columns lcols/lcseg as above
     int64_t lnph = 0;
     dlr::PhaseDesc *lpdesc = nullptr;
+    int64_t lnpart = 0;
     uint32_t *lpptr = nullptr, *lpslot = nullptr, *lpws = nullptr;
     uint16_t *lprow = nullptr;
     float *lpval = nullptr;
@@ -786,11 +787,14 @@ void build_bands(const std::vector<uint32_t> &cptr, const std::vector<RowT> &cro
 // l's pieces, phase by phase, from cseg[l] -- so k_long_combine adds each
 // column's partials in row order.  Per phase an entry-balanced wave
 // schedule over the pieces (<= 64 pieces, ~kWin entries per wave).
-// DLR_LONG_PIECE overrides the piece size (1..1024; default 64)
+// DLR_LONG_PIECE overrides the piece size (1..1024; default 63: a wave's
+// pieces then start 63 floats apart in its LDS product slab, one bank
+// apart, where 64-entry pieces put every summing lane on the same bank --
+// C3 long phases 427 -> 333 us; tools/lp_ab.sh sweeps 31..127)
 int64_t long_piece() {
     const char *e = getenv("DLR_LONG_PIECE");
-    const int64_t v = e ? atoll(e) : 64;
-    return v >= 1 && v <= 1024 ? v : 64;
+    const int64_t v = e ? atoll(e) : 63;
+    return v >= 1 && v <= 1024 ? v : 63;
 }
 struct LPhaseBuild {
     std::vector<dlr::PhaseDesc> desc;
@@ -1217,7 +1221,7 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
     }
     const int64_t nl = t.any_long ? t.lcoff[bb + 1] - t.lcoff[bb] : 0;
     if (e == hipSuccess && nl > 0 && t.lnph > 0) {
-        dlr::DevLPhase lp{t.lpdesc + b * t.lnph, t.lpptr, t.lpslot, t.lpws, t.lprow, t.lpval, t.lnph};
+        dlr::DevLPhase lp{t.lpdesc + b * t.lnph, reinterpret_cast<const uint2 *>(t.lpptr), t.lpws, t.lprow, t.lpval, t.lnph, (uint32_t)t.lnpart};
         e = dlr::launch_long_phase(lp, t.lcols + t.lcoff[bb], t.lcseg + (t.lcoff[bb] + (int64_t)b), nl, c->resid,
                                    t.lpart, t.gacc, c->stream);
     } else if (e == hipSuccess && nl > 0) {
@@ -1705,14 +1709,24 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 if ((r = upload(c, &t.lcols, cols.data(), cols.size()))) return r;
                 if ((r = upload(c, &t.lcseg, ph.cseg.data(), ph.cseg.size()))) return r;
                 if ((r = upload(c, &t.lpdesc, ph.desc.data(), ph.desc.size()))) return r;
-                if ((r = upload(c, &t.lpptr, ph.ptr.data(), ph.ptr.size()))) return r;
-                if ((r = upload(c, &t.lpslot, ph.slot.data(), ph.slot.size()))) return r;
+                {  // (piece pointer, partial slot) pairs, one 8-byte load per piece
+                    std::vector<uint32_t> ps(ph.ptr.size() * 2);
+                    for (size_t q = 0; q < ph.ptr.size(); ++q) {
+                        ps[2 * q] = ph.ptr[q];
+                        ps[2 * q + 1] = ph.slot[q];
+                    }
+                    if ((r = upload(c, &t.lpptr, ps.data(), ps.size()))) return r;
+                }
                 if ((r = upload(c, &t.lpws, ph.ws.data(), ph.ws.size()))) return r;
-                if ((r = upload(c, &t.lprow, ph.row.data(), ph.row.size(), kPad))) return r;
-                if (!t.unit && (r = upload(c, &t.lpval, ph.val.data(), ph.val.size(), kPad))) return r;
-                if ((r = dev_alloc(c, (void **)&t.lpart, (size_t)std::max<int64_t>(1, ph.maxpart) * 4))) return r;
+                // a full window of padding: k_long_phase loads whole windows unclamped
+                if ((r = upload(c, &t.lprow, ph.row.data(), ph.row.size(), (size_t)dlr::kLPWinPad))) return r;
+                if (!t.unit && (r = upload(c, &t.lpval, ph.val.data(), ph.val.size(), (size_t)dlr::kLPWinPad)))
+                    return r;
+                if (ph.maxpart > (int64_t)UINT32_MAX - 64) return fail(c, DLR_E_ARG, "too many long-column pieces");
+                t.lnpart = ph.maxpart;
+                if ((r = dev_alloc(c, (void **)&t.lpart, (size_t)(ph.maxpart + 64) * 4))) return r;
                 lbytes = (int64_t)(cols.size() * 4 + ph.cseg.size() * 4 + ph.desc.size() * sizeof(dlr::PhaseDesc) +
-                                   (ph.ptr.size() * 2 + ph.ws.size()) * 4 + (ph.row.size() + kPad) * (t.unit ? 2 : 6) +
+                                   (ph.ptr.size() * 2 + ph.ws.size()) * 4 + (ph.row.size() + dlr::kLPWinPad) * (t.unit ? 2 : 6) +
                                    ph.maxpart * 4);
                 resid_need = std::max(resid_need, t.lnph * (int64_t)dlr::kLPhase);
                 return DLR_OK;

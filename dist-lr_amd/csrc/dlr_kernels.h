@@ -92,23 +92,24 @@ struct DevBand {
 // Long columns of one batch in ROW PHASES of kLPhase rows (band mode):
 // phase p's entries (phase-local rows, ascending per column) are cut into
 // PIECES of <= 64 consecutive entries of one column; piece s of the phase
-// spans [ptr[desc[p].ptr + s], ... + s + 1) of row/val offset by
-// desc[p].ent, and its partial goes to part[slot[desc[p].ptr + s]]; waves
+// spans [ps[desc[p].ptr + s].x, ps[... + s + 1].x) of row/val offset by
+// desc[p].ent, and its partial goes to part[ps[desc[p].ptr + s].y]; waves
 // take pieces [ws[desc[p].ws + t], ... + t + 1) (<= 64 pieces, ~one window
 // of entries).
 constexpr int kLPhase = 16384;  // rows per phase (64 KB of residuals in LDS)
 constexpr int kLPWaves = 16;    // waves per workgroup (one workgroup per phase)
+constexpr int kLPWinPad = 1024; // padding entries after the phase rows (one unclamped window)
 struct PhaseDesc {
     int64_t ptr, ent, ws, ntasks;
 };
 struct DevLPhase {
     const PhaseDesc *desc;
-    const uint32_t *ptr;
-    const uint32_t *slot;
+    const uint2 *ps;  // (entry pointer, partial slot) per piece
     const uint32_t *ws;
     const uint16_t *row;
     const float *val;
     int64_t nph;
+    uint32_t npart;  // partials; part[npart, npart + 64) is a write sink for idle lanes
 };
 
 // Dense rows (row-major N x D fp32) and 0/1 labels as floats.

@@ -1003,6 +1003,98 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad_band(DevBand bd, const R
 // every column sequential and bitwise).  Pieces keep every lane's serial
 // chain <= 64 adds: a hot column's ~2,000 entries per phase would
 // otherwise be one lane's chain while its wave's other lanes idle.
+// A wave's tasks are software-pipelined three deep: while it sums task i
+// (LDS work), the entry window of task i+1, the piece pointers of task i+2
+// and the task bounds of task i+3 are already in flight -- each a
+// dependent load of the one before, which the unpipelined loop waited for
+// in turn (three round trips per ~1,000-entry task).  Loads are
+// unconditional (clamped to the wave's last task), so the compiler's
+// in-order vmcnt accounting waits for exactly the stage it needs.  Same
+// sums in the same order as before.
+template <bool UNIT>
+struct LPWindow {
+    ushort4 iv[kWin / (kVec * kWave)];
+    float4 v[kWin / (kVec * kWave)];
+};
+// The window's loads are unclamped (the phase rows carry kLPWinPad entries
+// of padding) and its entries outside [e0, e1) are gathered and multiplied
+// like the others: their products land in slab slots no piece of this task
+// reads, and every row index is phase-local (< kLPhase), so the gathers stay
+// inside the staged residuals.
+template <bool UNIT>
+__device__ __forceinline__ void lp_load_window(LPWindow<UNIT> &w, uint32_t base, int lane,
+                                               const uint16_t *__restrict__ row, const float *__restrict__ val) {
+    constexpr int kT = kWin / (kVec * kWave);
+#pragma unroll
+    for (int t = 0; t < kT; ++t) {
+        const uint32_t e = base + t * (kVec * kWave) + lane * kVec;
+        w.iv[t] = load_stream(reinterpret_cast<const ushort4 *>(row + e));
+        if constexpr (UNIT)
+            w.v[t] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+        else
+            w.v[t] = load_stream(reinterpret_cast<const float4 *>(val + e));
+    }
+}
+// gathers (from the phase's LDS residuals), products, ordered piece sums of
+// the window [ws, ws + kWin)
+template <bool UNIT, int K>
+__device__ __forceinline__ void lp_window_sums(const LPWindow<UNIT> &w, uint32_t ws, const uint32_t (&a)[K],
+                                               const uint32_t (&b)[K], float (&acc)[K], int lane, const float *s_r,
+                                               float *lds) {
+    constexpr int kT = kWin / (kVec * kWave);
+    constexpr int kChunk = kVec * kWave;
+    float g[kT][kVec];
+#pragma unroll
+    for (int t = 0; t < kT; ++t) {
+        g[t][0] = s_r[w.iv[t].x];
+        g[t][1] = s_r[w.iv[t].y];
+        g[t][2] = s_r[w.iv[t].z];
+        g[t][3] = s_r[w.iv[t].w];
+    }
+#pragma unroll
+    for (int t = 0; t < kT; ++t) {
+        const int o = t * kChunk + lane * kVec;
+        float4 p;
+        if constexpr (UNIT) {  // fl32(r * 1.0f) == r
+            p = make_float4(g[t][0], g[t][1], g[t][2], g[t][3]);
+        } else {
+            p.x = g[t][0] * w.v[t].x;
+            p.y = g[t][1] * w.v[t].y;
+            p.z = g[t][2] * w.v[t].z;
+            p.w = g[t][3] * w.v[t].w;
+        }
+        *reinterpret_cast<float4 *>(lds + o) = p;
+    }
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t lo = a[k] > ws ? a[k] : ws;
+        const uint32_t hi = b[k] < ws + kWin ? b[k] : ws + kWin;
+        int o = (int)(lo - ws);
+        const int oe = hi > lo ? (int)(hi - ws) : o;
+        float sum = acc[k];
+        // a piece is <= 63 entries: 16 LDS reads in flight per wait, then 4,
+        // then 1 (the chain's adds stay in order)
+        for (; o + 16 <= oe; o += 16) {
+            float x[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) x[u] = lds[o + u];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) sum = sum + x[u];
+        }
+        for (; o + 4 <= oe; o += 4) {
+            const float x0 = lds[o], x1 = lds[o + 1], x2 = lds[o + 2], x3 = lds[o + 3];
+            sum = sum + x0;
+            sum = sum + x1;
+            sum = sum + x2;
+            sum = sum + x3;
+        }
+        for (; o < oe; ++o) sum = sum + lds[o];
+        acc[k] = sum;
+    }
+    wave_sync();
+}
+
 template <bool UNIT>
 __global__ __launch_bounds__(kLPWaves *kWave) void k_long_phase(DevLPhase lp, const float *__restrict__ resid,
                                                                 float *__restrict__ part) {
@@ -1021,30 +1113,95 @@ __global__ __launch_bounds__(kLPWaves *kWave) void k_long_phase(DevLPhase lp, co
     }
     __syncthreads();
     const PhaseDesc d = lp.desc[p];
-    const uint32_t *ptr = lp.ptr + d.ptr;
+    const uint2 *ps = lp.ps + d.ptr;
     const uint32_t *ws = lp.ws + d.ws;
     const uint16_t *row = lp.row + d.ent;
     const float *val = UNIT ? nullptr : lp.val + d.ent;
     constexpr int K = kBandPairsPerLane;  // pieces per lane: s0 + lane + 64k
-    for (int64_t t = wv; t < d.ntasks; t += kLPWaves) {  // wave-uniform
-        const int64_t s0 = ws[t], sl = ws[t + 1];
-        const int64_t e0 = ptr[s0], e1 = ptr[sl];
-        int64_t a[K], b[K];
-        float acc[K];
-        uint32_t slot[K];
+    const int nt = (int)d.ntasks;
+    const int mine = nt > wv ? (nt - wv + kLPWaves - 1) / kLPWaves : 0;  // this wave's tasks
+    if (mine == 0) return;                                                // wave-uniform
+    const int last = wv + (mine - 1) * kLPWaves;
+    auto task_of = [&](int i) { return i < mine ? wv + i * kLPWaves : last; };
+    // stage 0: task bounds (every lane loads both; uniform values)
+    auto load_bounds = [&](int i, uint32_t &w0, uint32_t &w1) {
+        const int t = task_of(i);
+        w0 = ws[t];
+        w1 = ws[t + 1];
+    };
+    // stage 1: piece pointers and slots; e1 = ptr[sl]
+    auto load_meta = [&](uint32_t s0, uint32_t sl, uint32_t (&a)[K], uint32_t (&b)[K], uint32_t (&slot)[K],
+                         uint32_t &e1) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const int64_t q = s0 + lane + (int64_t)k * kWave;
-            const bool valid = q < sl;
-            a[k] = valid ? (int64_t)ptr[q] : e1;
-            b[k] = valid ? (int64_t)ptr[q + 1] : e1;
-            slot[k] = valid ? lp.slot[d.ptr + q] : 0u;
-            acc[k] = 0.0f;
+            const uint32_t q = s0 + lane + k * kWave;
+            const uint32_t qc = q < sl ? q : sl;
+            const uint2 pa = ps[qc];  // used unconditionally: the load is not sunk under the select
+            a[k] = pa.x;
+            b[k] = ps[q < sl ? q + 1 : sl].x;
+            slot[k] = q < sl ? pa.y : lp.npart + lane;  // idle lanes store to the sink
         }
-        ordered_segments_dot<uint16_t, UNIT, K>(e0, e1, a, b, acc, lane, row, val, s_r, slab);
+        e1 = ps[sl].x;
+    };
+    uint32_t w0, w1;  // bounds of task i + 2 (in flight)
+    uint32_t s0c, slc, a[K], b[K], slot[K], e1v;            // task i
+    uint32_t s0n, sln, an[K], bn[K], slotn[K], e1n;         // task i + 1 (in flight)
+    LPWindow<UNIT> win;
+    // prologue
+    load_bounds(0, w0, w1);
+    s0c = __builtin_amdgcn_readfirstlane(w0);
+    slc = __builtin_amdgcn_readfirstlane(w1);
+    load_meta(s0c, slc, a, b, slot, e1v);
+    load_bounds(1, w0, w1);
+    uint32_t e0c = __builtin_amdgcn_readfirstlane(a[0]), e1c = __builtin_amdgcn_readfirstlane(e1v);
+    lp_load_window<UNIT>(win, e0c & ~uint32_t(kVec - 1), lane, row, val);
+    s0n = __builtin_amdgcn_readfirstlane(w0);
+    sln = __builtin_amdgcn_readfirstlane(w1);
+    load_meta(s0n, sln, an, bn, slotn, e1n);
+    load_bounds(2, w0, w1);
+    for (int i = 0; i < mine; ++i) {
+        // 1. task i + 1's bounds of entries -> its window
+        const uint32_t e0x = __builtin_amdgcn_readfirstlane(an[0]), e1x = __builtin_amdgcn_readfirstlane(e1n);
+        LPWindow<UNIT> wnext;
+        lp_load_window<UNIT>(wnext, e0x & ~uint32_t(kVec - 1), lane, row, val);
+        // 2. task i + 2's bounds -> its pointers; task i + 3's bounds
+        const uint32_t s0x = __builtin_amdgcn_readfirstlane(w0), slx = __builtin_amdgcn_readfirstlane(w1);
+        uint32_t ax[K], bx[K], slotx[K], e1y;
+        load_meta(s0x, slx, ax, bx, slotx, e1y);
+        load_bounds(i + 3, w0, w1);
+        // 3. task i
+        float acc[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-            if (s0 + lane + (int64_t)k * kWave < sl) part[slot[k]] = acc[k];
+        for (int k = 0; k < K; ++k) acc[k] = 0.0f;
+        const uint32_t base = e0c & ~uint32_t(kVec - 1);
+        lp_window_sums<UNIT, K>(win, base, a, b, acc, lane, s_r, slab);
+        for (uint32_t wst = base + kWin; wst < e1c; wst += kWin) {  // rare: a task past one window
+            LPWindow<UNIT> wx;
+            lp_load_window<UNIT>(wx, wst, lane, row, val);
+            lp_window_sums<UNIT, K>(wx, wst, a, b, acc, lane, s_r, slab);
+        }
+        // unconditional stores (idle lanes into the sink): a fixed count of
+        // stores keeps the next waits exact (vmcnt counts stores on gfx9)
+#pragma unroll
+        for (int k = 0; k < K; ++k) part[slot[k]] = acc[k];
+        // rotate
+        s0c = s0n;
+        slc = sln;
+        e0c = e0x;
+        e1c = e1x;
+        win = wnext;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            a[k] = an[k];
+            b[k] = bn[k];
+            slot[k] = slotn[k];
+            an[k] = ax[k];
+            bn[k] = bx[k];
+            slotn[k] = slotx[k];
+        }
+        s0n = s0x;
+        sln = slx;
+        e1n = e1y;
     }
 }
 
