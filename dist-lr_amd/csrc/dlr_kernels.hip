@@ -1590,7 +1590,8 @@ __global__ __launch_bounds__(kFuseThreads) void k_dense_fused(DevDense dd, int64
     {                                                                                                          \
         const int qc_ = min((q), nsub - 1);                                                                    \
         _Pragma("unroll") for (int p = 0; p < nreg; ++p)                                                       \
-            RG[p] = *reinterpret_cast<const v4f *>(dd.X + s_roff[qc_ * kFuseRows + fri[p]] + fc[p]);           \
+            RG[p] = __builtin_nontemporal_load(                                                                \
+                reinterpret_cast<const v4f *>(dd.X + s_roff[qc_ * kFuseRows + fri[p]] + fc[p]));                \
     }
 #define DLR_FUSE_STORE(q, RG)                                                                                  \
     {                                                                                                          \
