@@ -132,13 +132,15 @@ def grad_dense(X, y, rows, w, C_: float = 1.0) -> np.ndarray:
     return g
 
 
-def grad_csr(csr, y, rows, w, C_: float = 1.0) -> np.ndarray:
+def grad_csr(csr, y, rows, w, C_: float = 1.0, return_resid: bool = False):
+    """lr.cc:34-41 for one batch; with return_resid also the residuals
+    sigma(z_s) - y_s per batch position s (lr.cc:36-37)."""
     rp, col, val = csr
     D = len(w)
     g = np.zeros(D, dtype=np.float32)
     scratch = np.zeros(len(rows), dtype=np.float32)
     _lib.orc_grad_csr(_p(rp), _p(col), _p(val), _p(y), D, _p(rows), len(rows), _p(w), C_, _p(g), _p(scratch))
-    return g
+    return (g, scratch) if return_resid else g
 
 
 def server_update(w: np.ndarray, grads: Sequence[np.ndarray], lr: float, mode: int = MODE_MEAN) -> None:

@@ -192,3 +192,73 @@ def test_banded_forced_collectives(classic, monkeypatch):
     res = run_engine([ds], 123, meta["num_iteration"], meta["batch_size"], meta["learning_rate"],
                      mode=meta["mode"])
     assert res.w.astype("<f4").tobytes().hex() == meta["w"]
+
+
+def _long_phase_order(prods_by_col, piece, Bn, w, C_=1.0, phase=16384):
+    """The documented long-column order in band mode (dlr_kernels.hip
+    k_long_phase + k_long_combine): per column, its products in
+    batch-row order cut at 16,384-row phase boundaries, each phase's run cut
+    into pieces of `piece` entries summed sequentially in fp32 from +0; the
+    piece partials (phase by phase) added by 64 lanes -- lane l takes partials
+    l, l + 64, ... in order -- and the lane sums by the xor-butterfly tree
+    (off 32, 16, ..., 1; lane 0's value); then lr.cc:40."""
+    out = {}
+    f32 = np.float32
+    for j, (pos, prod) in prods_by_col.items():
+        parts = []
+        ph = pos // phase
+        for p in np.unique(ph):
+            run = prod[ph == p]
+            for o in range(0, len(run), piece):
+                parts.append(np.cumsum(run[o:o + piece], dtype=f32)[-1])
+        parts = np.asarray(parts, dtype=f32)
+        v = np.zeros(64, dtype=f32)
+        for l in range(64):
+            if len(parts[l::64]):
+                v[l] = np.cumsum(parts[l::64], dtype=f32)[-1]
+        for off in (32, 16, 8, 4, 2, 1):
+            v = (v + v[np.arange(64) ^ off]).astype(f32)
+        G = v[0]
+        l2 = f32(f32(f32(C_) * w[j]) / f32(Bn))
+        out[j] = f32(np.float64(G) / np.float64(Bn) + np.float64(l2))
+    return out
+
+
+@pytest.mark.parametrize("piece", [63, 64, 7, 1024])
+def test_long_phase_order_bitwise(monkeypatch, piece):
+    # pins k_long_phase / k_long_combine to their documented summation order
+    # bit for bit (a restatement in numpy on the oracle's residuals), across
+    # piece sizes: 63 (default), 64, short pieces (7: many pieces per lane)
+    # and 1,024-entry pieces (tasks whose entries span two windows)
+    monkeypatch.setenv("DLR_BAND_ROWS", "8192")
+    monkeypatch.setenv("DLR_LONG_PIECE", str(piece))
+    D = 1 << 24
+    ds = _c3_shards(1, rows=60_000)[0]
+    rp, col, val, lab = ds.csr()
+    N = len(lab)
+    counts = np.bincount(col, minlength=D)
+    long_cols = np.flatnonzero(counts > 4096)
+    assert len(long_cols) >= 30
+    w0 = dlr.init_weight(D)
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(w0)
+        eng.load_train(ds, -1)
+        assert eng.train_band_rows() == 8192
+        got = eng.worker_gradient(0, 1.0)
+    finally:
+        eng.close()
+    rows = oracle.batch_rows(N, -1, 0)
+    g_orc, resid = oracle.grad_csr((rp, col, val), lab, rows, w0, return_resid=True)
+    row_of = np.repeat(np.arange(N), np.diff(rp))
+    prods = {}
+    for j in long_cols:
+        k = np.flatnonzero(col == j)                 # entries of column j, rows ascending
+        pos = row_of[k]
+        prods[j] = (pos, (resid[pos] * val[k]).astype(np.float32))
+    want = _long_phase_order(prods, piece, N, w0)
+    bad = [j for j in long_cols if np.float32(got[j]).tobytes() != want[j].tobytes()]
+    assert not bad, f"{len(bad)} long columns off the documented order, e.g. {bad[:3]}"
+    # and the short columns stay the reference's sequential sums
+    short = counts <= 4096
+    assert_same_weights(got[short], g_orc[short], "short-column gradient")
