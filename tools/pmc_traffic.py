@@ -80,8 +80,13 @@ def main() -> int:
     # the number of steps (= margin dispatches: bench.py runs the margin and
     # the gradient stage equally often).  C2 has one kernel per stage; C3's
     # gradient is 12 band launches + long phases + combine + finalize.
-    roles = [("margin", ["k_margin"]), ("grad", ["k_grad", "k_long_", "k_band_finalize"])]
-    steps = len(pick(bf, "k_margin")) or 1
+    # Dense shards (C4): the fused pass is the margin role (it also forms the
+    # gradient partials), the chunk combine + update the grad role.  Huge D
+    # (C5): the dense L2 pass and the scatter are the update role.
+    roles = [("margin", ["k_margin", "k_dense_fused", "k_dense_margin"]),
+             ("grad", ["k_grad", "k_long_", "k_band_finalize", "k_dense_grad", "k_dense_combine"]),
+             ("update", ["k_dense_l2", "k_scatter", "k_merge_update", "k_sparse_merge"])]
+    steps = len([x for k in roles[0][1] for x in pick(bf, k)]) or 1
     total = 0.0
     for short, keys in roles:
         f = [x for k in keys for x in pick(bf, k)]
