@@ -1,0 +1,37 @@
+"""The committed PMC traffic figures (profiles/traffic*.json, which bench.py
+reports as roofline.traffic) must be reproducible from the committed raw
+rocprofv3 counter CSVs (profiles/r02_pmc_<config>/) with tools/pmc_traffic.py
+-- no figure in the bench line without its raw data."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CASES = [
+    ("traffic.json", "r02_pmc_c2", "D1000000_nnz50_B65536", "lds"),
+    ("traffic_c3.json", "r02_pmc_c3", "D16777216_nnz39_B-1", "classic"),
+    ("traffic_c4.json", "r02_pmc_c4", "D4096_nnz4096_B65536", "dense"),
+    ("traffic_c5.json", "r02_pmc_c5", "D268435456_nnz10_B1024", "touched"),
+]
+
+
+@pytest.mark.parametrize("name,raw,key,layout", CASES)
+def test_traffic_reproducible_from_raw_counters(name, raw, key, layout):
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"),
+                          os.path.join(ROOT, "profiles", raw), "--workload-key", key, "--layout", layout],
+                         check=True, capture_output=True, text=True).stdout
+    got = json.loads(out)
+    with open(os.path.join(ROOT, "profiles", name)) as f:
+        want = json.load(f)
+    assert got["workload_key"] == want["workload_key"] == key
+    assert got["hbm_bytes_per_step"] == want["hbm_bytes_per_step"]
+    assert got["hbm_bytes_per_step"] > 0
+    # the read correction is the measured gfx950 factor (~2: FETCH_SIZE counts
+    # half of a wide streaming read), not an assumed constant
+    assert 1.8 < got["calibration"]["read_factor"] < 2.2
