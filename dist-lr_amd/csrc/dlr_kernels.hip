@@ -1539,9 +1539,10 @@ __global__ __launch_bounds__(256) void k_dense_grad_blocked(DevDense dd, int64_t
 // gradient run side by side (one wave of each per SIMD):
 //   margin   waves 0-3, sub-chunk t: wave i takes row i; lane l sums the
 //            columns 256u + 4l .. +3, u = 0, 1, ..., in order (LDS reads
-//            conflict-free), then lane 0 adds the 64 partials in lane
-//            order: z is a fixed blocked order, not lr.cc:108-112's single
-//            chain (the same tolerance regime as the blocked gradient);
+//            conflict-free), then the 64 lane partials combine by the
+//            xor-butterfly tree: z is a fixed blocked order, not
+//            lr.cc:108-112's single chain (the same tolerance regime as the
+//            blocked gradient);
 //   gradient waves 4-7, sub-chunk t - 1: column quad g sums r_i * x_i in
 //            row order, continuing across the chunk's sub-chunks -- exactly
 //            k_dense_grad_blocked's per-chunk order -- into part[k].
@@ -1623,23 +1624,13 @@ __global__ __launch_bounds__(kFuseThreads) void k_dense_fused(DevDense dd, int64
                     z = z + wq.z * xv.z;
                     z = z + wq.w * xv.w;
                 }
-                s_zp[i * 64 + lane] = z;
-                wave_sync();
+                // the 64 lane partials by the xor-butterfly tree (every
+                // lane ends with the same z): off the serial lane-0 chain
+                // that every step's closing barrier waited for
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) z = z + __shfl_xor(z, off);
                 const int64_t row = i0 + (int64_t)t * kFuseRows + i;
-                if (lane == 0 && row < i1) {
-                    float4 pz[16];
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) pz[u] = *reinterpret_cast<const float4 *>(s_zp + i * 64 + 4 * u);
-                    float zz = 0.0f;
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) {
-                        zz = zz + pz[u].x;
-                        zz = zz + pz[u].y;
-                        zz = zz + pz[u].z;
-                        zz = zz + pz[u].w;
-                    }
-                    s_r[(t & 1) * kFuseRows + i] = sigmoid_ref(zz) - s_lab[t * kFuseRows + i];
-                }
+                if (lane == 0 && row < i1) s_r[(t & 1) * kFuseRows + i] = sigmoid_ref(z) - s_lab[t * kFuseRows + i];
             }
         } else if (t >= 1) {
             const int q = t - 1;
