@@ -272,3 +272,64 @@ def test_fused_dense_c4_epoch_and_streamed(monkeypatch):
         oracle.server_update(w, [g], lr)
     a, bb = res["device"].astype(np.float64), w.astype(np.float64)
     assert np.all(np.abs(a - bb) <= 1e-5 * np.abs(bb) + 1e-6)
+
+
+def _glibc_exp():
+    import ctypes
+    libm = ctypes.CDLL("libm.so.6")
+    libm.exp.restype = ctypes.c_double
+    libm.exp.argtypes = [ctypes.c_double]
+    return libm.exp
+
+
+def _fused_order_gradient(X, y, rows, w, C_=1.0, chunk=256):
+    """The documented order of k_dense_fused + k_dense_combine (DESIGN.md §3
+    item 3): row i's margin = 64 lane partials -- lane l sums columns
+    256u + 4l .. 4l + 3 (u ascending) in order, fl32 products, from +0 --
+    combined by the xor-butterfly tree (off 32 .. 1); r_i = fl32(sigma) - y_i
+    (lr.cc:113, glibc exp); per 256-row chunk, G_k[j] = rows in order from
+    +0; G[j] = chunks in order from +0; then lr.cc:40."""
+    f32 = np.float32
+    Xb = X[rows].astype(f32)
+    Bn, D = Xb.shape
+    parts = np.zeros((64, Bn), dtype=f32)
+    for l in range(64):
+        for u in range(D // 256):
+            for c in range(4):
+                j = 256 * u + 4 * l + c
+                parts[l] = parts[l] + (w[j] * Xb[:, j]).astype(f32)
+    v = parts
+    for off in (32, 16, 8, 4, 2, 1):
+        v = (v + v[np.arange(64) ^ off]).astype(f32)
+    z = v[0]
+    ex = _glibc_exp()
+    sig = np.array([f32(1.0 / (1.0 + ex(-float(zi)))) for zi in z], dtype=f32)
+    r = (sig - y[rows].astype(f32)).astype(f32)
+    G = np.zeros(D, dtype=f32)
+    for k0 in range(0, Bn, chunk):
+        part = np.zeros(D, dtype=f32)
+        for i in range(k0, min(k0 + chunk, Bn)):
+            part = part + (r[i] * Xb[i]).astype(f32)
+        G = (G + part).astype(f32)
+    l2 = (f32(C_) * w).astype(f32) / f32(Bn)
+    return (G.astype(np.float64) / np.float64(Bn) + l2.astype(f32).astype(np.float64)).astype(f32)
+
+
+@pytest.mark.parametrize("D,B,N", [(512, 600, 1000), (4096, 300, 500)])
+def test_fused_dense_order_bitwise(monkeypatch, D, B, N):
+    # pins the fused pass to its documented (non-reference) order bit for
+    # bit: the pushed gradient of batch 1 (wrapping when B does not divide
+    # N) against a numpy restatement; ragged last chunk (600 = 2 x 256 + 88)
+    monkeypatch.setenv("DLR_DENSE_GRAD", "fused")
+    dd = dlr.DenseDataset.generate(N, D, seed=17, stream=1)
+    X, y = dd.arrays()
+    w0 = dlr.init_weight(D)
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(w0)
+        eng.load_train_dense(dd, B)
+        got = eng.worker_gradient(1, 1.0)
+    finally:
+        eng.close()
+    want = _fused_order_gradient(X, y, oracle.batch_rows(N, B, 1), w0)
+    assert_same_weights(got, want, "fused pushed gradient")
