@@ -356,145 +356,6 @@ __global__ __launch_bounds__(NW *kWave) void k_margin_hot(DevBatch bt, const flo
     }
 }
 
-// ordered_segment_dot for a unit-valued, frequency-ordered shard with the
-// HOT hottest weights in LDS (`hot`), COMPACTING the cold gathers: per
-// window, hot products are read from LDS straight into the product slab;
-// each cold entry parks its column id (bits) in its slab slot and its slot
-// number in this wave's list (ballot + mbcnt), then the wave gathers only
-// the list -- ceil(cold / 64) rounds of global loads, every lane busy --
-// and writes each weight over its column id.  The plain HOT variant makes
-// every lane issue a global load per entry (hot ones clamped to w[0]):
-// 16 load instructions per window where ~7 carry cold entries (C3: 58% of
-// the entries are hot).  Column ids >= nt_from are gathered non-temporally
-// (the coldest tail -- read once -- leaves L2 to the warmer tier).  Same
-// products, same in-order sums: bitwise the other margins.
-template <int HOT>
-__device__ __forceinline__ float ordered_segment_dot_compact(int64_t e0, int64_t e1, int64_t a, int64_t b, int lane,
-                                                             const int32_t *__restrict__ idx,
-                                                             const float *__restrict__ table, float *lds,
-                                                             uint16_t *list, const float *hot, unsigned nt_from) {
-    constexpr int kT = kWin / (kVec * kWave);
-    constexpr int kChunk = kVec * kWave;
-    const int64_t base = e0 & ~int64_t(kVec - 1);
-    float acc = 0.0f;
-    unsigned *ldsu = reinterpret_cast<unsigned *>(lds);
-    for (int64_t ws = base; ws < e1; ws += kWin) {
-        const int64_t left = e1 - ws;  // wave-uniform
-        int4 iv[kT];
-#pragma unroll
-        for (int t = 0; t < kT; ++t) {
-            if (t * kChunk < left) {
-                const int64_t e = ws + t * kChunk + lane * kVec;
-                const int64_t ec = e < e1 ? e : ws + t * kChunk;
-                iv[t] = load_stream(reinterpret_cast<const int4 *>(idx + ec));
-            }
-        }
-        // (2a) hot products from LDS; cold slots get their column id and a
-        // list entry.  Slots outside [e0, e1) are never summed: left as is.
-        unsigned ncold = 0;  // wave-uniform
-#pragma unroll
-        for (int t = 0; t < kT; ++t) {
-            if (t * kChunk < left) {
-                const int o = t * kChunk + lane * kVec;
-                const int64_t e = ws + o;
-                const unsigned ii[4] = {(unsigned)iv[t].x, (unsigned)iv[t].y, (unsigned)iv[t].z, (unsigned)iv[t].w};
-                float q[4];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const bool valid = e + c >= e0 && e + c < e1;
-                    const bool cold = valid && ii[c] >= (unsigned)HOT;
-                    const float h = hot[ii[c] < (unsigned)HOT ? ii[c] : 0u];
-                    q[c] = cold ? __uint_as_float(ii[c]) : h;
-                    const unsigned long long m = __builtin_amdgcn_ballot_w64(cold);
-                    const unsigned before =
-                        __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-                    if (cold) list[ncold + before] = (uint16_t)(o + c);
-                    ncold += (unsigned)__popcll(m);
-                }
-                *reinterpret_cast<float4 *>(lds + o) = make_float4(q[0], q[1], q[2], q[3]);
-            }
-        }
-        wave_sync();
-        // (2b) the cold gathers, 8 rounds of loads in flight at a time
-        for (unsigned r0 = 0; r0 < ncold; r0 += 8 * kWave) {
-            unsigned pos[8], col[8];
-            float g[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const unsigned k = r0 + u * kWave + lane;
-                pos[u] = k < ncold ? (unsigned)list[k] : 0xFFFFu;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) col[u] = pos[u] != 0xFFFFu ? ldsu[pos[u]] : 0u;
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                if (pos[u] != 0xFFFFu) {
-                    if (col[u] >= nt_from)
-                        g[u] = __builtin_nontemporal_load(table + col[u]);
-                    else
-                        g[u] = table[col[u]];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (pos[u] != 0xFFFFu) lds[pos[u]] = g[u];
-        }
-        wave_sync();
-        // (3) this lane's row, in order (rows are short: < 64 entries)
-        const int64_t lo = a > ws ? a : ws;
-        const int64_t hi = b < ws + kWin ? b : ws + kWin;
-        int o = (int)(lo - ws);
-        const int oe = (int)(hi - ws);
-        for (; o + 8 <= oe; o += 8) {
-            const float x0 = lds[o], x1 = lds[o + 1], x2 = lds[o + 2], x3 = lds[o + 3];
-            const float x4 = lds[o + 4], x5 = lds[o + 5], x6 = lds[o + 6], x7 = lds[o + 7];
-            acc = acc + x0;
-            acc = acc + x1;
-            acc = acc + x2;
-            acc = acc + x3;
-            acc = acc + x4;
-            acc = acc + x5;
-            acc = acc + x6;
-            acc = acc + x7;
-        }
-        for (; o < oe; ++o) acc = acc + lds[o];
-        wave_sync();
-    }
-    return acc;
-}
-
-// k_margin_hot for unit-valued shards with the cold gathers compacted
-// (ordered_segment_dot_compact).  LDS: HOT weights + per wave a kWin
-// product slab and a kWin list of slot numbers.
-template <int HOT, int NW, int SEG>
-__global__ __launch_bounds__(NW *kWave) void k_margin_hot_compact(DevBatch bt, const float *__restrict__ w,
-                                                                  float *__restrict__ resid, unsigned nt_from) {
-    __shared__ __attribute__((aligned(16))) float s_w[HOT];
-    __shared__ __attribute__((aligned(16))) float s_p[NW][kWin];
-    __shared__ uint16_t s_l[NW][kWin];
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wv = threadIdx.x / kWave;
-    {
-        const float4 *src = reinterpret_cast<const float4 *>(w);
-        float4 *dst = reinterpret_cast<float4 *>(s_w);
-#pragma unroll
-        for (int k = 0; k < HOT / 4 / (NW * kWave); ++k) dst[k * NW * kWave + threadIdx.x] = src[k * NW * kWave + threadIdx.x];
-    }
-    __syncthreads();
-    const int64_t nblk = (bt.rows + NW * SEG - 1) / (NW * SEG);
-    for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-        const int64_t row0 = (blk * NW + wv) * SEG;
-        if (row0 >= bt.rows) continue;  // wave-uniform (no barrier in the loop)
-        const int64_t my = row0 + lane;
-        const bool valid = lane < SEG && my < bt.rows;
-        const float y = valid ? bt.label[my] : 0.0f;
-        const int64_t rlast = min(row0 + SEG, bt.rows);
-        const int64_t e0 = bt.row_ptr[row0], e1 = bt.row_ptr[rlast];
-        const int64_t a = valid ? bt.row_ptr[my] : e1, b = valid ? bt.row_ptr[my + 1] : e1;
-        const float z = ordered_segment_dot_compact<HOT>(e0, e1, a, b, lane, bt.col, w, s_p[wv], s_l[wv], s_w, nt_from);
-        if (valid) resid[my] = sigmoid_ref(z) - y;
-    }
-}
 
 __device__ __forceinline__ double softplus(double t) { return t > 0 ? t + log1p(exp(-t)) : log1p(exp(t)); }
 
@@ -1909,36 +1770,8 @@ hipError_t launch_margin_hot(const DevBatch &bt, const float *w, int64_t D, floa
         const char *e = getenv("DLR_MARGIN_HOT_SHAPE");
         return e ? atoi(e) : 0;
     }();
-    // DLR_MARGIN_COMPACT=1 (A/B only): the compacted-cold-gather variant for
-    // unit-valued shards (C3: margin 1.90 ms against 1.76 ms for the plain
-    // hot margin, profiles/r02_c3_margin_ab.txt); DLR_MARGIN_NT=<id> there:
-    // columns >= id gathered non-temporally (2^19 / 2^20 / 2^21: no change).
-    static const bool compact = [] {
-        const char *e = getenv("DLR_MARGIN_COMPACT");
-        return e && atoi(e) != 0;
-    }();
-    static const unsigned nt_from = [] {
-        const char *e = getenv("DLR_MARGIN_NT");
-        return e ? (unsigned)strtoul(e, nullptr, 0) : 0xFFFFFFFFu;
-    }();
-    if (compact && shape == 0 && D >= 16384 && bt.val == nullptr) {
-        const unsigned cap = (unsigned)ncu;
-#define DLR_MHC(SEG)                                                                                            \
-    case SEG:                                                                                                   \
-        hipLaunchKernelGGL((k_margin_hot_compact<16384, 16, SEG>),                                              \
-                           dim3(std::min<unsigned>(grid_for(bt.rows, 16 * SEG), cap)), dim3(16 * kWave), 0, s, bt, \
-                           w, resid, nt_from);                                                                  \
-        break;
-        switch (margin_seg(bt)) {
-            DLR_MHC(16)
-            DLR_MHC(32)
-            DLR_MHC(64)
-            default:
-                return hipErrorInvalidValue;
-        }
-#undef DLR_MHC
-        return hipGetLastError();
-    }
+    // (a compacted-cold-gather variant -- ballot + list of the cold entries
+    // -- measured slower: 1.90 vs 1.76 ms, profiles/r02_c3_margin_ab.txt)
     if (shape == 0 && D >= 16384) return launch_mh<16384, 16>(bt, w, resid, (unsigned)ncu, s);
     if (shape == 2 && D >= 16384) return launch_mh<16384, 8>(bt, w, resid, (unsigned)ncu, s);
     if (shape == 3 && D >= 24576) return launch_mh<24576, 8>(bt, w, resid, (unsigned)ncu, s);
