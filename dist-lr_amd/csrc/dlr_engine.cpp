@@ -109,6 +109,13 @@ struct TrainShard {
     // streamed sparse shard: every per-batch array (StreamArr)
     bool sparse_stream = false;
     std::vector<StreamArr> sarr;
+    // coalesced staging of a streamed sparse shard: batch b's slices of
+    // every streamed array packed back to back (256-B aligned) in one
+    // page-locked buffer at sboff[b] (sbsz[b] bytes), array a of batch b at
+    // soff[b * sarr.size() + a] -- one H2D copy per batch into sslot[0|1]
+    char *shost = nullptr;
+    std::vector<size_t> sboff, sbsz, soff;
+    void *sslot[2] = {nullptr, nullptr};
     bool row16 = false;
     uint32_t *cptr = nullptr;   // n_batches x (D+1)
     void *crow = nullptr;
@@ -287,6 +294,9 @@ void free_train(dlr_ctx *c) {
             dev_free(c, a.slot[1]);
             *a.field = nullptr;  // the bound view pointed into a slot
         }
+        if (t.shost) (void)hipHostFree(t.shost);
+        dev_free(c, t.sslot[0]);
+        dev_free(c, t.sslot[1]);
     }
     if (t.streamed) {
         if (c->cstream) (void)hipStreamSynchronize(c->cstream);
@@ -897,6 +907,63 @@ void for_batches(int64_t nb, int nthreads, Fn fn) {
     for (auto &x : th) x.join();
 }
 
+// After every streamed array is placed: pack each batch's slices of all of
+// them into one page-locked buffer (batch-major), so staging a batch is ONE
+// H2D copy ("coalesced CSR upload of each minibatch"), and replace the
+// per-array host copies and device slots by two batch-sized slots.
+int coalesce_stream(dlr_ctx *c, int nthreads) {
+    TrainShard &t = c->train;
+    static const bool on = [] {  // DLR_STREAM_COALESCE=0: one copy per array and batch (A/B)
+        const char *e = getenv("DLR_STREAM_COALESCE");
+        return !(e && strcmp(e, "0") == 0);
+    }();
+    if (!on) return DLR_OK;
+    const size_t nb = t.plan.size(), na = t.sarr.size();
+    t.soff.assign(nb * na, 0);
+    t.sbsz.assign(nb, 0);
+    t.sboff.assign(nb + 1, 0);
+    size_t maxs = 256;
+    for (size_t b = 0; b < nb; ++b) {
+        size_t o = 0;
+        for (size_t k = 0; k < na; ++k) {
+            const StreamArr &a = t.sarr[k];
+            o = (o + 255) & ~(size_t)255;
+            t.soff[b * na + k] = o;
+            if (a.end[b] > a.beg[b]) o += ((size_t)(a.end[b] - a.beg[b]) + a.pad) * a.es;
+        }
+        t.sbsz[b] = o;
+        t.sboff[b + 1] = t.sboff[b] + ((o + 255) & ~(size_t)255);
+        maxs = std::max(maxs, o);
+    }
+    HIPC(c, hipHostMalloc((void **)&t.shost, std::max<size_t>(t.sboff[nb], 256), hipHostMallocDefault));
+    for_batches((int64_t)nb, nthreads, [&](int64_t b) {
+        for (size_t k = 0; k < na; ++k) {
+            const StreamArr &a = t.sarr[k];
+            if (a.end[(size_t)b] <= a.beg[(size_t)b]) continue;
+            memcpy(t.shost + t.sboff[(size_t)b] + t.soff[(size_t)b * na + k], a.host + (size_t)a.beg[(size_t)b] * a.es,
+                   ((size_t)(a.end[(size_t)b] - a.beg[(size_t)b]) + a.pad) * a.es);
+        }
+    });
+    for (StreamArr &a : t.sarr) {  // the array-major copies and slots are no longer needed
+        if (a.registered) (void)hipHostUnregister(const_cast<char *>(a.host));
+        a.registered = false;
+        a.keep.reset();
+        a.host = nullptr;
+        for (int k = 0; k < 2; ++k) {
+            t.bytes -= (int64_t)(a.cap * a.es);
+            dev_free(c, a.slot[k]);
+            a.slot[k] = nullptr;
+        }
+    }
+    for (int k = 0; k < 2; ++k) {
+        const int rc = dev_alloc(c, &t.sslot[k], maxs);
+        if (rc) return rc;
+    }
+    t.bytes += (int64_t)(2 * maxs);
+    return DLR_OK;
+}
+
+
 // Counts of (column, phase) for batch sp; cnt has D*P entries.
 void pcsc_count(const CsrView &ds, const dlr::BatchSpan &sp, const PcscBuild &pb, std::vector<uint32_t> &cnt) {
     std::fill(cnt.begin(), cnt.end(), 0u);
@@ -1079,12 +1146,18 @@ hipError_t stage_dense(dlr_ctx *c, int64_t b, int s) {
 hipError_t stage_sparse(dlr_ctx *c, int64_t b, int s) {
     TrainShard &t = c->train;
     hipError_t e = hipStreamWaitEvent(c->cstream, c->ev_free[s], 0);
-    for (StreamArr &a : t.sarr) {
-        if (e != hipSuccess) break;
-        const int64_t beg = a.beg[(size_t)b], end = a.end[(size_t)b];
-        if (end <= beg) continue;
-        e = hipMemcpyAsync(a.slot[s], a.host + (size_t)beg * a.es, ((size_t)(end - beg) + a.pad) * a.es,
-                           hipMemcpyHostToDevice, c->cstream);
+    if (t.shost) {
+        if (e == hipSuccess && t.sbsz[(size_t)b] > 0)  // the batch's slices, one coalesced copy
+            e = hipMemcpyAsync(t.sslot[s], t.shost + t.sboff[(size_t)b], t.sbsz[(size_t)b], hipMemcpyHostToDevice,
+                               c->cstream);
+    } else {
+        for (StreamArr &a : t.sarr) {
+            if (e != hipSuccess) break;
+            const int64_t beg = a.beg[(size_t)b], end = a.end[(size_t)b];
+            if (end <= beg) continue;
+            e = hipMemcpyAsync(a.slot[s], a.host + (size_t)beg * a.es, ((size_t)(end - beg) + a.pad) * a.es,
+                               hipMemcpyHostToDevice, c->cstream);
+        }
     }
     if (e == hipSuccess) e = hipEventRecord(c->ev_ready[s], c->cstream);
     t.sb[s] = e == hipSuccess ? b : -1;
@@ -1103,8 +1176,12 @@ hipError_t sparse_batch(dlr_ctx *c, int64_t b) {
         e = stage_sparse(c, b, s);
     }
     if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_ready[s], 0);
-    for (StreamArr &a : t.sarr) {
-        void *p = static_cast<char *>(a.slot[s]) - (ptrdiff_t)((size_t)a.beg[(size_t)b] * a.es);
+    const size_t na = t.sarr.size();
+    for (size_t k = 0; k < na; ++k) {
+        const StreamArr &a = t.sarr[k];
+        char *base = t.shost ? static_cast<char *>(t.sslot[s]) + t.soff[(size_t)b * na + k]
+                             : static_cast<char *>(a.slot[s]);
+        void *p = base - (ptrdiff_t)((size_t)a.beg[(size_t)b] * a.es);
         memcpy(a.field, &p, sizeof p);
     }
     return e;
@@ -1858,6 +1935,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         HIPC(c, hipStreamSynchronize(c->stream));
         c->resid_cap = resid_need;
     }
+    if (t.sparse_stream && (rc = coalesce_stream(c, nthreads))) return rc;
     // streamed: the slots (counted by place()); resident: the shard arrays
     if (!t.sparse_stream)
         t.bytes = (int64_t)((t.n_rows + 1) * 8 + (t.nnz + kPad) * (t.unit ? 4 : 8) + t.n_rows * 4) + csc_bytes;

@@ -244,7 +244,8 @@ int dlr_load_test_dense(dlr_ctx *ctx, const dlr_dense *ds);
  * device slots on a copy stream while the previous batch computes --
  * PCIe-bound.  Dense shards stream the caller's rows in place (registered:
  * the dlr_dense must outlive the loaded shard); sparse shards stream a
- * page-locked copy of their CSR and per-batch column-major slices (every
+ * page-locked, batch-major copy of their CSR and per-batch column-major
+ * slices, each batch staged by ONE copy (every
  * layout except band mode, whose one >= 2^21-row batch is not worth
  * streaming: DLR_E_ARG).  AUTO (default) streams only when the shard would
  * not leave 8 GiB of HBM free.  Results are bitwise identical either way.
