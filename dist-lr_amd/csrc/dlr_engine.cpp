@@ -913,11 +913,8 @@ void for_batches(int64_t nb, int nthreads, Fn fn) {
 // per-array host copies and device slots by two batch-sized slots.
 int coalesce_stream(dlr_ctx *c, int nthreads) {
     TrainShard &t = c->train;
-    static const bool on = [] {  // DLR_STREAM_COALESCE=0: one copy per array and batch (A/B)
-        const char *e = getenv("DLR_STREAM_COALESCE");
-        return !(e && strcmp(e, "0") == 0);
-    }();
-    if (!on) return DLR_OK;
+    const char *ev = getenv("DLR_STREAM_COALESCE");  // "0": one copy per array and batch (A/B; read per load)
+    if (ev && strcmp(ev, "0") == 0) return DLR_OK;
     const size_t nb = t.plan.size(), na = t.sarr.size();
     t.soff.assign(nb * na, 0);
     t.sbsz.assign(nb, 0);

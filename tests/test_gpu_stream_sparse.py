@@ -47,6 +47,20 @@ def test_streamed_sparse_bitwise(monkeypatch, layout, B):
     assert_same_weights(got.w, orc.w)
 
 
+@pytest.mark.parametrize("coalesce", ["1", "0"])
+def test_streamed_copy_paths_bitwise(monkeypatch, coalesce):
+    # one coalesced copy per batch (default) and one copy per array and
+    # batch (DLR_STREAM_COALESCE=0): the same bytes land in the slots
+    monkeypatch.setenv("DLR_STREAM_COALESCE", coalesce)
+    monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
+    D = 30000
+    ds = dlr.Dataset.generate(3000, D, 20, value_mode=1, seed=23, stream=1)
+    monkeypatch.setenv("DLR_RESIDENCY", "stream")
+    got = run_engine([ds], D, 2, 1001, 0.1)
+    orc = oracle.run_worker([_csr(ds)], D, 2, 1001, 0.1)
+    assert_same_weights(got.w, orc.w)
+
+
 @pytest.mark.parametrize("value_mode", [0, 1])
 def test_streamed_long_columns(monkeypatch, value_mode):
     # classic layout with chunked long columns (per-batch long arrays streamed too)
