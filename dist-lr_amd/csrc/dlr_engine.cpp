@@ -81,6 +81,15 @@ struct TrainShard {
     uint16_t *prow = nullptr;     // entries (batch-relative offsets poff)
     float *pval = nullptr;
     std::vector<int64_t> poff;    // entry offset of each batch (+ total)
+    // streamed shards: only the block bases are streamed; the batch's ends /
+    // rows / values are built on the device from its CSR before its gradient
+    // (dlr_kernels.h launch_pcsc_build) into these one-batch buffers
+    bool gpu_pcsc = false;
+    int64_t pR = 0;
+    uint8_t *gends = nullptr;
+    uint16_t *grow = nullptr;
+    float *gval = nullptr;
+    uint32_t *gscratch = nullptr;
     // touched-column layout (huge D, small batches): per batch the touched
     // columns tcols[tcoff[b] .. +tncols[b]), segment pointers in cptr at
     // tpoff[b] (tncols[b]+1 entries), entries at coff[b] in crow/cval
@@ -305,7 +314,8 @@ void free_train(dlr_ctx *c) {
     }
     for (void *p : {(void *)t.row_ptr, (void *)t.col, (void *)t.val, (void *)t.label, (void *)t.w_row_ptr,
                     (void *)t.w_col, (void *)t.w_val, (void *)t.w_label, (void *)t.cptr, t.crow, (void *)t.cval,
-                    (void *)t.pbase, (void *)t.pends, (void *)t.prow, (void *)t.pval, (void *)t.tcols,
+                    (void *)t.pbase, (void *)t.pends, (void *)t.prow, (void *)t.pval, (void *)t.gends, (void *)t.grow,
+                    (void *)t.gval, (void *)t.gscratch, (void *)t.tcols,
                     (void *)t.lcols, (void *)t.lcseg, (void *)t.lsptr, t.lrow, (void *)t.lval, (void *)t.lpart, (void *)t.lsched,
                     (void *)t.dX, (void *)t.dpart, (void *)t.wsched, (void *)t.bcols, (void *)t.bptr,
                     (void *)t.bws, t.brow, (void *)t.bval, (void *)t.gacc, (void *)t.lpdesc, (void *)t.lpptr,
@@ -1042,6 +1052,27 @@ void pcsc_fill(const CsrView &ds, const std::vector<dlr::BatchSpan> &plan, int64
     });
 }
 
+// The block bases alone (pcsc_fill's first half), for a streamed shard
+// whose layout is built on the device.
+void pcsc_bases(const CsrView &ds, const std::vector<dlr::BatchSpan> &plan, int64_t D, const PcscBuild &pb,
+                std::vector<uint32_t> &base, int nthreads) {
+    const int64_t nb = (int64_t)plan.size();
+    for_batches(nb, nthreads, [&](int64_t b) {
+        std::vector<uint32_t> cnt((size_t)(D * pb.P));
+        pcsc_count(ds, plan[(size_t)b], pb, cnt);
+        uint32_t *bs = base.data() + (size_t)b * (size_t)(pb.pblocks + 1);
+        uint32_t at = 0;
+        for (int64_t g = 0; g < pb.groups; ++g)
+            for (int p = 0; p < pb.P; ++p) {
+                bs[g * pb.P + p] = at;
+                uint32_t o = 0;
+                for (int64_t j = g * 64; j < std::min(D, g * 64 + 64); ++j) o += cnt[(size_t)(j * pb.P + p)];
+                at += (o + 3) & ~3u;
+            }
+        bs[pb.pblocks] = at;
+    });
+}
+
 // Touched-column copy of one batch: the batch's entries sorted by (column,
 // batch row) -- a stable sort of the batch in row order, so each column's
 // segment lists its rows in the order lr.cc:37 visits them.
@@ -1195,6 +1226,15 @@ hipError_t sparse_batch_done(dlr_ctx *c, int64_t b) {
     return e;
 }
 
+// A streamed shard's LDS layout for batch b, built on the device from the
+// batch's CSR (just staged) and its streamed block bases.
+hipError_t build_layout(dlr_ctx *c, int64_t b) {
+    const TrainShard &t = c->train;
+    if (!t.gpu_pcsc) return hipSuccess;
+    return dlr::launch_pcsc_build(batch_view(c, b), t.pbase + (size_t)b * (size_t)(t.pblocks + 1), t.phases, t.pR,
+                                  t.pblocks, t.gscratch, t.gends, t.grow, t.gval, c->stream);
+}
+
 // Batch b's rows as the dense kernels see them: the resident shard (rows
 // from plan.first_row, wrapping), or the slot b is staged in (rows 0..B-1;
 // the engine stream waits for its copy).
@@ -1246,6 +1286,8 @@ hipError_t launch_margin(dlr_ctx *c, int64_t b) {
 
 dlr::DevPcsc pcsc_view(const dlr_ctx *c, int64_t b) {
     const TrainShard &t = c->train;
+    if (t.gpu_pcsc)  // built on the device for the current batch
+        return {t.pbase + (size_t)b * (size_t)(t.pblocks + 1), t.gends, t.grow, t.gval, t.phases};
     return {t.pbase + (size_t)b * (size_t)(t.pblocks + 1), t.pends + (size_t)b * (size_t)t.pblocks * 64,
             t.prow + t.poff[(size_t)b], t.pval + t.poff[(size_t)b], t.phases};
 }
@@ -1658,20 +1700,42 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         for (int64_t b = 0; b < nb; ++b) t.poff[(size_t)b + 1] = t.poff[(size_t)b] + pb.size[(size_t)b];
         const int64_t total = t.poff[(size_t)nb];
         std::vector<uint32_t> base((size_t)nb * (size_t)(pb.pblocks + 1));
-        std::vector<uint8_t> ends((size_t)nb * (size_t)pb.pblocks * 64);
-        std::vector<uint16_t> prow((size_t)total, 0);
-        std::vector<float> pval((size_t)total, 0.0f);
-        pcsc_fill(src, t.plan, D, pb, t.poff, base, ends, prow, pval, nthreads);
-        const int64_t pbk = pb.pblocks;
-        const RangeFn r_base = [&](int64_t b) { return std::make_pair(b * (pbk + 1), (b + 1) * (pbk + 1)); };
-        const RangeFn r_ends = [&](int64_t b) { return std::make_pair(b * pbk * 64, (b + 1) * pbk * 64); };
-        const RangeFn r_ent = [&](int64_t b) { return std::make_pair(t.poff[(size_t)b], t.poff[(size_t)b + 1]); };
-        if ((rc = place(c, &t.pbase, base.data(), base.size(), 0, r_base))) return rc;
-        if ((rc = place(c, &t.pends, ends.data(), ends.size(), 0, r_ends))) return rc;
-        if ((rc = place(c, &t.prow, prow.data(), prow.size(), 256, r_ent))) return rc;
-        if ((rc = place(c, &t.pval, pval.data(), pval.size(), 256, r_ent))) return rc;
-        csc_bytes = (int64_t)(base.size() * 4 + ends.size() + (total + 256) * 6);
-        resid_need = (int64_t)pb.P * pb.R;  // the fills read whole phases
+        const char *gb = getenv("DLR_STREAM_DEVICE_LAYOUT");  // "0": stream the host-built layout (A/B)
+        t.gpu_pcsc = t.sparse_stream && !(gb && strcmp(gb, "0") == 0);
+        if (t.gpu_pcsc) {
+            pcsc_bases(src, t.plan, D, pb, base, nthreads);
+            const int64_t pbk = pb.pblocks;
+            const RangeFn r_base = [&](int64_t b) { return std::make_pair(b * (pbk + 1), (b + 1) * (pbk + 1)); };
+            if ((rc = place(c, &t.pbase, base.data(), base.size(), 0, r_base))) return rc;
+            int64_t maxsz = 0;
+            for (int64_t b = 0; b < nb; ++b) maxsz = std::max(maxsz, pb.size[(size_t)b]);
+            t.pR = pb.R;
+            if ((rc = dev_alloc(c, (void **)&t.gends, (size_t)pbk * 64))) return rc;
+            if ((rc = dev_alloc(c, (void **)&t.grow, (size_t)(maxsz + 256) * 2))) return rc;
+            if ((rc = dev_alloc(c, (void **)&t.gval, (size_t)(maxsz + 256) * 4))) return rc;
+            if ((rc = dev_alloc(c, (void **)&t.gscratch, (size_t)pbk * 64 * 4))) return rc;
+            HIPC(c, hipMemsetAsync(t.grow, 0, (size_t)(maxsz + 256) * 2, c->stream));  // padded window reads
+            HIPC(c, hipMemsetAsync(t.gval, 0, (size_t)(maxsz + 256) * 4, c->stream));
+            csc_bytes = (int64_t)(pbk * 64 * 5 + (maxsz + 256) * 6);
+            t.bytes += csc_bytes;  // one batch's device-built layout (streamed: not in the slots)
+            resid_need = (int64_t)pb.P * pb.R;
+        }
+        if (!t.gpu_pcsc) {
+            std::vector<uint8_t> ends((size_t)nb * (size_t)pb.pblocks * 64);
+            std::vector<uint16_t> prow((size_t)total, 0);
+            std::vector<float> pval((size_t)total, 0.0f);
+            pcsc_fill(src, t.plan, D, pb, t.poff, base, ends, prow, pval, nthreads);
+            const int64_t pbk = pb.pblocks;
+            const RangeFn r_base = [&](int64_t b) { return std::make_pair(b * (pbk + 1), (b + 1) * (pbk + 1)); };
+            const RangeFn r_ends = [&](int64_t b) { return std::make_pair(b * pbk * 64, (b + 1) * pbk * 64); };
+            const RangeFn r_ent = [&](int64_t b) { return std::make_pair(t.poff[(size_t)b], t.poff[(size_t)b + 1]); };
+            if ((rc = place(c, &t.pbase, base.data(), base.size(), 0, r_base))) return rc;
+            if ((rc = place(c, &t.pends, ends.data(), ends.size(), 0, r_ends))) return rc;
+            if ((rc = place(c, &t.prow, prow.data(), prow.size(), 256, r_ent))) return rc;
+            if ((rc = place(c, &t.pval, pval.data(), pval.size(), 256, r_ent))) return rc;
+            csc_bytes = (int64_t)(base.size() * 4 + ends.size() + (total + 256) * 6);
+            resid_need = (int64_t)pb.P * pb.R;  // the fills read whole phases
+        }
     } else if (t.touched) {
         t.row16 = t.B <= 65536;
         std::vector<TouchedBatch> tbs((size_t)nb);
@@ -2104,7 +2168,10 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
     if (bt.rows > c->resid_cap) return fail(c, DLR_E_STATE, "dlr_train_step: residual buffer too small");
     hipEvent_t t_step, t0;
     time_begin(c, &t_step);
-    if (c->train.sparse_stream) HIPC(c, sparse_batch(c, b));  // binds the batch's slot (the views below)
+    if (c->train.sparse_stream) {
+        HIPC(c, sparse_batch(c, b));  // binds the batch's slot (the views below)
+        HIPC(c, build_layout(c, b));
+    }
     time_begin(c, &t0);
     HIPC(c, launch_margin(c, b));
     time_end(c, 0, t0);
@@ -2187,7 +2254,10 @@ int dlr_worker_gradient(dlr_ctx *c, int64_t b, float C, float *grad_out, int64_t
     struct {
         int64_t rows;
     } const bt{c->train.plan[(size_t)b].rows};
-    if (c->train.sparse_stream) HIPC(c, sparse_batch(c, b));
+    if (c->train.sparse_stream) {
+        HIPC(c, sparse_batch(c, b));
+        HIPC(c, build_layout(c, b));
+    }
     HIPC(c, launch_margin(c, b));
     if (c->train.touched) {
         // full pushed vector: the L2 term everywhere, the touched columns' g

@@ -153,7 +153,11 @@ hipError_t launch_long_phase(const DevLPhase &lp, const uint32_t *cols, const ui
                              const float *resid, float *part, float *graw, hipStream_t s);
 hipError_t launch_band_finalize(const float *gacc, float *w, float *gout, int64_t D, int64_t B, float lr, float C,
                                 bool fused, hipStream_t s);
-int grad_lds_fill(int64_t B);  // float4 fills per thread = rows per phase / 4,096
+int grad_lds_fill(int64_t B);
+// The LDS layout (DevPcsc row/val/ends) of one batch built on the device
+// from its CSR and block bases (streamed shards); scratch: pblocks*64 uint32.
+hipError_t launch_pcsc_build(const DevBatch &bt, const uint32_t *base, int P, int64_t R, int64_t pblocks,
+                             uint32_t *scratch, uint8_t *ends, uint16_t *row, float *val, hipStream_t s);  // float4 fills per thread = rows per phase / 4,096
 hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float *resid, float *w, float *gout,
                            float lr, float C, bool fused, hipStream_t s);
 // Touched-column layout (dlr_kernels.hip "Touched-column layout"): cs.ptr

@@ -454,6 +454,89 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad(DevCsc cs, const RowT *_
     }
 }
 
+// ---------------------------------------------------------------------------
+// The LDS layout of one batch (DevPcsc: per 64-column group and row phase a
+// block of entries, column by column, rows ascending, each block padded to 4
+// entries) built ON THE DEVICE from the batch's CSR, for a streamed shard:
+// then only the CSR and the block bases cross PCIe (the host's pcsc_fill
+// output is ~45% of a C2 batch's bytes).  Same bytes as pcsc_fill:
+//   (1) counts per (block, lane) by atomics; (2) a wave per block scans its
+//   64 counts into the end offsets and per-lane cursors and zeroes the
+//   block's padding; (3) entries scattered at atomically taken cursors --
+//   in any order within a (block, lane) run -- then (4) every run sorted by
+//   row (runs hold distinct rows: a column appears once per row), which is
+//   pcsc_fill's row-ordered layout exactly.
+__global__ __launch_bounds__(256) void k_pcsc_count(DevBatch bt, int P, int64_t R, uint32_t *__restrict__ cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= bt.rows) return;
+    const int64_t p = i / R;
+    for (int64_t k = bt.row_ptr[i]; k < bt.row_ptr[i + 1]; ++k) {
+        const uint32_t c = (uint32_t)bt.col[k];
+        atomicAdd(cnt + ((int64_t)(c >> 6) * P + p) * 64 + (c & 63), 1u);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pcsc_scan(const uint32_t *__restrict__ base, int64_t pblocks,
+                                                   uint32_t *__restrict__ cnt, uint8_t *__restrict__ ends,
+                                                   uint16_t *__restrict__ row, float *__restrict__ val) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t blk = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+    if (blk >= pblocks) return;  // wave-uniform
+    const uint32_t v = cnt[blk * 64 + lane];
+    uint32_t incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    const uint32_t b0 = base[blk];
+    ends[blk * 64 + lane] = (uint8_t)incl;
+    cnt[blk * 64 + lane] = b0 + incl - v;  // this lane's cursor
+    const uint32_t total = __shfl(incl, 63);
+    const uint32_t padded = (total + 3) & ~3u;
+    if ((uint32_t)lane < padded - total) {  // the block's padding entries
+        row[b0 + total + lane] = 0;
+        val[b0 + total + lane] = 0.0f;
+    }
+}
+
+template <bool UNIT>
+__global__ __launch_bounds__(256) void k_pcsc_scatter(DevBatch bt, int P, int64_t R, uint32_t *__restrict__ cur,
+                                                      uint16_t *__restrict__ row, float *__restrict__ val) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= bt.rows) return;
+    const int64_t p = i / R;
+    const uint16_t li = (uint16_t)(i - p * R);
+    for (int64_t k = bt.row_ptr[i]; k < bt.row_ptr[i + 1]; ++k) {
+        const uint32_t c = (uint32_t)bt.col[k];
+        const uint32_t pos = atomicAdd(cur + ((int64_t)(c >> 6) * P + p) * 64 + (c & 63), 1u);
+        row[pos] = li;
+        val[pos] = UNIT ? 1.0f : bt.val[k];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pcsc_order(const uint32_t *__restrict__ base, const uint8_t *__restrict__ ends,
+                                                    int64_t pblocks, uint16_t *__restrict__ row,
+                                                    float *__restrict__ val) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (block, lane)
+    if (q >= pblocks * 64) return;
+    const int64_t blk = q >> 6;
+    const int l = (int)(q & 63);
+    const uint32_t b0 = base[blk];
+    const uint32_t a = b0 + (l ? ends[q - 1] : 0u), e = b0 + ends[q];
+    for (uint32_t x = a + 1; x < e; ++x) {  // insertion sort by row (runs are short)
+        const uint16_t r = row[x];
+        const float v = val[x];
+        uint32_t y = x;
+        for (; y > a && row[y - 1] > r; --y) {
+            row[y] = row[y - 1];
+            val[y] = val[y - 1];
+        }
+        row[y] = r;
+        val[y] = v;
+    }
+}
+
 // Long columns (classic layout, e.g. Zipf-hot features of a full-shard
 // Criteo batch, BASELINE C3): a column with more than DLR_LONG_COLUMN
 // entries (default 4,096) would be one lane's serial chain of millions of
@@ -1788,6 +1871,23 @@ hipError_t launch_predict(const DevBatch &bt, const float *w, unsigned long long
     else if (grid > 0)
         hipLaunchKernelGGL(k_predict<false>, dim3(grid), dim3(kWaves * kWave), 0, s, bt, w, correct, ll_part);
     hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(64), 0, s, ll_part, grid, ll_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_pcsc_build(const DevBatch &bt, const uint32_t *base, int P, int64_t R, int64_t pblocks,
+                             uint32_t *scratch, uint8_t *ends, uint16_t *row, float *val, hipStream_t s) {
+    if (bt.rows <= 0 || pblocks <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(scratch, 0, (size_t)pblocks * 64 * 4, s);
+    if (e != hipSuccess) return e;
+    const unsigned gr = grid_for(bt.rows, 256);
+    hipLaunchKernelGGL(k_pcsc_count, dim3(gr), dim3(256), 0, s, bt, P, R, scratch);
+    hipLaunchKernelGGL(k_pcsc_scan, dim3(grid_for(pblocks * kWave, 256)), dim3(256), 0, s, base, pblocks, scratch, ends,
+                       row, val);
+    if (bt.val == nullptr)
+        hipLaunchKernelGGL(k_pcsc_scatter<true>, dim3(gr), dim3(256), 0, s, bt, P, R, scratch, row, val);
+    else
+        hipLaunchKernelGGL(k_pcsc_scatter<false>, dim3(gr), dim3(256), 0, s, bt, P, R, scratch, row, val);
+    hipLaunchKernelGGL(k_pcsc_order, dim3(grid_for(pblocks * 64, 256)), dim3(256), 0, s, base, ends, pblocks, row, val);
     return hipGetLastError();
 }
 

@@ -47,11 +47,14 @@ def test_streamed_sparse_bitwise(monkeypatch, layout, B):
     assert_same_weights(got.w, orc.w)
 
 
-@pytest.mark.parametrize("coalesce", ["1", "0"])
-def test_streamed_copy_paths_bitwise(monkeypatch, coalesce):
-    # one coalesced copy per batch (default) and one copy per array and
-    # batch (DLR_STREAM_COALESCE=0): the same bytes land in the slots
+@pytest.mark.parametrize("coalesce,device_layout", [("1", "1"), ("0", "1"), ("1", "0"), ("0", "0")])
+def test_streamed_copy_paths_bitwise(monkeypatch, coalesce, device_layout):
+    # one coalesced copy per batch (default) or one copy per array and batch
+    # (DLR_STREAM_COALESCE=0); the LDS layout built on the device from the
+    # staged CSR (default) or streamed as built on the host
+    # (DLR_STREAM_DEVICE_LAYOUT=0): the same sums either way
     monkeypatch.setenv("DLR_STREAM_COALESCE", coalesce)
+    monkeypatch.setenv("DLR_STREAM_DEVICE_LAYOUT", device_layout)
     monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
     D = 30000
     ds = dlr.Dataset.generate(3000, D, 20, value_mode=1, seed=23, stream=1)
