@@ -308,6 +308,9 @@ def run_rank(args):
     layout = "dense" if args.kind == "dense" else \
         {dlr.LAYOUT_CLASSIC: "classic", dlr.LAYOUT_LDS: "lds", dlr.LAYOUT_TOUCHED: "touched"}[eng.train_layout()]
     band_rows = eng.train_band_rows() if args.kind != "dense" else 0
+    margin_kind = "dense rows" if args.kind == "dense" else \
+        ["gathers", "product margin (pass 1 separate)",
+         "product margin (pass 1 fused into the previous step's gradient)"][eng.train_product_margin()]
     log(f"[rank {rank}] shard {args.rows} x {D}, nnz/row {args.nnz}: generated {t_gen:.1f}s, "
         f"{'streamed from host' if streamed else 'resident'} {train_bytes / 2**30:.2f} GiB in {t_load:.1f}s, "
         f"{nb} batches/epoch, gradient layout {layout}")
@@ -459,6 +462,7 @@ def run_rank(args):
                                    f"batch {B}, sync SGD lr {args.lr}, C=1",
                        "name": args.config, "gradient_layout": layout + (f"+bands({band_rows} rows)" if band_rows else ""),
                        "values": "unit (all 1.0f, not stored)" if unit else "fp32",
+                       "margin": margin_kind,
                        "rows_per_gpu": args.rows, "num_feature_dim": D, "nnz_per_row": args.nnz,
                        "batch_size": B, "parallelism": f"dp{world}"},
             "roofline": roofline,

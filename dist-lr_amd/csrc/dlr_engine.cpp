@@ -90,6 +90,18 @@ struct TrainShard {
     uint16_t *grow = nullptr;
     float *gval = nullptr;
     uint32_t *gscratch = nullptr;
+    // product margin (pcsc batches; dlr_kernels.h DevPm): batch b's slice
+    // list offsets at b*(pmS+1) of pm_lbeg, its list/values at pmo_list[b],
+    // chunk offsets at pmo_pofs[b], regions and slot-list offsets at pmo_rg[b]
+    // (rg, qoff), slot lists at pmo_qs[b]; pm_p holds one batch's products.
+    // pm_fused: the fused k_grad_lds forms the next batch's products.
+    bool pm = false, pm_fused = false;
+    int64_t pmS = 0;
+    int pm_groups = 0, pm_split = 1;
+    uint32_t *pm_lbeg = nullptr, *pm_list = nullptr, *pm_pofs = nullptr, *pm_rg = nullptr, *pm_qoff = nullptr;
+    float *pm_val = nullptr, *pm_p = nullptr;
+    uint16_t *pm_qs = nullptr;
+    std::vector<int64_t> pmo_list, pmo_pofs, pmo_rg, pmo_qs;
     // touched-column layout (huge D, small batches): per batch the touched
     // columns tcols[tcoff[b] .. +tncols[b]), segment pointers in cptr at
     // tpoff[b] (tncols[b]+1 entries), entries at coff[b] in crow/cval
@@ -201,6 +213,10 @@ struct dlr_ctx {
     double *h_ll = nullptr;                   // pinned
     TrainShard train;
     TestShard test;
+    // product margin: the batch whose products pm_p holds, formed from the
+    // CURRENT weights by the last step's fused gradient (-1: none; every
+    // entry point that changes w or the shard resets it)
+    int64_t pm_ready = -1;
     // touched-layout step buffers: newv (world 1: new weights of the touched
     // columns); sparse exchange (world > 1): send block [count|cols|g],
     // all-gathered blocks, merged (col, new weight) per entry
@@ -319,9 +335,12 @@ void free_train(dlr_ctx *c) {
                     (void *)t.lcols, (void *)t.lcseg, (void *)t.lsptr, t.lrow, (void *)t.lval, (void *)t.lpart, (void *)t.lsched,
                     (void *)t.dX, (void *)t.dpart, (void *)t.wsched, (void *)t.bcols, (void *)t.bptr,
                     (void *)t.bws, t.brow, (void *)t.bval, (void *)t.gacc, (void *)t.lpdesc, (void *)t.lpptr,
-                    (void *)t.lpslot, (void *)t.lpws, (void *)t.lprow, (void *)t.lpval})
+                    (void *)t.lpslot, (void *)t.lpws, (void *)t.lprow, (void *)t.lpval, (void *)t.pm_lbeg,
+                    (void *)t.pm_list, (void *)t.pm_pofs, (void *)t.pm_rg, (void *)t.pm_qoff, (void *)t.pm_val,
+                    (void *)t.pm_p, (void *)t.pm_qs})
         dev_free(c, p);
     t = TrainShard();
+    c->pm_ready = -1;
 }
 
 template <typename T>
@@ -540,6 +559,7 @@ int change_perm(dlr_ctx *c, std::vector<int32_t> &&np) {
     HIPC(c, hipMemcpyAsync(oldw.data(), c->w, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     for (int64_t j = 0; j < D; ++j) neww[(size_t)pid(np, j)] = oldw[(size_t)pid(c->perm, j)];
+    c->pm_ready = -1;
     HIPC(c, hipMemcpyAsync(c->w, neww.data(), (size_t)D * 4, hipMemcpyHostToDevice, c->stream));
     TestShard &t = c->test;
     if (t.loaded && !t.dense && t.nnz > 0) {
@@ -1052,6 +1072,108 @@ void pcsc_fill(const CsrView &ds, const std::vector<dlr::BatchSpan> &plan, int64
     });
 }
 
+// Product-margin layout of one batch (dlr_kernels.h DevPm).  Returns false
+// when the batch does not fit it (a region over kPmCap products, a chunk
+// over kPmMaxChunk, a row over 8 * kPmMaxGroups entries).
+struct PmBatch {
+    std::vector<uint32_t> lbeg, list, pofs, rg, qoff;
+    std::vector<float> val;
+    std::vector<uint16_t> qs;
+    int groups = 0;
+    int64_t maxslice = 0;
+};
+
+bool pm_batch(const CsrView &ds, const dlr::BatchSpan &sp, int64_t D, bool unit, PmBatch &o) {
+    const int64_t N = ds.n_rows, R = sp.rows;
+    const int64_t S = (D + dlr::kPmSlice - 1) / dlr::kPmSlice, nblk = (R + dlr::kPmRows - 1) / dlr::kPmRows;
+    if (nblk > dlr::kPmMaxBlocks) return false;
+    // a region's chunks in the order of their slice's XCD (workgroup s runs
+    // on XCD s % 8): each XCD's pass-1 stores land in adjacent chunks
+    std::vector<int64_t> sorder;
+    for (int x = 0; x < 8; ++x)
+        for (int64_t q = x; q < S; q += 8) sorder.push_back(q);
+    auto row_of = [&](int64_t i) { return (sp.first_row + i) % N; };
+    std::vector<uint32_t> cnt((size_t)(nblk * S), 0), slice_n((size_t)S + 1, 0);
+    for (int64_t i = 0; i < R; ++i) {
+        const int64_t r = row_of(i), k = i / dlr::kPmRows;
+        if (ds.row_ptr[r + 1] - ds.row_ptr[r] > 8 * dlr::kPmMaxGroups) return false;
+        for (int64_t e = ds.row_ptr[r]; e < ds.row_ptr[r + 1]; ++e) ++cnt[(size_t)(k * S + ds.col[e] / dlr::kPmSlice)];
+    }
+    // chunks padded to whole 4-slot groups (pass 1 stores 16 bytes per group)
+    std::vector<uint32_t> cofs((size_t)(nblk * S));
+    o.rg.assign((size_t)nblk + 1, 0);
+    uint32_t at = 0;
+    for (int64_t k = 0; k < nblk; ++k) {
+        o.rg[(size_t)k] = at;
+        for (int64_t q : sorder) {
+            const uint32_t n = (cnt[(size_t)(k * S + q)] + 3) & ~3u;
+            if (n > (uint32_t)dlr::kPmMaxChunk) return false;
+            cofs[(size_t)(k * S + q)] = at;
+            at += n;
+            slice_n[(size_t)q + 1] += n;
+        }
+        if (at - o.rg[(size_t)k] > (uint32_t)dlr::kPmCap) return false;
+    }
+    o.rg[(size_t)nblk] = at;
+    for (int64_t q = 0; q < S; ++q) {
+        o.maxslice = std::max<int64_t>(o.maxslice, slice_n[(size_t)q + 1]);
+        slice_n[(size_t)q + 1] += slice_n[(size_t)q];
+    }
+    o.lbeg.assign(slice_n.begin(), slice_n.end());
+    const size_t E = slice_n[(size_t)S];
+    o.list.assign(E, 0);
+    if (!unit) o.val.assign(E, 0.0f);
+    o.pofs.assign((size_t)(S * nblk), 0);
+    for (int64_t q = 0; q < S; ++q)
+        for (int64_t k = 0; k < nblk; ++k) o.pofs[(size_t)(q * nblk + k)] = cofs[(size_t)(k * S + q)];
+    // padding entries: column 0, value 0, the group's block and rank
+    for (int64_t q = 0; q < S; ++q) {
+        uint32_t li = slice_n[(size_t)q];
+        for (int64_t k = 0; k < nblk; ++k) {
+            const uint32_t n = cnt[(size_t)(k * S + q)], np = (n + 3) & ~3u;
+            for (uint32_t j = n; j < np; ++j) o.list[li + j] = (uint32_t)k << 12 | j << 22;
+            li += np;
+        }
+    }
+    // entries: slice q's list holds block k's chunk at its padded offset
+    std::vector<uint32_t> lcur((size_t)(nblk * S));
+    for (int64_t q = 0; q < S; ++q) {
+        uint32_t li = slice_n[(size_t)q];
+        for (int64_t k = 0; k < nblk; ++k) {
+            lcur[(size_t)(k * S + q)] = li;
+            li += (cnt[(size_t)(k * S + q)] + 3) & ~3u;
+        }
+    }
+    std::vector<uint32_t> fill(cofs);
+    o.qoff.assign((size_t)nblk + 1, 0);
+    o.qs.clear();
+    o.groups = 0;
+    for (int64_t k = 0; k < nblk; ++k) {
+        const int64_t i0 = k * dlr::kPmRows, i1 = std::min(R, i0 + dlr::kPmRows);
+        int64_t ml = 0;
+        for (int64_t i = i0; i < i1; ++i) ml = std::max(ml, ds.row_ptr[row_of(i) + 1] - ds.row_ptr[row_of(i)]);
+        const int g = (int)((ml + 7) / 8);
+        o.groups = std::max(o.groups, g);
+        const size_t q0 = o.qs.size();
+        o.qoff[(size_t)k] = (uint32_t)q0;
+        o.qs.resize(q0 + (size_t)g * 512, 0);
+        for (int64_t i = i0; i < i1; ++i) {
+            const int64_t r = row_of(i), l = i - i0;
+            for (int64_t e = ds.row_ptr[r], kk = 0; e < ds.row_ptr[r + 1]; ++e, ++kk) {
+                const int64_t q = ds.col[e] / dlr::kPmSlice;
+                const uint32_t slot = fill[(size_t)(k * S + q)]++;
+                const uint32_t j = slot - cofs[(size_t)(k * S + q)];
+                const uint32_t li = lcur[(size_t)(k * S + q)]++;
+                o.list[li] = (uint32_t)(ds.col[e] % dlr::kPmSlice) | (uint32_t)k << 12 | j << 22;
+                if (!unit) o.val[li] = ds.val[e];
+                o.qs[q0 + (size_t)(kk / 8) * 512 + (size_t)l * 8 + (size_t)(kk % 8)] = (uint16_t)(slot - o.rg[(size_t)k]);
+            }
+        }
+    }
+    o.qoff[(size_t)nblk] = (uint32_t)o.qs.size();
+    return true;
+}
+
 // The block bases alone (pcsc_fill's first half), for a streamed shard
 // whose layout is built on the device.
 void pcsc_bases(const CsrView &ds, const std::vector<dlr::BatchSpan> &plan, int64_t D, const PcscBuild &pb,
@@ -1145,6 +1267,23 @@ dlr::DevBatch batch_view(const dlr_ctx *c, int64_t b) {
     const int64_t nnz = t.coff[(size_t)b + 1] - t.coff[(size_t)b];  // upper bound (aligned)
     if (b == t.wrap_batch) return {t.w_row_ptr, t.w_col, t.w_val, t.w_label, sp.rows, nnz};
     return {t.row_ptr + sp.first_row, t.col, t.val, t.label + sp.first_row, sp.rows, nnz};
+}
+
+dlr::DevPm pm_view(const dlr_ctx *c, int64_t b) {
+    const TrainShard &t = c->train;
+    dlr::DevPm v{};
+    v.lbeg = t.pm_lbeg + b * (t.pmS + 1);
+    v.list = t.pm_list + t.pmo_list[(size_t)b];
+    v.val = t.pm_val ? t.pm_val + t.pmo_list[(size_t)b] : nullptr;
+    v.pofs = t.pm_pofs + t.pmo_pofs[(size_t)b];
+    v.rg = t.pm_rg + t.pmo_rg[(size_t)b];
+    v.qoff = t.pm_qoff + t.pmo_rg[(size_t)b];
+    v.qs = t.pm_qs + t.pmo_qs[(size_t)b];
+    v.S = t.pmS;
+    v.nblk = t.pmo_rg[(size_t)b + 1] - t.pmo_rg[(size_t)b] - 1;
+    v.groups = t.pm_groups;
+    v.split = t.pm_split;
+    return v;
 }
 
 // Streamed dense shard: copy batch b's rows (wrapping to row 0 as
@@ -1270,7 +1409,9 @@ hipError_t dense_batch_done(dlr_ctx *c, int64_t b) {
     return e;
 }
 
-hipError_t launch_margin(dlr_ctx *c, int64_t b) {
+// rowsum_only (dlr_stage_time): the product margin's pass 2 alone, on
+// whatever products pm_p holds (the same work; the residuals are not used).
+hipError_t launch_margin(dlr_ctx *c, int64_t b, bool rowsum_only = false) {
     const TrainShard &t = c->train;
     if (t.dense) {
         dlr::DevDense dd;
@@ -1279,6 +1420,16 @@ hipError_t launch_margin(dlr_ctx *c, int64_t b) {
         if (e != hipSuccess) return e;
         if (t.dfused) return dlr::launch_dense_fused(dd, first, t.plan[(size_t)b].rows, c->w, t.dpart, c->stream);
         return dlr::launch_dense_margin(dd, first, t.plan[(size_t)b].rows, c->w, c->resid, c->stream);
+    }
+    if (t.pm) {
+        // products of batch b from the current weights: made by the previous
+        // step's fused gradient when it guessed b, else pass 1 now
+        if (c->pm_ready != b && !rowsum_only) {
+            const hipError_t e = dlr::launch_pm_products(pm_view(c, b), c->w, c->D, t.pm_p, c->stream);
+            if (e != hipSuccess) return e;
+        }
+        c->pm_ready = -1;  // this step changes the weights
+        return dlr::launch_pm_margin(pm_view(c, b), batch_view(c, b), t.pm_p, c->resid, c->stream);
     }
     if (t.margin_hot) return dlr::launch_margin_hot(batch_view(c, b), c->w, c->D, c->resid, c->stream);
     return dlr::launch_margin_residual(batch_view(c, b), c->w, c->resid, c->stream);
@@ -1318,7 +1469,17 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
         if (e == hipSuccess) e = dense_batch_done(c, b);
         return e;
     }
-    if (t.pcsc) return dlr::launch_grad_lds(pcsc_view(c, b), c->D, B, c->resid, c->w, gout, lr, C, fused, c->stream);
+    if (t.pcsc) {
+        if (t.pm_fused && fused) {
+            // the update, then the next batch's products from the new weights
+            const int64_t nx = (b + 1) % (int64_t)t.plan.size();
+            const hipError_t e = dlr::launch_grad_lds_pm(pcsc_view(c, b), c->D, B, c->resid, c->w, lr, C,
+                                                         pm_view(c, nx), t.pm_p, c->stream);
+            if (e == hipSuccess) c->pm_ready = nx;
+            return e;
+        }
+        return dlr::launch_grad_lds(pcsc_view(c, b), c->D, B, c->resid, c->w, gout, lr, C, fused, c->stream);
+    }
     const size_t bb = (size_t)b;
     const size_t esz = t.row16 ? 2 : 4;
     hipError_t e = hipSuccess;
@@ -1482,6 +1643,7 @@ int dlr_set_weights(dlr_ctx *c, const float *w, int64_t D) {
         for (int64_t j = 0; j < D; ++j) tmp[(size_t)c->perm[(size_t)j]] = w[j];
         w = tmp.data();
     }
+    c->pm_ready = -1;
     HIPC(c, hipMemcpyAsync(c->w, w, (size_t)D * 4, hipMemcpyHostToDevice, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     return DLR_OK;
@@ -1735,6 +1897,84 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             if ((rc = place(c, &t.pval, pval.data(), pval.size(), 256, r_ent))) return rc;
             csc_bytes = (int64_t)(base.size() * 4 + ends.size() + (total + 256) * 6);
             resid_need = (int64_t)pb.P * pb.R;  // the fills read whole phases
+        }
+        // Product margin (dlr_kernels.hip "Product margin"): resident shards
+        // whose batches fit it, with enough column slices to fill the GPU
+        // (DLR_PM=0 off, =1 on whenever the batches fit).
+        const char *pme = getenv("DLR_PM");
+        const int64_t S = (D + dlr::kPmSlice - 1) / dlr::kPmSlice;
+        if (!t.sparse_stream && !(pme && strcmp(pme, "0") == 0) && ((pme && strcmp(pme, "1") == 0) || S >= 128)) {
+            std::vector<PmBatch> pm((size_t)nb);
+            std::atomic<bool> ok{true};
+            for_batches(nb, nthreads, [&](int64_t b) {
+                if (ok && !pm_batch(src, t.plan[(size_t)b], D, t.unit, pm[(size_t)b])) ok = false;
+            });
+            if (ok) {
+                t.pmS = S;
+                t.pmo_list.assign((size_t)nb + 1, 0);
+                t.pmo_pofs.assign((size_t)nb + 1, 0);
+                t.pmo_rg.assign((size_t)nb + 1, 0);
+                t.pmo_qs.assign((size_t)nb + 1, 0);
+                int64_t pcap = 0, maxslice = 0;
+                for (int64_t b = 0; b < nb; ++b) {
+                    const PmBatch &q = pm[(size_t)b];
+                    t.pmo_list[(size_t)b + 1] = t.pmo_list[(size_t)b] + (int64_t)q.list.size();
+                    t.pmo_pofs[(size_t)b + 1] = t.pmo_pofs[(size_t)b] + (int64_t)q.pofs.size();
+                    t.pmo_rg[(size_t)b + 1] = t.pmo_rg[(size_t)b] + (int64_t)q.rg.size();
+                    t.pmo_qs[(size_t)b + 1] = t.pmo_qs[(size_t)b] + (int64_t)q.qs.size();
+                    pcap = std::max<int64_t>(pcap, q.rg.back());
+                    maxslice = std::max(maxslice, q.maxslice);
+                    t.pm_groups = std::max(t.pm_groups, q.groups);
+                }
+                t.pm_split = (int)std::min<int64_t>(16, std::max<int64_t>(1, (maxslice + 16383) / 16384));
+                auto cat32 = [&](std::vector<uint32_t> PmBatch::*f, const std::vector<int64_t> &off) {
+                    std::vector<uint32_t> v((size_t)off.back());
+                    for (int64_t b = 0; b < nb; ++b)
+                        std::copy(((pm[(size_t)b]).*f).begin(), ((pm[(size_t)b]).*f).end(), v.begin() + off[(size_t)b]);
+                    return v;
+                };
+                std::vector<uint32_t> lbeg((size_t)(nb * (S + 1)));
+                for (int64_t b = 0; b < nb; ++b)
+                    std::copy(pm[(size_t)b].lbeg.begin(), pm[(size_t)b].lbeg.end(), lbeg.begin() + b * (S + 1));
+                if ((rc = upload(c, &t.pm_lbeg, lbeg.data(), lbeg.size()))) return rc;
+                {
+                    std::vector<uint32_t> v = cat32(&PmBatch::list, t.pmo_list);
+                    if ((rc = upload(c, &t.pm_list, v.data(), v.size(), 64))) return rc;
+                }
+                if (!t.unit) {
+                    std::vector<float> v((size_t)t.pmo_list.back());
+                    for (int64_t b = 0; b < nb; ++b)
+                        std::copy(pm[(size_t)b].val.begin(), pm[(size_t)b].val.end(), v.begin() + t.pmo_list[(size_t)b]);
+                    if ((rc = upload(c, &t.pm_val, v.data(), v.size(), 64))) return rc;
+                }
+                {
+                    std::vector<uint32_t> v = cat32(&PmBatch::pofs, t.pmo_pofs);
+                    if ((rc = upload(c, &t.pm_pofs, v.data(), v.size()))) return rc;
+                }
+                {
+                    std::vector<uint32_t> v = cat32(&PmBatch::rg, t.pmo_rg);
+                    if ((rc = upload(c, &t.pm_rg, v.data(), v.size()))) return rc;
+                }
+                {
+                    std::vector<uint32_t> v = cat32(&PmBatch::qoff, t.pmo_rg);
+                    if ((rc = upload(c, &t.pm_qoff, v.data(), v.size()))) return rc;
+                }
+                {
+                    std::vector<uint16_t> v((size_t)t.pmo_qs.back());
+                    for (int64_t b = 0; b < nb; ++b)
+                        std::copy(pm[(size_t)b].qs.begin(), pm[(size_t)b].qs.end(), v.begin() + t.pmo_qs[(size_t)b]);
+                    if ((rc = upload(c, &t.pm_qs, v.data(), v.size(), 8))) return rc;
+                }
+                if ((rc = dev_alloc(c, (void **)&t.pm_p, (size_t)(pcap + 64) * 4))) return rc;
+                HIPC(c, hipMemsetAsync(t.pm_p, 0, (size_t)(pcap + 64) * 4, c->stream));
+                csc_bytes += (int64_t)(lbeg.size() * 4 + t.pmo_list.back() * (t.unit ? 4 : 8) +
+                                       t.pmo_pofs.back() * 4 + t.pmo_rg.back() * 8 + t.pmo_qs.back() * 2 + pcap * 4);
+                t.pm = true;
+                const char *pf = getenv("DLR_PM_FUSED");
+                t.pm_fused = !c->comm && !(pf && strcmp(pf, "0") == 0);
+            } else if (pme && strcmp(pme, "1") == 0) {
+                return fail(c, DLR_E_ARG, "dlr_load_train: DLR_PM=1 but the batches do not fit the product margin");
+            }
         }
     } else if (t.touched) {
         t.row16 = t.B <= 65536;
@@ -2300,6 +2540,7 @@ int dlr_server_apply(dlr_ctx *c, const float *grads, int W, int64_t D, float lr,
     int rc = dev_alloc(c, (void **)&buf, (size_t)W * (size_t)D * 4);
     if (rc) return rc;
     hipError_t e = hipMemcpyAsync(buf, grads, (size_t)W * (size_t)D * 4, hipMemcpyHostToDevice, c->stream);
+    c->pm_ready = -1;
     if (e == hipSuccess) e = dlr::launch_merge_update(buf, W, D, D, c->w, lr, mode, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     dev_free(c, buf);
@@ -2385,7 +2626,9 @@ int dlr_stage_time(dlr_ctx *c, int stage, int64_t first, int64_t count, float lr
         const int64_t bb = (first + k) % nb;
         const int64_t rows = t.plan[(size_t)bb].rows;
         if (stage == DLR_STAGE_MARGIN) {
-            e = launch_margin(c, bb);
+            // product margin: pass 2 alone -- in the training step pass 1 runs
+            // inside the previous step's gradient (counted there)
+            e = launch_margin(c, bb, t.pm_fused);
         } else if (t.touched) {
             const int64_t n = t.tncols[(size_t)bb];
             const uint32_t *cols = t.tcols + t.tcoff[(size_t)bb];
@@ -2407,6 +2650,7 @@ int dlr_stage_time(dlr_ctx *c, int stage, int64_t first, int64_t count, float lr
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     c->timing = was;
+    c->pm_ready = -1;  // the stages ran without their partners
     if (e != hipSuccess) return fail(c, DLR_E_HIP, std::string("dlr_stage_time: ") + hipGetErrorString(e));
     if (avg_ms) *avg_ms = (double)ms / (double)count;
     return DLR_OK;
@@ -2434,6 +2678,12 @@ int dlr_train_unit_values(dlr_ctx *c) {
     if (!c) return DLR_E_ARG;
     if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_unit_values: no training shard loaded");
     return c->train.unit ? 1 : 0;
+}
+
+int dlr_train_product_margin(dlr_ctx *c) {
+    if (!c) return DLR_E_ARG;
+    if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_product_margin: no training shard loaded");
+    return c->train.pm ? (c->train.pm_fused ? 2 : 1) : 0;
 }
 
 int dlr_train_band_rows(dlr_ctx *c) {

@@ -112,6 +112,40 @@ struct DevLPhase {
     uint32_t npart;  // partials; part[npart, npart + 64) is a write sink for idle lanes
 };
 
+// PRODUCT MARGIN of one batch (dlr_kernels.hip "Product margin"; LDS-layout
+// batches).  The batch's rows fall in blocks of kPmRows; its columns in
+// slices of kPmSlice (the columns of one k_grad_lds workgroup).  Every
+// product fl32(w_j * x_ij) of the batch has a slot in the product array p:
+// block k's products fill its REGION [rg[k], rg[k+1]) (4-aligned, <=
+// kPmCap), one chunk per slice (chunks ordered by the XCD of their slice's
+// workgroup; each padded to a multiple of 4 slots), rows ascending within a
+// chunk.  Pass 1 (workgroup = slice s) forms slice s's products: list
+// entries [lbeg[s], lbeg[s+1]) of list/val (multiples of 4), entry =
+// (column within slice | block << 12 | rank in chunk << 22), the chunk of
+// block k starting at p[pofs[s*nblk + k]]; padding entries (column 0,
+// value 0) complete each chunk's last 4-slot group.  Pass 2 (wave = block)
+// copies its region into LDS and each lane adds its row's products in
+// column order through its slot list: qs[qoff[k] + (i/8)*512 + lane*8 + i%8]
+// = region slot of the row's i-th entry (qoff[k+1] - qoff[k] = 512 * groups).
+constexpr int kPmSlice = 4096;
+constexpr int kPmRows = 64;
+constexpr int kPmCap = 4096;
+constexpr int kPmMaxGroups = 16;  // rows of up to 128 entries
+constexpr int kPmMaxChunk = 1024;
+constexpr int kPmMaxBlocks = 1024;
+struct DevPm {
+    const uint32_t *lbeg;  // S + 1, relative to list/val
+    const uint32_t *list;
+    const float *val;      // null: unit values
+    const uint32_t *pofs;  // S x nblk
+    const uint32_t *rg;    // nblk + 1
+    const uint32_t *qoff;  // nblk + 1, relative to qs
+    const uint16_t *qs;
+    int64_t S, nblk;
+    int groups;            // max slot groups of a block (8 entries each)
+    int split;             // pass-1 workgroups per slice (standalone pass)
+};
+
 // Dense rows (row-major N x D fp32) and 0/1 labels as floats.
 struct DevDense {
     const float *X;
@@ -160,6 +194,15 @@ hipError_t launch_pcsc_build(const DevBatch &bt, const uint32_t *base, int P, in
                              uint32_t *scratch, uint8_t *ends, uint16_t *row, float *val, hipStream_t s);  // float4 fills per thread = rows per phase / 4,096
 hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float *resid, float *w, float *gout,
                            float lr, float C, bool fused, hipStream_t s);
+// Product margin: pass 1 (the products of pm's batch from w), pass 2 (the
+// margins, sigmoid and residuals of bt's rows from those products).
+hipError_t launch_pm_products(const DevPm &pm, const float *w, int64_t D, float *p, hipStream_t s);
+hipError_t launch_pm_margin(const DevPm &pm, const DevBatch &bt, const float *p, float *resid, hipStream_t s);
+// k_grad_lds (fused update) that also forms the products of the NEXT batch
+// (next: its product-margin view) from the weights it has just updated:
+// pass 1 for free in the gradient's workgroups (slice s = workgroup s).
+hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const float *resid, float *w, float lr,
+                              float C, const DevPm &next, float *p, hipStream_t s);
 // Touched-column layout (dlr_kernels.hip "Touched-column layout"): cs.ptr
 // spans the ncols touched columns cols[] of the batch.
 hipError_t launch_grad_touched(const DevCsc &cs, const uint32_t *cols, int64_t ncols, const float *resid,

@@ -685,11 +685,177 @@ constexpr int kGradNG = 4;      // 64-column groups per wave
 constexpr int kBlk = 256;       // window = one phase block (<= 255 entries)
 constexpr int kBlkPad = kBlk + 8;  // product slab per wave: lane reads at o + [0, 8) never leave it
 
-template <int FILL, bool FUSED, bool NTW>
+// ---------------------------------------------------------------------------
+// Product margin (LDS-layout batches; dlr_kernels.h DevPm).  The gather
+// margin (k_margin_residual) issues one random 4-byte L2 request per entry
+// and runs at the L2 request rate (C2: 3.28M per batch, ~21 us).  Here the
+// weights are read by SLICE instead: pass 1 -- one workgroup per 4,096-column
+// slice, i.e. the columns of one k_grad_lds workgroup, which can run it
+// right after its update -- stages the slice's weights in LDS and forms the
+// batch's products in the slice, writing them block by block into the
+// product array; pass 2 -- a wave per 64-row block -- copies the block's
+// products (one contiguous region) into LDS with 16-byte loads and each lane
+// adds its row's products in column order through a precomputed slot list.
+// The products are the same fl32(w_j * x_ij) and each row's additions run in
+// the same (column) order from +0: bitwise k_margin_residual's residuals.
+
+// Pass 1 of one workgroup: the 4-entry groups [c0, c1) of slice s's list
+// (chunks are padded to whole groups: a group is 4 consecutive product
+// slots of one chunk, 16-byte aligned), U groups per thread in flight at
+// once (the rest in further rounds); one 16-byte store per group.
+template <int NT, int U>
+struct PmPass1 {
+    static constexpr int NPO = (kPmMaxBlocks + NT - 1) / NT;
+    uint4 pk[U];
+    float4 v[U];
+    uint32_t po[NPO];
+    uint32_t c0 = 0, c1 = 0;
+    // vector-memory instructions load() issues per thread, always (clamped
+    // addresses; the lists are padded): k_grad_lds waits for its fill with
+    // s_waitcnt vmcnt(kLoads) while these are still in flight
+    static constexpr int kLoads = NPO + 2 * U;
+    __device__ __forceinline__ void fetch(const DevPm &pm, uint32_t g0) {
+        const float *vp = pm.val ? pm.val : reinterpret_cast<const float *>(pm.list);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t g = g0 + u * NT + threadIdx.x;
+            const uint32_t gc = g < c1 ? g : c0;
+            pk[u] = load_stream(reinterpret_cast<const uint4 *>(pm.list) + gc);
+            v[u] = load_stream(reinterpret_cast<const float4 *>(vp) + gc);
+        }
+    }
+    __device__ __forceinline__ void load(const DevPm &pm, int s, int part = 0, int nparts = 1) {
+        const uint32_t b0 = pm.lbeg[s] / 4, b1 = pm.lbeg[s + 1] / 4;
+        const uint32_t n = b1 - b0, per = (n + nparts - 1) / nparts;
+        c0 = b0 + min(n, per * part);
+        c1 = b0 + min(n, per * (part + 1));
+        const int64_t nb = pm.nblk;
+#pragma unroll
+        for (int u = 0; u < NPO; ++u) {
+            const int64_t i = u * NT + threadIdx.x;
+            po[u] = pm.pofs[(int64_t)s * nb + (i < nb ? i : nb - 1)];
+        }
+        fetch(pm, c0);
+    }
+    __device__ __forceinline__ void stage_offsets(uint32_t *s_po) const {
+#pragma unroll
+        for (int u = 0; u < NPO; ++u) {
+            const int i = u * NT + threadIdx.x;
+            if (i < kPmMaxBlocks) s_po[i] = po[u];
+        }
+    }
+    // s_w: the slice's weights; s_po: the staged chunk offsets.  A group's
+    // slot is its first entry's (block, rank); padding entries (column 0,
+    // value 0) fill slots no row reads.
+    __device__ __forceinline__ void store(const DevPm &pm, const float *s_w, const uint32_t *s_po,
+                                          float *__restrict__ p) {
+        const bool unit = pm.val == nullptr;
+        for (uint32_t g0 = c0; g0 < c1; g0 += U * NT) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t g = g0 + u * NT + threadIdx.x;
+                if (g < c1) {
+                    const uint32_t k = (pk[u].x >> 12) & (kPmMaxBlocks - 1);
+                    float4 q;
+                    q.x = s_w[pk[u].x & (kPmSlice - 1)] * (unit ? 1.0f : v[u].x);
+                    q.y = s_w[pk[u].y & (kPmSlice - 1)] * (unit ? 1.0f : v[u].y);
+                    q.z = s_w[pk[u].z & (kPmSlice - 1)] * (unit ? 1.0f : v[u].z);
+                    q.w = s_w[pk[u].w & (kPmSlice - 1)] * (unit ? 1.0f : v[u].w);
+                    *reinterpret_cast<float4 *>(p + s_po[k] + (pk[u].x >> 22)) = q;
+                }
+            }
+            if (g0 + U * NT < c1) fetch(pm, g0 + U * NT);
+        }
+    }
+};
+
+// Standalone pass 1: SPLIT (pm.split) workgroups per slice, all on the
+// slice's XCD (workgroup x runs on XCD x % 8): slice s = (x/8/SPLIT)*8 + x%8,
+// so each XCD's L2 serves its 1/8 of w and the region chunks it writes are
+// adjacent (a region's chunks are ordered by XCD).
+__global__ __launch_bounds__(1024) void k_pm_products(DevPm pm, const float *__restrict__ w, int64_t D,
+                                                      float *__restrict__ p) {
+    __shared__ __attribute__((aligned(16))) float s_w[kPmSlice];
+    __shared__ uint32_t s_po[kPmMaxBlocks];
+    const int x = blockIdx.x, xcd = x & 7, k = x >> 3;
+    const int s = (k / pm.split) * 8 + xcd, part = k % pm.split;
+    if (s >= pm.S) return;  // whole workgroup
+    PmPass1<1024, 4> pp;
+    const int64_t j = (int64_t)s * kPmSlice + 4 * threadIdx.x;  // one float4 per thread
+    const float4 wv = j + 3 < D ? *reinterpret_cast<const float4 *>(w + j)
+                                : make_float4(j < D ? w[j] : 0.f, j + 1 < D ? w[j + 1] : 0.f,
+                                              j + 2 < D ? w[j + 2] : 0.f, 0.f);
+    pp.load(pm, s, part, pm.split);
+    reinterpret_cast<float4 *>(s_w)[threadIdx.x] = wv;
+    pp.stage_offsets(s_po);
+    __syncthreads();
+    pp.store(pm, s_w, s_po, p);
+}
+
+// Pass 2: a wave per block; lane l owns row 64k + l of bt.
+template <int QG>
+__global__ __launch_bounds__(256) void k_pm_margin(DevPm pm, DevBatch bt, const float *__restrict__ p,
+                                                   float *__restrict__ resid) {
+    __shared__ __attribute__((aligned(16))) float s_reg[4][kPmCap];
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    const int64_t blk = (int64_t)blockIdx.x * 4 + wv;
+    const int64_t r0 = blk * kPmRows;
+    if (r0 >= bt.rows) return;  // wave-uniform
+    const uint32_t a = pm.rg[blk], b = pm.rg[blk + 1];
+    const uint32_t q0 = pm.qoff[blk], q1 = pm.qoff[blk + 1];
+    const int64_t my = r0 + lane;
+    const bool valid = my < bt.rows;
+    const int64_t mc = valid ? my : r0;
+    const int len = valid ? (int)(bt.row_ptr[mc + 1] - bt.row_ptr[mc]) : 0;
+    const float y = bt.label[mc];
+    float *sr = s_reg[wv];
+    const int n4 = (int)((b - a) >> 2);
+    const int ngrp = (int)((q1 - q0) >> 9);
+    constexpr int R4 = kPmCap / 4 / kWave;
+    // the region and the slot lists in flight at once
+    float4 rv[R4];
+    uint4 qv[QG];
+#pragma unroll
+    for (int t = 0; t < R4; ++t)
+        if (t * kWave < n4) {
+            const int tt = t * kWave + lane < n4 ? t * kWave + lane : 0;
+            rv[t] = load_stream(reinterpret_cast<const float4 *>(p + a) + tt);
+        }
+#pragma unroll
+    for (int g = 0; g < QG; ++g)
+        if (g < ngrp) qv[g] = load_stream(reinterpret_cast<const uint4 *>(pm.qs + q0) + g * kWave + lane);
+#pragma unroll
+    for (int t = 0; t < R4; ++t)
+        if (t * kWave < n4 && t * kWave + lane < n4) reinterpret_cast<float4 *>(sr)[t * kWave + lane] = rv[t];
+    wave_sync();
+    float acc = 0.0f;
+#pragma unroll
+    for (int g = 0; g < QG; ++g) {
+        if (g >= ngrp) break;  // wave-uniform
+        const uint32_t qq[4] = {qv[g].x, qv[g].y, qv[g].z, qv[g].w};
+        float x[8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            x[2 * u] = sr[qq[u] & 0xFFFFu];
+            x[2 * u + 1] = sr[qq[u] >> 16];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const float t = acc + x[u];
+            acc = (g * 8 + u < len) ? t : acc;
+        }
+    }
+    if (valid) resid[my] = sigmoid_ref(acc) - y;
+}
+
+// PM (with FUSED): after the update, form the NEXT batch's products of this
+// workgroup's slice (pm_pass1 below) from the new weights.
+template <int FILL, bool FUSED, bool NTW, bool PM = false>
 __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int64_t D, int64_t B,
                                                                 const float *__restrict__ resid,
                                                                 float *__restrict__ w, float *__restrict__ gout,
-                                                                float Bf, double Bd, float lr, float C) {
+                                                                float Bf, double Bd, float lr, float C,
+                                                                DevPm pn = DevPm{}, float *__restrict__ pm_p = nullptr) {
     constexpr int R = FILL * 4096;
     constexpr int NG = kGradNG;
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -700,6 +866,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     const int P = pc.phases;
     const int64_t ng = (D + 63) / 64;
     const int64_t gfirst = (int64_t)blockIdx.x * (kGradWaves * NG) + wv;
+    PmPass1<kGradWaves * kWave, 4> pm;
     unsigned bs[NG][2], off[NG][2], cnt[NG][2], nblk[NG][2];
     float acc[NG], wj[NG];
     ushort4 rq[NG][2];
@@ -757,6 +924,12 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     DLR_STAMP(0);
     windows(0);
     fill(0);
+    if (PM) {
+        // the next batch's slice list: in flight under the whole gradient
+        asm volatile("" ::: "memory");
+        pm.load(pn, blockIdx.x);
+        asm volatile("" ::: "memory");
+    }
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
         if (p >= P) break;  // uniform
@@ -765,7 +938,10 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
             DLR_STAMP(3);
             fill((int64_t)p * R);  // resid is padded to P*R floats
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (PM && p == 0)  // the fill, not the pass-1 loads issued after it
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(decltype(pm)::kLoads) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         DLR_STAMP(1 + 3 * p);
 #pragma unroll
@@ -826,6 +1002,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     __syncthreads();
     DLR_STAMP(5);
 #endif
+    if (PM) __syncthreads();  // every wave is done with s_r: pass 1 reuses it
 #pragma unroll
     for (int gi = 0; gi < NG; ++gi) {
         const int64_t j = (gfirst + kGradWaves * gi) * 64 + lane;
@@ -835,10 +1012,17 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
         const float g = (float)((double)acc[gi] / Bd + (double)l2);
         if (FUSED) {
             const float step = lr * g;
-            w[j] = wj[gi] - step;
+            const float wn = wj[gi] - step;
+            w[j] = wn;
+            if (PM) smem[(wv + kGradWaves * gi) * 64 + lane] = wn;  // column j - kPmSlice*blockIdx.x
         } else {
             gout[j] = g;
         }
+    }
+    if (PM) {
+        pm.stage_offsets(reinterpret_cast<uint32_t *>(smem + kPmSlice));
+        __syncthreads();
+        pm.store(pn, smem, reinterpret_cast<const uint32_t *>(smem + kPmSlice), pm_p);
     }
 }
 
@@ -1973,6 +2157,59 @@ hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float 
             return hipErrorInvalidValue;
     }
 #undef DLR_GL
+    return hipGetLastError();
+}
+
+hipError_t launch_pm_products(const DevPm &pm, const float *w, int64_t D, float *p, hipStream_t s) {
+    if (pm.S <= 0) return hipSuccess;
+    if (pm.nblk > kPmMaxBlocks || pm.split < 1) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)(((pm.S + 7) / 8) * 8 * pm.split);
+    hipLaunchKernelGGL(k_pm_products, dim3(grid), dim3(1024), 0, s, pm, w, D, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_pm_margin(const DevPm &pm, const DevBatch &bt, const float *p, float *resid, hipStream_t s) {
+    if (bt.rows <= 0) return hipSuccess;
+    if ((bt.rows + kPmRows - 1) / kPmRows != pm.nblk) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)((pm.nblk + 3) / 4));
+    if (pm.groups <= 4)
+        hipLaunchKernelGGL((k_pm_margin<4>), grid, dim3(256), 0, s, pm, bt, p, resid);
+    else if (pm.groups <= 8)
+        hipLaunchKernelGGL((k_pm_margin<8>), grid, dim3(256), 0, s, pm, bt, p, resid);
+    else if (pm.groups <= kPmMaxGroups)
+        hipLaunchKernelGGL((k_pm_margin<kPmMaxGroups>), grid, dim3(256), 0, s, pm, bt, p, resid);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const float *resid, float *w, float lr,
+                              float C, const DevPm &next, float *p, hipStream_t s) {
+    if (D <= 0) return hipSuccess;
+    const int64_t ng = (D + 63) / 64;
+    const unsigned grid = (unsigned)((ng + kGradWaves * kGradNG - 1) / (kGradWaves * kGradNG));
+    static_assert(kGradWaves * kGradNG * 64 == kPmSlice, "a gradient workgroup's columns are one slice");
+    if ((int64_t)grid != next.S || next.nblk > kPmMaxBlocks) return hipErrorInvalidValue;
+    const dim3 blk(kGradWaves * kWave);
+    const float Bf = (float)B;
+    const double Bd = (double)B;
+    const int fill = grad_lds_fill(B);
+    const size_t lds = std::max((size_t)fill * 4096 * 4 + (size_t)kGradWaves * kBlkPad * 4,
+                                (size_t)(kPmSlice + kPmMaxBlocks) * 4);
+#define DLR_GLP(F)                                                                                            \
+    case F:                                                                                                   \
+        hipLaunchKernelGGL((k_grad_lds<F, true, false, true>), dim3(grid), blk, lds, s, pc, D, B, resid, w,   \
+                           nullptr, Bf, Bd, lr, C, next, p);                                                 \
+        break;
+    switch (fill) {
+        DLR_GLP(1)
+        DLR_GLP(2)
+        DLR_GLP(4)
+        DLR_GLP(8)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef DLR_GLP
     return hipGetLastError();
 }
 

@@ -42,7 +42,7 @@ SYMBOLS = [
     "dlr_set_weights", "dlr_get_weights", "dlr_load_train", "dlr_load_test", "dlr_load_train_dense",
     "dlr_load_test_dense", "dlr_set_residency", "dlr_train_residency",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
-    "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_train_band_rows", "dlr_train_relabeled", "dlr_train_unit_values",
+    "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_train_band_rows", "dlr_train_relabeled", "dlr_train_unit_values", "dlr_train_product_margin",
     "dlr_memory_info",
 ]
 
@@ -155,6 +155,7 @@ _sig("dlr_train_layout", C.c_int, P)
 _sig("dlr_train_band_rows", C.c_int, P)
 _sig("dlr_train_relabeled", C.c_int, P)
 _sig("dlr_train_unit_values", C.c_int, P)
+_sig("dlr_train_product_margin", C.c_int, P)
 _sig("dlr_memory_info", C.c_int, P, C.POINTER(i64), C.POINTER(i64))
 
 
@@ -559,6 +560,14 @@ class Engine:
         rc = lib.dlr_train_unit_values(self._h)
         self._c(min(rc, 0))
         return rc == 1
+
+    def train_product_margin(self) -> int:
+        """0: gather margin; 1: product margin with a separate pass 1; 2:
+        product margin with pass 1 fused into the previous step's gradient
+        (dlr_train_product_margin)."""
+        rc = lib.dlr_train_product_margin(self._h)
+        self._c(min(rc, 0))
+        return rc
 
     def memory_info(self) -> Tuple[int, int]:
         a, b = i64(), i64()

@@ -346,6 +346,17 @@ int dlr_train_relabeled(dlr_ctx *ctx);
  * is checked the same way on its own. */
 int dlr_train_unit_values(dlr_ctx *ctx);
 
+/* The margin of the loaded sparse training shard: 0 = gathers (one weight
+ * read per entry), 1 = PRODUCT MARGIN with a separate pass 1, 2 = product
+ * margin with pass 1 inside the previous step's gradient (one rank).  The
+ * product margin (LDS-layout batches, >= 128 column slices of 4,096; resident
+ * shards) forms every product fl32(w_j * x_ij) by column slice from LDS-staged
+ * weights, then sums each row's products in column order from LDS: bitwise
+ * the gather margin.  DLR_PM=0 turns it off, DLR_PM=1 on for any batches that
+ * fit; DLR_PM_FUSED=0 keeps pass 1 separate.  Replaces lr.cc:108-114's
+ * Sigmoid_ dot product for these shards (same arithmetic). */
+int dlr_train_product_margin(dlr_ctx *ctx);
+
 /* Device bytes resident for the loaded shards (for reporting). */
 int dlr_memory_info(dlr_ctx *ctx, int64_t *train_bytes, int64_t *test_bytes);
 

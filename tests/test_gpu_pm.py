@@ -1,0 +1,171 @@
+"""Product margin (dlr_kernels.hip "Product margin", dlr_train_product_margin):
+the margin of lr.cc:108-114 formed as products by column slice (pass 1, from
+LDS-staged weights; fused into the previous step's gradient on one rank) and
+row sums from LDS (pass 2).  Same products, same column order of additions
+from +0, so every result must be BITWISE the gather margin's -- and the
+oracle's -- whether pass 1 ran fused (the next batch guessed right), on its
+own (a guess missed, the weights changed in between, world > 1), or not at
+all (DLR_PM=0)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import distlr_amd as dlr
+import oracle
+from engine_driver import run_engine, run_group
+from test_gpu_parity import assert_same_weights, compare_runs, oracle_shard
+
+pytestmark = pytest.mark.gpu
+
+
+def _ragged(seed, D, n, max_len=100, empty=300):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, max_len, size=n)
+    lens[rng.choice(n, empty, replace=False)] = 0
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    col = np.concatenate([np.sort(rng.choice(D, k, replace=False)) for k in lens]).astype(np.int32)
+    val = rng.integers(1, 10001, size=len(col)).astype(np.float32) / np.float32(10000)
+    lab = rng.integers(0, 2, size=n).astype(np.int32)
+    return dlr.Dataset.from_csr(rp, col, val, lab, D)
+
+
+def _mode_of(ds, D, B):
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(dlr.init_weight(D))
+        eng.load_train(ds, B)
+        return eng.train_product_margin()
+    finally:
+        eng.close()
+
+
+@pytest.fixture(params=["fused", "separate"])
+def pm_on(request, monkeypatch):
+    monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
+    monkeypatch.setenv("DLR_PM", "1")
+    monkeypatch.setenv("DLR_PM_FUSED", "1" if request.param == "fused" else "0")
+    return 2 if request.param == "fused" else 1
+
+
+@pytest.mark.parametrize("value_mode", [0, 1])
+@pytest.mark.parametrize("B", [1, 7, 100, 999, 1000, 1001, 2500, -1])
+def test_pm_batch_sizes_and_wraps(pm_on, B, value_mode):
+    # unit (value_mode 0: no value arrays) and fp32 values; batches that
+    # divide N, wrap at the epoch end, or wrap twice (B > N)
+    D = 30000
+    ds = dlr.Dataset.generate(1000, D, 20, value_mode=value_mode, seed=3, stream=1)
+    assert _mode_of(ds, D, B) == pm_on
+    eng = run_engine([ds], D, 3, B, 0.1)
+    orc = oracle.run_worker([oracle_shard(ds, D)], D, 3, B, 0.1)
+    compare_runs(eng, orc)
+
+
+def test_pm_ragged_empty_and_long_rows(pm_on):
+    # rows of 0..99 entries (the slot lists of a block: up to 13 groups of 8)
+    D = 20000
+    ds = _ragged(7, D, 3000)
+    test = _ragged(8, D, 500)
+    eng = run_engine([ds], D, 3, 257, 0.3, test=test, test_interval=1)
+    orc = oracle.run_worker([oracle_shard(ds, D)], D, 3, 257, 0.3, test=oracle_shard(test, D), test_interval=1)
+    compare_runs(eng, orc)
+
+
+def test_pm_rows_too_long_fall_back(monkeypatch):
+    # a row over 128 entries does not fit the slot lists: DLR_PM=1 is an
+    # error, the default quietly keeps the gather margin
+    D = 5000
+    ds = dlr.Dataset.generate(300, D, 200, value_mode=1, seed=5, stream=1)
+    monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
+    monkeypatch.setenv("DLR_PM", "1")
+    with pytest.raises(dlr.DLRError, match="product margin"):
+        _mode_of(ds, D, 64)
+    monkeypatch.delenv("DLR_PM")
+    assert _mode_of(ds, D, 64) == 0
+
+
+def test_pm_guess_misses_and_weight_changes(monkeypatch):
+    # The fused gradient forms the products of batch b+1: steps out of order,
+    # repeated batches, set_weights and predict between steps must all give
+    # the gather margin's bits (DLR_PM=0, same sequence).
+    D = 12000
+    ds = dlr.Dataset.generate(2000, D, 24, value_mode=1, seed=11, stream=1)
+    test = dlr.Dataset.generate(300, D, 24, value_mode=1, seed=11, stream=2)
+    rng = np.random.default_rng(3)
+    nb = 4
+    order = [0, 1, 2, 3, 0, 2, 2, 1, 3, 0, 0, 1, 2, 3]
+    perturb = {5: rng.standard_normal(D).astype(np.float32) * np.float32(0.01), 9: None}
+
+    def run(pm):
+        monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
+        monkeypatch.setenv("DLR_PM", pm)
+        eng = dlr.Engine(D)
+        try:
+            eng.set_weights(dlr.init_weight(D))
+            assert eng.load_train(ds, 500) == nb
+            eng.load_test(test)
+            assert eng.train_product_margin() == (2 if pm == "1" else 0)
+            out = []
+            for k, b in enumerate(order):
+                if k in perturb:
+                    w = eng.get_weights()
+                    if perturb[k] is not None:
+                        eng.set_weights(w + perturb[k])
+                    else:
+                        out.append(eng.predict())
+                eng.train_step(b, 0.2, 1.0)
+                out.append(eng.get_weights())
+            return out
+        finally:
+            eng.close()
+
+    got, ref = run("1"), run("0")
+    for a, b in zip(got, ref):
+        if isinstance(a, tuple):
+            assert a == b
+        else:
+            assert_same_weights(a, b)
+
+
+@pytest.mark.parametrize("mode", [dlr.MODE_SYNC_MEAN, dlr.MODE_SYNC_LAST, dlr.MODE_ASYNC])
+@pytest.mark.parametrize("W", [2, 3])
+def test_pm_world_gt_1(pm_on, W, mode):
+    # world > 1 (loopback group): the gradient is not fused with the update,
+    # so pass 1 runs on its own every step (mode 1 whatever DLR_PM_FUSED)
+    D = 9000
+    shards = [dlr.Dataset.generate(1200, D, 18, value_mode=1, seed=13, stream=r + 1) for r in range(W)]
+    eng = run_group(shards, D, 2, 300, 0.2, mode=mode)
+    orc = oracle.run_worker([oracle_shard(s, D) for s in shards], D, 2, 300, 0.2, mode=mode)
+    assert_same_weights(eng.w, orc.w)
+
+
+def test_pm_parameter_server_topology(pm_on):
+    # W workers through dlr_worker_gradient / dlr_server_apply
+    D = 9000
+    shards = [dlr.Dataset.generate(1200, D, 18, value_mode=1, seed=17, stream=r + 1) for r in range(2)]
+    eng = run_engine(shards, D, 2, 300, 0.2)
+    orc = oracle.run_worker([oracle_shard(s, D) for s in shards], D, 2, 300, 0.2)
+    compare_runs(eng, orc)
+
+
+def test_pm_default_on_c2_shape():
+    # The headline shape turns the product margin on by default (245 column
+    # slices); two epochs + a step vs the gather margin and the oracle.
+    D = 1_000_000
+    ds = dlr.Dataset.generate(200_000, D, 50, value_mode=1, seed=12, stream=1)
+    rp, col, val, lab = ds.csr()
+    w0 = dlr.init_weight(D)
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(w0)
+        nb = eng.load_train(ds, 65536)
+        assert eng.train_layout() == dlr.LAYOUT_LDS and eng.train_product_margin() == 2
+        w = w0.copy()
+        for b in range(2 * nb + 1):
+            bb = b % nb
+            eng.train_step(bb, 0.2, 1.0)
+            g = oracle.grad_csr((rp, col, val), lab, oracle.batch_rows(len(lab), 65536, bb), w)
+            oracle.server_update(w, [g], 0.2)
+        assert_same_weights(eng.get_weights(), w)
+    finally:
+        eng.close()
