@@ -1171,6 +1171,15 @@ bool pm_batch(const CsrView &ds, const dlr::BatchSpan &sp, int64_t D, bool unit,
         }
     }
     o.qoff[(size_t)nblk] = (uint32_t)o.qs.size();
+    // pack the entries in groups of four (dlr_kernels.h DevPm)
+    for (size_t g = 0; g < E / 4; ++g) {
+        const uint32_t *e = o.list.data() + 4 * g;
+        const uint32_t k = (e[0] >> 12) & 1023u, j4 = (e[0] >> 22) / 4;
+        const uint32_t c0 = e[0] & 0xFFFu, c1 = e[1] & 0xFFFu, c2 = e[2] & 0xFFFu, c3 = e[3] & 0xFFFu;
+        o.list[2 * g] = c0 | c1 << 12 | (c2 & 0xFFu) << 24;
+        o.list[2 * g + 1] = c2 >> 8 | c3 << 4 | k << 16 | j4 << 26;
+    }
+    o.list.resize(E / 2);
     return true;
 }
 
@@ -1273,7 +1282,7 @@ dlr::DevPm pm_view(const dlr_ctx *c, int64_t b) {
     const TrainShard &t = c->train;
     dlr::DevPm v{};
     v.lbeg = t.pm_lbeg + b * (t.pmS + 1);
-    v.list = t.pm_list + t.pmo_list[(size_t)b];
+    v.list = t.pm_list + t.pmo_list[(size_t)b] / 2;  // two words per group of four entries
     v.val = t.pm_val ? t.pm_val + t.pmo_list[(size_t)b] : nullptr;
     v.pofs = t.pm_pofs + t.pmo_pofs[(size_t)b];
     v.rg = t.pm_rg + t.pmo_rg[(size_t)b];
@@ -1918,7 +1927,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 int64_t pcap = 0, maxslice = 0;
                 for (int64_t b = 0; b < nb; ++b) {
                     const PmBatch &q = pm[(size_t)b];
-                    t.pmo_list[(size_t)b + 1] = t.pmo_list[(size_t)b] + (int64_t)q.list.size();
+                    t.pmo_list[(size_t)b + 1] = t.pmo_list[(size_t)b] + (int64_t)q.list.size() * 2;  // entries
                     t.pmo_pofs[(size_t)b + 1] = t.pmo_pofs[(size_t)b] + (int64_t)q.pofs.size();
                     t.pmo_rg[(size_t)b + 1] = t.pmo_rg[(size_t)b] + (int64_t)q.rg.size();
                     t.pmo_qs[(size_t)b + 1] = t.pmo_qs[(size_t)b] + (int64_t)q.qs.size();
@@ -1938,7 +1947,9 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                     std::copy(pm[(size_t)b].lbeg.begin(), pm[(size_t)b].lbeg.end(), lbeg.begin() + b * (S + 1));
                 if ((rc = upload(c, &t.pm_lbeg, lbeg.data(), lbeg.size()))) return rc;
                 {
-                    std::vector<uint32_t> v = cat32(&PmBatch::list, t.pmo_list);
+                    std::vector<int64_t> words(t.pmo_list.size());
+                    for (size_t b = 0; b < words.size(); ++b) words[b] = t.pmo_list[b] / 2;
+                    std::vector<uint32_t> v = cat32(&PmBatch::list, words);
                     if ((rc = upload(c, &t.pm_list, v.data(), v.size(), 64))) return rc;
                 }
                 if (!t.unit) {
@@ -1967,7 +1978,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 }
                 if ((rc = dev_alloc(c, (void **)&t.pm_p, (size_t)(pcap + 64) * 4))) return rc;
                 HIPC(c, hipMemsetAsync(t.pm_p, 0, (size_t)(pcap + 64) * 4, c->stream));
-                csc_bytes += (int64_t)(lbeg.size() * 4 + t.pmo_list.back() * (t.unit ? 4 : 8) +
+                csc_bytes += (int64_t)(lbeg.size() * 4 + t.pmo_list.back() * (t.unit ? 2 : 6) +
                                        t.pmo_pofs.back() * 4 + t.pmo_rg.back() * 8 + t.pmo_qs.back() * 2 + pcap * 4);
                 t.pm = true;
                 const char *pf = getenv("DLR_PM_FUSED");

@@ -119,11 +119,13 @@ struct DevLPhase {
 // block k's products fill its REGION [rg[k], rg[k+1]) (4-aligned, <=
 // kPmCap), one chunk per slice (chunks ordered by the XCD of their slice's
 // workgroup; each padded to a multiple of 4 slots), rows ascending within a
-// chunk.  Pass 1 (workgroup = slice s) forms slice s's products: list
-// entries [lbeg[s], lbeg[s+1]) of list/val (multiples of 4), entry =
-// (column within slice | block << 12 | rank in chunk << 22), the chunk of
-// block k starting at p[pofs[s*nblk + k]]; padding entries (column 0,
-// value 0) complete each chunk's last 4-slot group.  Pass 2 (wave = block)
+// chunk.  Pass 1 (workgroup = slice s) forms slice s's products: entries
+// [lbeg[s], lbeg[s+1]) (multiples of 4) of val and, in groups of four, of
+// list -- two words per group: the four columns within the slice (12 bits
+// each, bits 0-47), the block k (bits 48-57) and the group's rank in its
+// chunk / 4 (bits 58-63); the chunk of block k starts at p[pofs[s*nblk + k]];
+// padding entries (column 0, value 0) complete each chunk's last group.
+// Pass 2 (wave = block)
 // copies its region into LDS and each lane adds its row's products in
 // column order through its slot list: qs[qoff[k] + (i/8)*512 + lane*8 + i%8]
 // = region slot of the row's i-th entry (qoff[k+1] - qoff[k] = 512 * groups).
@@ -131,11 +133,11 @@ constexpr int kPmSlice = 4096;
 constexpr int kPmRows = 64;
 constexpr int kPmCap = 4096;
 constexpr int kPmMaxGroups = 16;  // rows of up to 128 entries
-constexpr int kPmMaxChunk = 1024;
+constexpr int kPmMaxChunk = 256;  // slots (rank / 4 in 6 bits)
 constexpr int kPmMaxBlocks = 1024;
 struct DevPm {
     const uint32_t *lbeg;  // S + 1, relative to list/val
-    const uint32_t *list;
+    const uint32_t *list;  // 2 words per group of 4 entries
     const float *val;      // null: unit values
     const uint32_t *pofs;  // S x nblk
     const uint32_t *rg;    // nblk + 1

@@ -706,7 +706,7 @@ constexpr int kBlkPad = kBlk + 8;  // product slab per wave: lane reads at o + [
 template <int NT, int U>
 struct PmPass1 {
     static constexpr int NPO = (kPmMaxBlocks + NT - 1) / NT;
-    uint4 pk[U];
+    uint2 pk[U];  // a group: four 12-bit columns within the slice, block, rank / 4 (DevPm)
     float4 v[U];
     uint32_t po[NPO];
     uint32_t c0 = 0, c1 = 0;
@@ -715,13 +715,16 @@ struct PmPass1 {
     // s_waitcnt vmcnt(kLoads) while these are still in flight
     static constexpr int kLoads = NPO + 2 * U;
     __device__ __forceinline__ void fetch(const DevPm &pm, uint32_t g0) {
-        const float *vp = pm.val ? pm.val : reinterpret_cast<const float *>(pm.list);
+        // unit values: a dummy load (the list's own words, in range) keeps
+        // the instruction count fixed
+        const float4 *vp = pm.val ? reinterpret_cast<const float4 *>(pm.val) : reinterpret_cast<const float4 *>(pm.list);
+        const uint32_t vs = pm.val ? 0u : 1u;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t g = g0 + u * NT + threadIdx.x;
             const uint32_t gc = g < c1 ? g : c0;
-            pk[u] = load_stream(reinterpret_cast<const uint4 *>(pm.list) + gc);
-            v[u] = load_stream(reinterpret_cast<const float4 *>(vp) + gc);
+            pk[u] = load_stream(reinterpret_cast<const uint2 *>(pm.list) + gc);
+            v[u] = load_stream(vp + (gc >> vs));
         }
     }
     __device__ __forceinline__ void load(const DevPm &pm, int s, int part = 0, int nparts = 1) {
@@ -755,13 +758,14 @@ struct PmPass1 {
             for (int u = 0; u < U; ++u) {
                 const uint32_t g = g0 + u * NT + threadIdx.x;
                 if (g < c1) {
-                    const uint32_t k = (pk[u].x >> 12) & (kPmMaxBlocks - 1);
+                    const uint32_t x = pk[u].x, y = pk[u].y;
+                    const uint32_t k = (y >> 16) & (kPmMaxBlocks - 1), j = (y >> 26) * 4;
                     float4 q;
-                    q.x = s_w[pk[u].x & (kPmSlice - 1)] * (unit ? 1.0f : v[u].x);
-                    q.y = s_w[pk[u].y & (kPmSlice - 1)] * (unit ? 1.0f : v[u].y);
-                    q.z = s_w[pk[u].z & (kPmSlice - 1)] * (unit ? 1.0f : v[u].z);
-                    q.w = s_w[pk[u].w & (kPmSlice - 1)] * (unit ? 1.0f : v[u].w);
-                    *reinterpret_cast<float4 *>(p + s_po[k] + (pk[u].x >> 22)) = q;
+                    q.x = s_w[x & 0xFFFu] * (unit ? 1.0f : v[u].x);
+                    q.y = s_w[(x >> 12) & 0xFFFu] * (unit ? 1.0f : v[u].y);
+                    q.z = s_w[(x >> 24) | ((y & 0xFu) << 8)] * (unit ? 1.0f : v[u].z);
+                    q.w = s_w[(y >> 4) & 0xFFFu] * (unit ? 1.0f : v[u].w);
+                    *reinterpret_cast<float4 *>(p + s_po[k] + j) = q;
                 }
             }
             if (g0 + U * NT < c1) fetch(pm, g0 + U * NT);

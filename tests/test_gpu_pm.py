@@ -30,6 +30,10 @@ def _ragged(seed, D, n, max_len=100, empty=300):
     return dlr.Dataset.from_csr(rp, col, val, lab, D)
 
 
+# Shapes: a (64-row block, 4,096-column slice) chunk holds <= 256 products,
+# so D >= ~1,024 x nnz per row here.
+
+
 def _mode_of(ds, D, B):
     eng = dlr.Engine(D)
     try:
@@ -63,7 +67,7 @@ def test_pm_batch_sizes_and_wraps(pm_on, B, value_mode):
 
 def test_pm_ragged_empty_and_long_rows(pm_on):
     # rows of 0..99 entries (the slot lists of a block: up to 13 groups of 8)
-    D = 20000
+    D = 300_000
     ds = _ragged(7, D, 3000)
     test = _ragged(8, D, 500)
     eng = run_engine([ds], D, 3, 257, 0.3, test=test, test_interval=1)
@@ -88,7 +92,7 @@ def test_pm_guess_misses_and_weight_changes(monkeypatch):
     # The fused gradient forms the products of batch b+1: steps out of order,
     # repeated batches, set_weights and predict between steps must all give
     # the gather margin's bits (DLR_PM=0, same sequence).
-    D = 12000
+    D = 300_000
     ds = dlr.Dataset.generate(2000, D, 24, value_mode=1, seed=11, stream=1)
     test = dlr.Dataset.generate(300, D, 24, value_mode=1, seed=11, stream=2)
     rng = np.random.default_rng(3)
@@ -132,7 +136,7 @@ def test_pm_guess_misses_and_weight_changes(monkeypatch):
 def test_pm_world_gt_1(pm_on, W, mode):
     # world > 1 (loopback group): the gradient is not fused with the update,
     # so pass 1 runs on its own every step (mode 1 whatever DLR_PM_FUSED)
-    D = 9000
+    D = 200_000
     shards = [dlr.Dataset.generate(1200, D, 18, value_mode=1, seed=13, stream=r + 1) for r in range(W)]
     eng = run_group(shards, D, 2, 300, 0.2, mode=mode)
     orc = oracle.run_worker([oracle_shard(s, D) for s in shards], D, 2, 300, 0.2, mode=mode)
@@ -141,7 +145,7 @@ def test_pm_world_gt_1(pm_on, W, mode):
 
 def test_pm_parameter_server_topology(pm_on):
     # W workers through dlr_worker_gradient / dlr_server_apply
-    D = 9000
+    D = 200_000
     shards = [dlr.Dataset.generate(1200, D, 18, value_mode=1, seed=17, stream=r + 1) for r in range(2)]
     eng = run_engine(shards, D, 2, 300, 0.2)
     orc = oracle.run_worker([oracle_shard(s, D) for s in shards], D, 2, 300, 0.2)
