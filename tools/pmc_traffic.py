@@ -83,10 +83,12 @@ def main() -> int:
     # Dense shards (C4): the fused pass is the margin role (it also forms the
     # gradient partials), the chunk combine + update the grad role.  Huge D
     # (C5): the dense L2 pass and the scatter are the update role.
-    roles = [("margin", ["k_margin", "k_dense_fused", "k_dense_margin"]),
+    # Product margin (C2): pass 2 is the margin role, a separate pass 1
+    # (k_pm_products) too; a fused pass 1 is inside k_grad_lds (grad role).
+    roles = [("margin", ["k_margin", "k_pm_margin", "k_pm_products", "k_dense_fused", "k_dense_margin"]),
              ("grad", ["k_grad", "k_long_", "k_band_finalize", "k_dense_grad", "k_dense_combine"]),
              ("update", ["k_dense_l2", "k_scatter", "k_merge_update", "k_sparse_merge"])]
-    steps = len([x for k in roles[0][1] for x in pick(bf, k)]) or 1
+    steps = len([x for k in ["k_margin", "k_pm_margin", "k_dense_fused", "k_dense_margin"] for x in pick(bf, k)]) or 1
     total = 0.0
     for short, keys in roles:
         f = [x for k in keys for x in pick(bf, k)]
