@@ -1919,6 +1919,22 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 if (ok && !pm_batch(src, t.plan[(size_t)b], D, t.unit, pm[(size_t)b])) ok = false;
             });
             if (ok) {
+                // only where it leaves the headroom the residency choice keeps
+                // (8 GiB): else the gather margin, which needs no extra arrays
+                int64_t need = 0;
+                for (const PmBatch &q : pm)
+                    need += (int64_t)(q.list.size() * 4 + q.val.size() * 4 + q.pofs.size() * 4 + q.rg.size() * 8 +
+                                      q.qs.size() * 2 + q.lbeg.size() * 4);
+                size_t fr = 0, tot = 0;
+                HIPC(c, hipMemGetInfo(&fr, &tot));
+                if ((double)need + (double)((size_t)8 << 30) > (double)fr) {
+                    ok = false;
+                    if (pme && strcmp(pme, "1") == 0)
+                        return fail(c, DLR_E_NOMEM, "dlr_load_train: DLR_PM=1 but the product margin's arrays (" +
+                                                        std::to_string((long long)(need >> 20)) + " MiB) do not fit");
+                }
+            }
+            if (ok) {
                 t.pmS = S;
                 t.pmo_list.assign((size_t)nb + 1, 0);
                 t.pmo_pofs.assign((size_t)nb + 1, 0);

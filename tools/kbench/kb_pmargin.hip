@@ -186,6 +186,90 @@ __global__ __launch_bounds__(256) void k_m2(const uint32_t *__restrict__ rg, con
     if (valid) resid[my] = sig(acc) - y;
 }
 
+// pass 2 variants: DMA = region copied into LDS by global_load_lds (no
+// VGPR staging); HALF = two waves per block (each copies half the region and
+// sums 32 rows).
+template <int QG, bool DMA, bool HALF>
+__global__ __launch_bounds__(256) void k_m2v(const uint32_t *__restrict__ rg, const uint32_t *__restrict__ qoff,
+                                             const uint16_t *__restrict__ qs, const int64_t *__restrict__ row_ptr,
+                                             const float *__restrict__ label, int64_t rows,
+                                             const float *__restrict__ p, float *__restrict__ resid) {
+    constexpr int BPW = HALF ? 2 : 4;  // blocks per workgroup
+    __shared__ __attribute__((aligned(16))) float s_reg[BPW][CAP];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int sub = HALF ? (wv & 1) : 0;
+    const int64_t blk = (int64_t)blockIdx.x * BPW + (HALF ? wv >> 1 : wv);
+    const int64_t r0 = blk * RB;
+    if (r0 >= rows) return;
+    const uint32_t a = rg[blk], b = rg[blk + 1];
+    const uint32_t q0 = qoff[blk], q1 = qoff[blk + 1];
+    const int rl = HALF ? sub * 32 + (lane & 31) : lane;
+    const int64_t my = r0 + rl;
+    const bool valid = my < rows && (!HALF || lane < 32);
+    const int64_t mc = my < rows ? my : r0;
+    const int len = valid ? (int)(row_ptr[mc + 1] - row_ptr[mc]) : 0;
+    const float y = label[mc];
+    float *sr = s_reg[HALF ? wv >> 1 : wv];
+    const int n4 = (int)((b - a) >> 2);
+    const int ngrp = (int)((q1 - q0) >> 9);
+    constexpr int R4 = CAP / 4 / 64;
+    uint4 qv[QG];
+    if (DMA) {
+#pragma unroll
+        for (int t = 0; t < R4; ++t) {
+            const int tt = HALF ? 2 * t + sub : t;
+            if (tt * 64 < n4) {
+                const int e = tt * 64 + lane < n4 ? tt * 64 + lane : tt * 64;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(p + a + 4 * e),
+                                                 (__attribute__((address_space(3))) void *)(sr + tt * 256), 16, 0, 0);
+            }
+        }
+    } else {
+        float4 rv[R4];
+#pragma unroll
+        for (int t = 0; t < R4; ++t) {
+            const int tt = HALF ? 2 * t + sub : t;
+            if (tt * 64 < n4) {
+                const int e = tt * 64 + lane < n4 ? tt * 64 + lane : 0;
+                rv[t] = dlr::load_stream(reinterpret_cast<const float4 *>(p + a) + e);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < R4; ++t) {
+            const int tt = HALF ? 2 * t + sub : t;
+            if (tt * 64 < n4 && tt * 64 + lane < n4) reinterpret_cast<float4 *>(sr)[tt * 64 + lane] = rv[t];
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < QG; ++g)
+        if (g < ngrp) qv[g] = dlr::load_stream(reinterpret_cast<const uint4 *>(qs + q0) + g * 64 + rl);
+    if (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (HALF) __syncthreads();
+    else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    float acc = 0.0f;
+#pragma unroll
+    for (int g = 0; g < QG; ++g) {
+        if (g >= ngrp) break;
+        const uint32_t qq[4] = {qv[g].x, qv[g].y, qv[g].z, qv[g].w};
+        float x[8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            x[2 * u] = sr[qq[u] & 0xFFFF];
+            x[2 * u + 1] = sr[qq[u] >> 16];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const float t = acc + x[u];
+            acc = (g * 8 + u < len) ? t : acc;
+        }
+    }
+    if (valid) resid[my] = sig(acc) - y;
+}
+
 }  // namespace kb
 
 int main(int argc, char **argv) {
@@ -375,6 +459,29 @@ int main(int argc, char **argv) {
     timeit("production margin (k_margin_residual)", [&](int bt) { (void)dlr::launch_margin_residual(batch(bt), d_w, d_r1, 0); });
     timeit("pass 1 products (k_prod)", [&](int bt) { prod(bt); });
     timeit("pass 2 row sums (k_m2)", [&](int bt) { m2(bt); });
+#define M2V(DMA, HALF) [&](int bt) { hipLaunchKernelGGL((k_m2v<8, DMA, HALF>), dim3((unsigned)(nblk / (HALF ? 2 : 4))), dim3(256), 0, 0, \
+        d_rg + rg_off[bt], d_qoff + qo_off[bt], d_qs, d_rp + (int64_t)bt * B, d_lab + (int64_t)bt * B, B, d_p, d_r2); }
+    timeit("pass 2 variant plain", M2V(false, false));
+    timeit("pass 2 variant DMA", M2V(true, false));
+    timeit("pass 2 variant 2 waves/block", M2V(false, true));
+    timeit("pass 2 variant DMA + 2 waves/block", M2V(true, true));
+    {
+        // bitwise check of the variants (products from the last pass 1 of batch 0)
+        prod(0);
+        hipLaunchKernelGGL(k_m2<8>, dim3((unsigned)(nblk / 4)), dim3(256), 0, 0, d_rg + rg_off[0], d_qoff + qo_off[0], d_qs, d_rp, d_lab, B, d_p, d_r1);
+        std::vector<float> a(B), b(B);
+        CK(hipMemcpy(a.data(), d_r1, B * 4, hipMemcpyDeviceToHost));
+        const char *nm[4] = {"plain", "DMA", "half", "DMA+half"};
+        for (int v = 0; v < 4; ++v) {
+            if (v == 0) M2V(false, false)(0);
+            if (v == 1) M2V(true, false)(0);
+            if (v == 2) M2V(false, true)(0);
+            if (v == 3) M2V(true, true)(0);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(b.data(), d_r2, B * 4, hipMemcpyDeviceToHost));
+            printf("variant %s: %s\n", nm[v], memcmp(a.data(), b.data(), B * 4) ? "MISMATCH" : "bitwise equal");
+        }
+    }
     timeit("pass 1 + pass 2", [&](int bt) { prod(bt); m2(bt); });
     const unsigned g4 = (unsigned)(((S + 7) / 8) * 8);
     timeit("k_prod abl1 contiguous stores", [&](int bt) { hipLaunchKernelGGL((k_prod<1024, 1, 16, 1>), dim3(g4), dim3(1024), 0, 0, d_lbeg + lb_off[bt], d_list, d_lval, d_pofs + pofs_off[bt], (int)nblk, (int)S, d_w, D, d_p); });
