@@ -234,6 +234,11 @@ struct dlr_ctx {
     std::vector<int32_t> perm;
     int residency = DLR_RESIDENCY_AUTO;
     hipStream_t cstream = nullptr;
+    // band mode, pipelined (band_step_pipelined): the bands' gradient stream,
+    // one event per band's margins, the step start and the bands' end
+    hipStream_t gstream = nullptr;
+    std::vector<hipEvent_t> ev_band;
+    hipEvent_t ev_bstart = nullptr, ev_bdone = nullptr;
     hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
     std::vector<void *> allocs;
     // timing
@@ -1523,6 +1528,88 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
     return e;
 }
 
+// Band mode (row bands; BASELINE C3), pipelined: a band's short-column
+// gradient needs only the residuals of the band's own rows, so the margin
+// runs band by band on the engine stream and each band's gradient kernel
+// runs on a second stream as soon as its rows' margins exist, beside the
+// next band's margin (the margin waits on fabric misses of the cold
+// weights, the band kernel on L2 hits of its residual slice).  The long
+// columns' phases need every residual: they follow the last margin on the
+// engine stream; the update waits for both.  Same kernels, same sums:
+// bitwise the sequential order.  False when the bands do not map onto the
+// rows one to one (the caller then runs margin and gradient in sequence).
+bool band_pipeline_ok(const dlr_ctx *c, int64_t b) {
+    const TrainShard &t = c->train;
+    const char *pe = getenv("DLR_BAND_PIPE");  // "0": margin, then the gradient (A/B)
+    if ((pe && strcmp(pe, "0") == 0) || !t.band_shift || t.touched || t.dense || t.pcsc || t.sparse_stream) return false;
+    const int64_t rows = t.plan[(size_t)b].rows, BR = (int64_t)1 << t.band_shift;
+    return t.bfirst[(size_t)b + 1] - t.bfirst[(size_t)b] == (rows + BR - 1) / BR;
+}
+
+hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, float lr, float C, bool fused) {
+    TrainShard &t = c->train;
+    const size_t bb = (size_t)b;
+    const int64_t nbands = t.bfirst[bb + 1] - t.bfirst[bb];
+    hipError_t e = hipSuccess;
+    if (!c->gstream) {
+        e = hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_bstart, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_bdone, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    while ((int64_t)c->ev_band.size() < nbands) {
+        hipEvent_t ev;
+        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+        c->ev_band.push_back(ev);
+    }
+    const size_t esz = t.row16 ? 2 : 4;
+    const dlr::DevBatch all = batch_view(c, b);
+    const int64_t BR = (int64_t)1 << t.band_shift;
+    // the running sums are cleared on the engine stream (so the long-column
+    // phases below are ordered after it too); the bands' stream starts
+    // after that and everything queued before this step
+    e = hipMemsetAsync(t.gacc, 0, (size_t)c->D * 4, c->stream);
+    if (e == hipSuccess) e = hipEventRecord(c->ev_bstart, c->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->gstream, c->ev_bstart, 0);
+    for (int64_t k = 0; e == hipSuccess && k < nbands; ++k) {
+        const int64_t r0 = k * BR, r1 = std::min(all.rows, r0 + BR);
+        dlr::DevBatch sub = all;
+        sub.row_ptr = all.row_ptr + r0;
+        sub.label = all.label + r0;
+        sub.rows = r1 - r0;
+        sub.nnz = all.rows > 0 ? all.nnz * sub.rows / all.rows : 0;  // the margin's rows-per-wave heuristic
+        e = t.margin_hot ? dlr::launch_margin_hot(sub, c->w, c->D, c->resid + r0, c->stream)
+                         : dlr::launch_margin_residual(sub, c->w, c->resid + r0, c->stream);
+        if (e == hipSuccess) e = hipEventRecord(c->ev_band[(size_t)k], c->stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(c->gstream, c->ev_band[(size_t)k], 0);
+        if (e == hipSuccess) {
+            const TrainShard::Band &bd = t.bands[(size_t)(t.bfirst[bb] + k)];
+            dlr::DevBand dv{t.bcols + bd.pair, t.bptr + bd.ptr, t.bws + bd.ws, (const char *)t.brow + esz * (size_t)bd.ent,
+                            t.bval ? t.bval + bd.ent : nullptr, bd.nwaves, t.row16};
+            e = dlr::launch_grad_band(dv, c->resid, t.gacc, c->gstream);
+        }
+    }
+    if (e == hipSuccess) e = hipEventRecord(c->ev_bdone, c->gstream);
+    const int64_t nl = t.any_long ? t.lcoff[bb + 1] - t.lcoff[bb] : 0;
+    if (e == hipSuccess && nl > 0 && t.lnph > 0) {
+        dlr::DevLPhase lp{t.lpdesc + b * t.lnph, reinterpret_cast<const uint2 *>(t.lpptr), t.lpws, t.lprow, t.lpval,
+                          t.lnph, (uint32_t)t.lnpart};
+        e = dlr::launch_long_phase(lp, t.lcols + t.lcoff[bb], t.lcseg + (t.lcoff[bb] + (int64_t)b), nl, c->resid,
+                                   t.lpart, t.gacc, c->stream);
+    } else if (e == hipSuccess && nl > 0) {
+        dlr::DevLong lg{t.lcols + t.lcoff[bb], t.lcseg + (t.lcoff[bb] + (int64_t)b), t.lsptr + t.lsoff[bb],
+                        (const char *)t.lrow + esz * (size_t)t.leoff[bb], t.lval ? t.lval + t.leoff[bb] : nullptr, nl,
+                        t.lsoff[bb + 1] - t.lsoff[bb] - 1, t.row16};
+        if (t.lsched) lg.sched = t.lsched + t.lsoff[bb];
+        // the long columns' raw sums go to their own gacc entries (disjoint
+        // from the short columns' the bands write)
+        e = dlr::launch_grad_long(lg, B, c->resid, c->w, gout, t.lpart, lr, C, fused, c->stream, t.gacc);
+    }
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_bdone, 0);
+    if (e == hipSuccess) e = dlr::launch_band_finalize(t.gacc, c->w, gout, c->D, B, lr, C, fused, c->stream);
+    return e;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1628,6 +1715,7 @@ void dlr_destroy(dlr_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->cstream) (void)hipStreamSynchronize(ctx->cstream);
+    if (ctx->gstream) (void)hipStreamSynchronize(ctx->gstream);
     free_train(ctx);  // unregisters a streamed shard's host rows
     delete ctx->comm;  // RCCL: ncclCommDestroy; loopback: drops the group reference
     for (void *p : ctx->allocs) (void)hipFree(p);
@@ -1638,6 +1726,10 @@ void dlr_destroy(dlr_ctx *ctx) {
         if (ctx->ev_ready[k]) (void)hipEventDestroy(ctx->ev_ready[k]);
         if (ctx->ev_free[k]) (void)hipEventDestroy(ctx->ev_free[k]);
     }
+    for (hipEvent_t e : ctx->ev_band) (void)hipEventDestroy(e);
+    if (ctx->ev_bstart) (void)hipEventDestroy(ctx->ev_bstart);
+    if (ctx->ev_bdone) (void)hipEventDestroy(ctx->ev_bdone);
+    if (ctx->gstream) (void)hipStreamDestroy(ctx->gstream);
     if (ctx->cstream) (void)hipStreamDestroy(ctx->cstream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -2439,10 +2531,31 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
         HIPC(c, sparse_batch(c, b));  // binds the batch's slot (the views below)
         HIPC(c, build_layout(c, b));
     }
-    time_begin(c, &t0);
-    HIPC(c, launch_margin(c, b));
-    time_end(c, 0, t0);
-    if (c->train.touched) {
+    const bool piped = band_pipeline_ok(c, b);  // margin and band gradients interleaved (band mode)
+    if (!piped) {
+        time_begin(c, &t0);
+        HIPC(c, launch_margin(c, b));
+        time_end(c, 0, t0);
+    }
+    if (piped) {
+        // the margin, the gradient and (one rank) the update: one timed stage
+        time_begin(c, &t0);
+        HIPC(c, band_step_pipelined(c, b, bt.rows, c->comm ? c->g : nullptr, lr, C, !c->comm));
+        time_end(c, 1, t0);
+        if (c->comm) {
+            time_begin(c, &t0);
+            COMMC(c, all_to_all(c->g, c->recv, (size_t)c->chunk, c->stream, e_));
+            time_end(c, 3, t0);
+            int64_t kb, ke;
+            dlr_key_range(c->D, c->world, c->rank, &kb, &ke);
+            time_begin(c, &t0);
+            HIPC(c, dlr::launch_merge_update(c->recv, c->world, c->chunk, ke - kb, c->w + kb, lr, mode, c->stream));
+            time_end(c, 2, t0);
+            time_begin(c, &t0);
+            COMMC(c, all_gather(c->w + (int64_t)c->rank * c->chunk, c->w, (size_t)c->chunk, c->stream, e_));
+            time_end(c, 3, t0);
+        }
+    } else if (c->train.touched) {
         // touched columns (ordered gradient), then the dense L2 pass over
         // all D, then the touched columns' new weights (dlr_kernels.hip
         // "Touched-column layout").

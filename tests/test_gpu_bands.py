@@ -138,6 +138,21 @@ def test_c3_bands_long_phases_within_tolerance(monkeypatch, W):
     assert_same_weights(again.w, got.w)
 
 
+@pytest.mark.parametrize("W", [1, 2])
+def test_band_pipeline_bitwise_vs_sequential(monkeypatch, W):
+    # band mode runs the margin band by band with each band's gradient on a
+    # second stream beside the next band's margin, the long-column phases
+    # after the last margin (DLR_BAND_PIPE=0: margin, then gradient): the
+    # same kernels on the same data -- bitwise the same weights
+    D = 1 << 24
+    shards = _c3_shards(W, rows=80_000)
+    monkeypatch.setenv("DLR_BAND_ROWS", "8192")
+    got = run_engine(shards, D, 3, -1, 0.2)
+    monkeypatch.setenv("DLR_BAND_PIPE", "0")
+    ref = run_engine(shards, D, 3, -1, 0.2)
+    assert_same_weights(got.w, ref.w)
+
+
 def test_c3_banded_pushed_gradient(monkeypatch):
     # the N > 1 path's pushed gradient (non-fused finalize): short columns
     # bitwise the unbanded classic kernel's, long columns within 1e-5 of the
