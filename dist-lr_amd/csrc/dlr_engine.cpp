@@ -1470,6 +1470,28 @@ dlr::DevCsc csc_view(const dlr_ctx *c, int64_t b) {
     return cs;
 }
 
+// The long columns of batch b (classic layout, §3's chunked option): in row
+// phases (band mode: raw sums into gacc) or in chunks.
+hipError_t launch_long_columns(dlr_ctx *c, int64_t b, int64_t B, float *gout, float lr, float C, bool fused) {
+    const TrainShard &t = c->train;
+    const size_t bb = (size_t)b;
+    const size_t esz = t.row16 ? 2 : 4;
+    const int64_t nl = t.any_long ? t.lcoff[bb + 1] - t.lcoff[bb] : 0;
+    if (nl <= 0) return hipSuccess;
+    if (t.lnph > 0) {
+        dlr::DevLPhase lp{t.lpdesc + b * t.lnph, reinterpret_cast<const uint2 *>(t.lpptr), t.lpws, t.lprow, t.lpval,
+                          t.lnph, (uint32_t)t.lnpart};
+        return dlr::launch_long_phase(lp, t.lcols + t.lcoff[bb], t.lcseg + (t.lcoff[bb] + (int64_t)b), nl, c->resid,
+                                      t.lpart, t.gacc, c->stream);
+    }
+    dlr::DevLong lg{t.lcols + t.lcoff[bb], t.lcseg + (t.lcoff[bb] + (int64_t)b), t.lsptr + t.lsoff[bb],
+                    (const char *)t.lrow + esz * (size_t)t.leoff[bb], t.lval ? t.lval + t.leoff[bb] : nullptr, nl,
+                    t.lsoff[bb + 1] - t.lsoff[bb] - 1, t.row16};
+    if (t.lsched) lg.sched = t.lsched + t.lsoff[bb];
+    return dlr::launch_grad_long(lg, B, c->resid, c->w, gout, t.lpart, lr, C, fused, c->stream,
+                                 t.band_shift ? t.gacc : nullptr);
+}
+
 hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float lr, float C, bool fused) {
     const TrainShard &t = c->train;
     if (t.dense) {
@@ -1510,19 +1532,7 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
     } else {
         e = dlr::launch_grad(csc_view(c, b), c->D, c->resid, c->w, gout, B, lr, C, fused, c->stream);
     }
-    const int64_t nl = t.any_long ? t.lcoff[bb + 1] - t.lcoff[bb] : 0;
-    if (e == hipSuccess && nl > 0 && t.lnph > 0) {
-        dlr::DevLPhase lp{t.lpdesc + b * t.lnph, reinterpret_cast<const uint2 *>(t.lpptr), t.lpws, t.lprow, t.lpval, t.lnph, (uint32_t)t.lnpart};
-        e = dlr::launch_long_phase(lp, t.lcols + t.lcoff[bb], t.lcseg + (t.lcoff[bb] + (int64_t)b), nl, c->resid,
-                                   t.lpart, t.gacc, c->stream);
-    } else if (e == hipSuccess && nl > 0) {
-        dlr::DevLong lg{t.lcols + t.lcoff[bb], t.lcseg + (t.lcoff[bb] + (int64_t)b), t.lsptr + t.lsoff[bb],
-                        (const char *)t.lrow + esz * (size_t)t.leoff[bb], t.lval ? t.lval + t.leoff[bb] : nullptr, nl,
-                        t.lsoff[bb + 1] - t.lsoff[bb] - 1, t.row16};
-        if (t.lsched) lg.sched = t.lsched + t.lsoff[bb];
-        e = dlr::launch_grad_long(lg, B, c->resid, c->w, gout, t.lpart, lr, C, fused, c->stream,
-                                  t.band_shift ? t.gacc : nullptr);
-    }
+    if (e == hipSuccess) e = launch_long_columns(c, b, B, gout, lr, C, fused);
     if (e == hipSuccess && t.band_shift)
         e = dlr::launch_band_finalize(t.gacc, c->w, gout, c->D, B, lr, C, fused, c->stream);
     return e;
@@ -1590,21 +1600,9 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
         }
     }
     if (e == hipSuccess) e = hipEventRecord(c->ev_bdone, c->gstream);
-    const int64_t nl = t.any_long ? t.lcoff[bb + 1] - t.lcoff[bb] : 0;
-    if (e == hipSuccess && nl > 0 && t.lnph > 0) {
-        dlr::DevLPhase lp{t.lpdesc + b * t.lnph, reinterpret_cast<const uint2 *>(t.lpptr), t.lpws, t.lprow, t.lpval,
-                          t.lnph, (uint32_t)t.lnpart};
-        e = dlr::launch_long_phase(lp, t.lcols + t.lcoff[bb], t.lcseg + (t.lcoff[bb] + (int64_t)b), nl, c->resid,
-                                   t.lpart, t.gacc, c->stream);
-    } else if (e == hipSuccess && nl > 0) {
-        dlr::DevLong lg{t.lcols + t.lcoff[bb], t.lcseg + (t.lcoff[bb] + (int64_t)b), t.lsptr + t.lsoff[bb],
-                        (const char *)t.lrow + esz * (size_t)t.leoff[bb], t.lval ? t.lval + t.leoff[bb] : nullptr, nl,
-                        t.lsoff[bb + 1] - t.lsoff[bb] - 1, t.row16};
-        if (t.lsched) lg.sched = t.lsched + t.lsoff[bb];
-        // the long columns' raw sums go to their own gacc entries (disjoint
-        // from the short columns' the bands write)
-        e = dlr::launch_grad_long(lg, B, c->resid, c->w, gout, t.lpart, lr, C, fused, c->stream, t.gacc);
-    }
+    // the long columns' raw sums go to their own gacc entries (disjoint from
+    // the short columns' the bands write)
+    if (e == hipSuccess) e = launch_long_columns(c, b, B, gout, lr, C, fused);
     if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_bdone, 0);
     if (e == hipSuccess) e = dlr::launch_band_finalize(t.gacc, c->w, gout, c->D, B, lr, C, fused, c->stream);
     return e;
