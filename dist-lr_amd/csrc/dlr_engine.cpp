@@ -2042,6 +2042,8 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                     t.pm_groups = std::max(t.pm_groups, q.groups);
                 }
                 t.pm_split = (int)std::min<int64_t>(16, std::max<int64_t>(1, (maxslice + 16383) / 16384));
+                if (const char *sp = getenv("DLR_PM_SPLIT"))  // A/B: pass-1 workgroups per slice (separate pass)
+                    t.pm_split = std::max(t.pm_split, std::min(16, std::max(1, atoi(sp))));
                 auto cat32 = [&](std::vector<uint32_t> PmBatch::*f, const std::vector<int64_t> &off) {
                     std::vector<uint32_t> v((size_t)off.back());
                     for (int64_t b = 0; b < nb; ++b)
