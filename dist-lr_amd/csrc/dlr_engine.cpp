@@ -2044,49 +2044,33 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 t.pm_split = (int)std::min<int64_t>(16, std::max<int64_t>(1, (maxslice + 16383) / 16384));
                 if (const char *sp = getenv("DLR_PM_SPLIT"))  // A/B: pass-1 workgroups per slice (separate pass)
                     t.pm_split = std::max(t.pm_split, std::min(16, std::max(1, atoi(sp))));
-                auto cat32 = [&](std::vector<uint32_t> PmBatch::*f, const std::vector<int64_t> &off) {
-                    std::vector<uint32_t> v((size_t)off.back());
-                    for (int64_t b = 0; b < nb; ++b)
-                        std::copy(((pm[(size_t)b]).*f).begin(), ((pm[(size_t)b]).*f).end(), v.begin() + off[(size_t)b]);
-                    return v;
+                // one device array per member: the batches' parts back to back
+                // (offsets off[b] / div elements), each batch's host part
+                // released once copied, so the host peak stays ~1x the layout
+                auto cat_upload = [&](auto member, auto **dst, const std::vector<int64_t> &off, int64_t div,
+                                      size_t pad) -> int {
+                    using V = std::remove_reference_t<decltype(pm[0].*member)>;
+                    V v((size_t)(off.back() / div));
+                    for (int64_t b = 0; b < nb; ++b) {
+                        V &src = pm[(size_t)b].*member;
+                        std::copy(src.begin(), src.end(), v.begin() + off[(size_t)b] / div);
+                        V().swap(src);
+                    }
+                    return upload(c, dst, v.data(), v.size(), pad);
                 };
-                std::vector<uint32_t> lbeg((size_t)(nb * (S + 1)));
-                for (int64_t b = 0; b < nb; ++b)
-                    std::copy(pm[(size_t)b].lbeg.begin(), pm[(size_t)b].lbeg.end(), lbeg.begin() + b * (S + 1));
-                if ((rc = upload(c, &t.pm_lbeg, lbeg.data(), lbeg.size()))) return rc;
-                {
-                    std::vector<int64_t> words(t.pmo_list.size());
-                    for (size_t b = 0; b < words.size(); ++b) words[b] = t.pmo_list[b] / 2;
-                    std::vector<uint32_t> v = cat32(&PmBatch::list, words);
-                    if ((rc = upload(c, &t.pm_list, v.data(), v.size(), 64))) return rc;
-                }
-                if (!t.unit) {
-                    std::vector<float> v((size_t)t.pmo_list.back());
-                    for (int64_t b = 0; b < nb; ++b)
-                        std::copy(pm[(size_t)b].val.begin(), pm[(size_t)b].val.end(), v.begin() + t.pmo_list[(size_t)b]);
-                    if ((rc = upload(c, &t.pm_val, v.data(), v.size(), 64))) return rc;
-                }
-                {
-                    std::vector<uint32_t> v = cat32(&PmBatch::pofs, t.pmo_pofs);
-                    if ((rc = upload(c, &t.pm_pofs, v.data(), v.size()))) return rc;
-                }
-                {
-                    std::vector<uint32_t> v = cat32(&PmBatch::rg, t.pmo_rg);
-                    if ((rc = upload(c, &t.pm_rg, v.data(), v.size()))) return rc;
-                }
-                {
-                    std::vector<uint32_t> v = cat32(&PmBatch::qoff, t.pmo_rg);
-                    if ((rc = upload(c, &t.pm_qoff, v.data(), v.size()))) return rc;
-                }
-                {
-                    std::vector<uint16_t> v((size_t)t.pmo_qs.back());
-                    for (int64_t b = 0; b < nb; ++b)
-                        std::copy(pm[(size_t)b].qs.begin(), pm[(size_t)b].qs.end(), v.begin() + t.pmo_qs[(size_t)b]);
-                    if ((rc = upload(c, &t.pm_qs, v.data(), v.size(), 8))) return rc;
-                }
+                std::vector<int64_t> lboff((size_t)nb + 1);
+                for (int64_t b = 0; b <= nb; ++b) lboff[(size_t)b] = b * (S + 1);
+                const int64_t lbeg_n = lboff.back();
+                if ((rc = cat_upload(&PmBatch::lbeg, &t.pm_lbeg, lboff, 1, 0))) return rc;
+                if ((rc = cat_upload(&PmBatch::list, &t.pm_list, t.pmo_list, 2, 64))) return rc;  // 2 words / 4 entries
+                if (!t.unit && (rc = cat_upload(&PmBatch::val, &t.pm_val, t.pmo_list, 1, 64))) return rc;
+                if ((rc = cat_upload(&PmBatch::pofs, &t.pm_pofs, t.pmo_pofs, 1, 0))) return rc;
+                if ((rc = cat_upload(&PmBatch::rg, &t.pm_rg, t.pmo_rg, 1, 0))) return rc;
+                if ((rc = cat_upload(&PmBatch::qoff, &t.pm_qoff, t.pmo_rg, 1, 0))) return rc;
+                if ((rc = cat_upload(&PmBatch::qs, &t.pm_qs, t.pmo_qs, 1, 8))) return rc;
                 if ((rc = dev_alloc(c, (void **)&t.pm_p, (size_t)(pcap + 64) * 4))) return rc;
                 HIPC(c, hipMemsetAsync(t.pm_p, 0, (size_t)(pcap + 64) * 4, c->stream));
-                csc_bytes += (int64_t)(lbeg.size() * 4 + t.pmo_list.back() * (t.unit ? 2 : 6) +
+                csc_bytes += (int64_t)(lbeg_n * 4 + t.pmo_list.back() * (t.unit ? 2 : 6) +
                                        t.pmo_pofs.back() * 4 + t.pmo_rg.back() * 8 + t.pmo_qs.back() * 2 + pcap * 4);
                 t.pm = true;
                 const char *pf = getenv("DLR_PM_FUSED");
