@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "../../dist-lr_amd/csrc/dlr_kernels.hip"
@@ -49,6 +50,226 @@ __global__ void k_remap(int32_t *col, int64_t n, int mode) {
     if (i >= n) return;
     const int32_t c = col[i];
     if (c >= (1 << 20)) col[i] = mode == 1 ? (1 << 14) + (c & ((1 << 18) - (1 << 14) - 1)) : (c & ((1 << 14) - 1));
+}
+
+// Pipelined variant of ordered_segment_dot<int32_t, UNIT=true, HOT>: the
+// next window's column loads are issued right after this window's gathers,
+// so they are in flight under this window's gather wait and sums.
+template <int HOT>
+__device__ __forceinline__ float seg_dot_pipe(int64_t e0, int64_t e1, int64_t a, int64_t b, int lane,
+                                              const int32_t *__restrict__ idx, const float *__restrict__ table,
+                                              float *lds, const float *hot) {
+    constexpr int kWin = 1024, kVec = 4, kWave = 64;
+    constexpr int kT = kWin / (kVec * kWave);
+    constexpr int kChunk = kVec * kWave;
+    const int64_t base = e0 & ~int64_t(kVec - 1);
+    float acc = 0.0f;
+    int4 iv[kT];
+    auto load = [&](int64_t ws, int4 (&v)[kT]) {
+        const int64_t left = e1 - ws;
+#pragma unroll
+        for (int t = 0; t < kT; ++t) {
+            if (t * kChunk < left) {
+                const int64_t e = ws + t * kChunk + lane * kVec;
+                const int64_t ec = e < e1 ? e : ws + t * kChunk;
+                v[t] = dlr::load_stream(reinterpret_cast<const int4 *>(idx + ec));
+            }
+        }
+    };
+    if (base < e1) load(base, iv);
+    for (int64_t ws = base; ws < e1; ws += kWin) {
+        const int64_t left = e1 - ws;
+        float g[kT][kVec];
+#pragma unroll
+        for (int t = 0; t < kT; ++t) {
+            if (t * kChunk < left) {
+                const int64_t e = ws + t * kChunk + lane * kVec;
+                const unsigned i0 = (e >= e0 && e < e1) ? (unsigned)iv[t].x : 0u;
+                const unsigned i1 = (e + 1 >= e0 && e + 1 < e1) ? (unsigned)iv[t].y : 0u;
+                const unsigned i2 = (e + 2 >= e0 && e + 2 < e1) ? (unsigned)iv[t].z : 0u;
+                const unsigned i3 = (e + 3 >= e0 && e + 3 < e1) ? (unsigned)iv[t].w : 0u;
+                const float h0 = hot[i0 < HOT ? i0 : 0u], h1 = hot[i1 < HOT ? i1 : 0u];
+                const float h2 = hot[i2 < HOT ? i2 : 0u], h3 = hot[i3 < HOT ? i3 : 0u];
+                const float c0 = table[i0 < HOT ? 0u : i0], c1 = table[i1 < HOT ? 0u : i1];
+                const float c2 = table[i2 < HOT ? 0u : i2], c3 = table[i3 < HOT ? 0u : i3];
+                g[t][0] = i0 < HOT ? h0 : c0;
+                g[t][1] = i1 < HOT ? h1 : c1;
+                g[t][2] = i2 < HOT ? h2 : c2;
+                g[t][3] = i3 < HOT ? h3 : c3;
+            }
+        }
+        // the next window's columns, behind this window's gathers
+        int4 nv[kT];
+        if (ws + kWin < e1) load(ws + kWin, nv);
+#pragma unroll
+        for (int t = 0; t < kT; ++t) {
+            if (t * kChunk < left) {
+                const int o = t * kChunk + lane * kVec;
+                const int64_t e = ws + o;
+                float4 p;
+                p.x = (e >= e0 && e < e1) ? g[t][0] : 0.0f;
+                p.y = (e + 1 >= e0 && e + 1 < e1) ? g[t][1] : 0.0f;
+                p.z = (e + 2 >= e0 && e + 2 < e1) ? g[t][2] : 0.0f;
+                p.w = (e + 3 >= e0 && e + 3 < e1) ? g[t][3] : 0.0f;
+                *reinterpret_cast<float4 *>(lds + o) = p;
+            }
+        }
+        dlr::wave_sync();
+        const int64_t lo = a > ws ? a : ws;
+        const int64_t hi = b < ws + kWin ? b : ws + kWin;
+        int o = (int)(lo - ws);
+        const int oe = (int)(hi - ws);
+        for (; o + 8 <= oe; o += 8) {
+            const float x0 = lds[o], x1 = lds[o + 1], x2 = lds[o + 2], x3 = lds[o + 3];
+            const float x4 = lds[o + 4], x5 = lds[o + 5], x6 = lds[o + 6], x7 = lds[o + 7];
+            acc = acc + x0;
+            acc = acc + x1;
+            acc = acc + x2;
+            acc = acc + x3;
+            acc = acc + x4;
+            acc = acc + x5;
+            acc = acc + x6;
+            acc = acc + x7;
+        }
+        for (; o < oe; ++o) acc = acc + lds[o];
+        dlr::wave_sync();
+#pragma unroll
+        for (int t = 0; t < kT; ++t) iv[t] = nv[t];
+    }
+    return acc;
+}
+
+// Persistent hot margin, software-pipelined ACROSS the wave's row blocks
+// (a C3 block of 16 rows is one window of ~624 entries): while block i's
+// gathers and sums run, block i+1's column window and block i+2's row
+// pointers are in flight.  Same products, same in-order sums as
+// k_margin_hot.
+template <int HOT, int NW, int SEG>
+__global__ __launch_bounds__(NW * 64) void k_margin_hot_pipe(dlr::DevBatch bt, const float *__restrict__ w,
+                                                           float *__restrict__ resid) {
+    constexpr int kWin = 1024, kVec = 4, kT = kWin / (kVec * 64), kChunk = kVec * 64;
+    __shared__ __attribute__((aligned(16))) float s_w[HOT];
+    __shared__ float s_p[NW][kWin];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x / 64;
+    {
+        const float4 *src = reinterpret_cast<const float4 *>(w);
+        float4 *dst = reinterpret_cast<float4 *>(s_w);
+#pragma unroll
+        for (int k = 0; k < HOT / 4 / (NW * 64); ++k) dst[k * NW * 64 + threadIdx.x] = src[k * NW * 64 + threadIdx.x];
+    }
+    __syncthreads();
+    float *lds = s_p[wv];
+    const int64_t nblk = (bt.rows + NW * SEG - 1) / (NW * SEG);
+    struct Blk {
+        int64_t row0 = -1, e0 = 0, e1 = 0, a = 0, b = 0;
+        float y = 0.0f;
+        bool valid = false;
+    };
+    // the row pointers of block blk (row0 < 0: no block)
+    auto ptrs = [&](int64_t blk, Blk &q) {
+        q.row0 = -1;
+        if (blk >= nblk) return;
+        const int64_t row0 = (blk * NW + wv) * SEG;
+        if (row0 >= bt.rows) return;
+        q.row0 = row0;
+        const int64_t my = row0 + lane;
+        q.valid = lane < SEG && my < bt.rows;
+        const int64_t rlast = min(row0 + SEG, bt.rows);
+        q.e0 = bt.row_ptr[row0];
+        q.e1 = bt.row_ptr[rlast];
+        const int64_t mc = q.valid ? my : row0;
+        q.a = bt.row_ptr[mc];
+        q.b = bt.row_ptr[mc + 1];
+        q.y = bt.label[mc];
+    };
+    // block q's single window (SEG rows of <= 1024 entries in total)
+    auto window = [&](const Blk &q, int4 (&v)[kT]) {
+        if (q.row0 < 0) return;
+        const int64_t ws = q.e0 & ~int64_t(kVec - 1);
+        const int64_t left = q.e1 - ws;
+#pragma unroll
+        for (int t = 0; t < kT; ++t) {
+            if (t * kChunk < left) {
+                const int64_t e = ws + t * kChunk + lane * kVec;
+                const int64_t ec = e < q.e1 ? e : ws + t * kChunk;
+                v[t] = dlr::load_stream(reinterpret_cast<const int4 *>(bt.col + ec));
+            }
+        }
+    };
+    Blk cur, nxt, nn;
+    int4 iv[kT], nv[kT];
+    ptrs(blockIdx.x, cur);
+    ptrs(blockIdx.x + gridDim.x, nxt);
+    window(cur, iv);
+    for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        if (cur.row0 >= 0) {
+            const int64_t ws = cur.e0 & ~int64_t(kVec - 1);
+            const int64_t left = cur.e1 - ws;
+            float g[kT][kVec];
+#pragma unroll
+            for (int t = 0; t < kT; ++t) {
+                if (t * kChunk < left) {
+                    const int64_t e = ws + t * kChunk + lane * kVec;
+                    const unsigned i0 = (e >= cur.e0 && e < cur.e1) ? (unsigned)iv[t].x : 0u;
+                    const unsigned i1 = (e + 1 >= cur.e0 && e + 1 < cur.e1) ? (unsigned)iv[t].y : 0u;
+                    const unsigned i2 = (e + 2 >= cur.e0 && e + 2 < cur.e1) ? (unsigned)iv[t].z : 0u;
+                    const unsigned i3 = (e + 3 >= cur.e0 && e + 3 < cur.e1) ? (unsigned)iv[t].w : 0u;
+                    const float h0 = s_w[i0 < HOT ? i0 : 0u], h1 = s_w[i1 < HOT ? i1 : 0u];
+                    const float h2 = s_w[i2 < HOT ? i2 : 0u], h3 = s_w[i3 < HOT ? i3 : 0u];
+                    const float c0 = w[i0 < HOT ? 0u : i0], c1 = w[i1 < HOT ? 0u : i1];
+                    const float c2 = w[i2 < HOT ? 0u : i2], c3 = w[i3 < HOT ? 0u : i3];
+                    g[t][0] = i0 < HOT ? h0 : c0;
+                    g[t][1] = i1 < HOT ? h1 : c1;
+                    g[t][2] = i2 < HOT ? h2 : c2;
+                    g[t][3] = i3 < HOT ? h3 : c3;
+                }
+            }
+            // behind this block's gathers: the next block's window, the
+            // block after's row pointers
+            window(nxt, nv);
+            ptrs(blk + 2 * (int64_t)gridDim.x, nn);
+#pragma unroll
+            for (int t = 0; t < kT; ++t) {
+                if (t * kChunk < left) {
+                    const int o = t * kChunk + lane * kVec;
+                    const int64_t e = ws + o;
+                    float4 p;
+                    p.x = (e >= cur.e0 && e < cur.e1) ? g[t][0] : 0.0f;
+                    p.y = (e + 1 >= cur.e0 && e + 1 < cur.e1) ? g[t][1] : 0.0f;
+                    p.z = (e + 2 >= cur.e0 && e + 2 < cur.e1) ? g[t][2] : 0.0f;
+                    p.w = (e + 3 >= cur.e0 && e + 3 < cur.e1) ? g[t][3] : 0.0f;
+                    *reinterpret_cast<float4 *>(lds + o) = p;
+                }
+            }
+            dlr::wave_sync();
+            float acc = 0.0f;
+            int o = (int)(cur.a - ws);
+            const int oe = (int)(cur.b - ws);
+            for (; o + 8 <= oe; o += 8) {
+                const float x0 = lds[o], x1 = lds[o + 1], x2 = lds[o + 2], x3 = lds[o + 3];
+                const float x4 = lds[o + 4], x5 = lds[o + 5], x6 = lds[o + 6], x7 = lds[o + 7];
+                acc = acc + x0;
+                acc = acc + x1;
+                acc = acc + x2;
+                acc = acc + x3;
+                acc = acc + x4;
+                acc = acc + x5;
+                acc = acc + x6;
+                acc = acc + x7;
+            }
+            for (; o < oe; ++o) acc = acc + lds[o];
+            dlr::wave_sync();
+            if (cur.valid) resid[cur.row0 + lane] = dlr::sigmoid_ref(acc) - cur.y;
+        } else {
+            window(nxt, nv);
+            ptrs(blk + 2 * (int64_t)gridDim.x, nn);
+        }
+        cur = nxt;
+        nxt = nn;
+#pragma unroll
+        for (int t = 0; t < kT; ++t) iv[t] = nv[t];
+    }
 }
 
 }  // namespace
@@ -119,6 +340,40 @@ int main(int argc, char **argv) {
         printf("%-58s %8.1f us\n", name, ms * 1000.0f / reps);
     };
     time_margin("k_margin_hot, measured rank mix");
+    {
+        // the pipelined variant: same grid as launch_margin_hot's default
+        // (16,384 hot weights x 16 waves, SEG 16, one workgroup per CU)
+        float *d_r2;
+        CK(hipMalloc(&d_r2, N * 4));
+        int dev = 0, ncu = 256;
+        CK(hipGetDevice(&dev));
+        CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        const int64_t nb = (N + 16 * 16 - 1) / (16 * 16);
+        const unsigned grid = (unsigned)std::min<int64_t>(nb, ncu);
+        std::vector<float> w0(D);
+        for (int64_t j = 0; j < D; ++j) w0[j] = (float)((j * 2654435761u) % 2001) * 1e-4f - 0.1f;
+        CK(hipMemcpy(d_w, w0.data(), D * 4, hipMemcpyHostToDevice));
+        CK(dlr::launch_margin_hot(bt, d_w, D, d_r, 0));
+        hipLaunchKernelGGL((k_margin_hot_pipe<16384, 16, 16>), dim3(grid), dim3(1024), 0, 0, bt, d_w, d_r2);
+        CK(hipDeviceSynchronize());
+        std::vector<float> r1(N), r2(N);
+        CK(hipMemcpy(r1.data(), d_r, N * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(r2.data(), d_r2, N * 4, hipMemcpyDeviceToHost));
+        int64_t bad = 0;
+        for (int64_t i = 0; i < N; ++i) bad += memcmp(&r1[i], &r2[i], 4) != 0;
+        printf("pipelined variant vs production: %lld of %lld residuals differ\n", (long long)bad, (long long)N);
+        const int reps = 10;
+        for (int k = 0; k < 2; ++k) hipLaunchKernelGGL((k_margin_hot_pipe<16384, 16, 16>), dim3(grid), dim3(1024), 0, 0, bt, d_w, d_r2);
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(a, 0));
+        for (int k = 0; k < reps; ++k) hipLaunchKernelGGL((k_margin_hot_pipe<16384, 16, 16>), dim3(grid), dim3(1024), 0, 0, bt, d_w, d_r2);
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        printf("%-58s %8.1f us\n", "k_margin_hot_pipe (next window's columns in flight)", ms * 1000.0f / reps);
+        time_margin("k_margin_hot again (same weights)");
+    }
     const int64_t n = N * F;
     hipLaunchKernelGGL(k_remap, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, d_col, n, 1);
     CK(hipDeviceSynchronize());
