@@ -7,7 +7,8 @@
 // margin timed as is and with the tail entries remapped into the warm
 // range (an upper bound of what a tail product margin could save: the
 // tail products would then be read from per-block regions instead of
-// gathered).  Development tool only.
+// gathered); and a variant of it software-pipelined across row blocks.
+// Development tool only.
 //
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -I include -I dist-lr_amd/csrc \
 //         tools/kbench/kb_c3tail.hip -o tools/kbench/kb_c3tail && ./tools/kbench/kb_c3tail
@@ -50,93 +51,6 @@ __global__ void k_remap(int32_t *col, int64_t n, int mode) {
     if (i >= n) return;
     const int32_t c = col[i];
     if (c >= (1 << 20)) col[i] = mode == 1 ? (1 << 14) + (c & ((1 << 18) - (1 << 14) - 1)) : (c & ((1 << 14) - 1));
-}
-
-// Pipelined variant of ordered_segment_dot<int32_t, UNIT=true, HOT>: the
-// next window's column loads are issued right after this window's gathers,
-// so they are in flight under this window's gather wait and sums.
-template <int HOT>
-__device__ __forceinline__ float seg_dot_pipe(int64_t e0, int64_t e1, int64_t a, int64_t b, int lane,
-                                              const int32_t *__restrict__ idx, const float *__restrict__ table,
-                                              float *lds, const float *hot) {
-    constexpr int kWin = 1024, kVec = 4, kWave = 64;
-    constexpr int kT = kWin / (kVec * kWave);
-    constexpr int kChunk = kVec * kWave;
-    const int64_t base = e0 & ~int64_t(kVec - 1);
-    float acc = 0.0f;
-    int4 iv[kT];
-    auto load = [&](int64_t ws, int4 (&v)[kT]) {
-        const int64_t left = e1 - ws;
-#pragma unroll
-        for (int t = 0; t < kT; ++t) {
-            if (t * kChunk < left) {
-                const int64_t e = ws + t * kChunk + lane * kVec;
-                const int64_t ec = e < e1 ? e : ws + t * kChunk;
-                v[t] = dlr::load_stream(reinterpret_cast<const int4 *>(idx + ec));
-            }
-        }
-    };
-    if (base < e1) load(base, iv);
-    for (int64_t ws = base; ws < e1; ws += kWin) {
-        const int64_t left = e1 - ws;
-        float g[kT][kVec];
-#pragma unroll
-        for (int t = 0; t < kT; ++t) {
-            if (t * kChunk < left) {
-                const int64_t e = ws + t * kChunk + lane * kVec;
-                const unsigned i0 = (e >= e0 && e < e1) ? (unsigned)iv[t].x : 0u;
-                const unsigned i1 = (e + 1 >= e0 && e + 1 < e1) ? (unsigned)iv[t].y : 0u;
-                const unsigned i2 = (e + 2 >= e0 && e + 2 < e1) ? (unsigned)iv[t].z : 0u;
-                const unsigned i3 = (e + 3 >= e0 && e + 3 < e1) ? (unsigned)iv[t].w : 0u;
-                const float h0 = hot[i0 < HOT ? i0 : 0u], h1 = hot[i1 < HOT ? i1 : 0u];
-                const float h2 = hot[i2 < HOT ? i2 : 0u], h3 = hot[i3 < HOT ? i3 : 0u];
-                const float c0 = table[i0 < HOT ? 0u : i0], c1 = table[i1 < HOT ? 0u : i1];
-                const float c2 = table[i2 < HOT ? 0u : i2], c3 = table[i3 < HOT ? 0u : i3];
-                g[t][0] = i0 < HOT ? h0 : c0;
-                g[t][1] = i1 < HOT ? h1 : c1;
-                g[t][2] = i2 < HOT ? h2 : c2;
-                g[t][3] = i3 < HOT ? h3 : c3;
-            }
-        }
-        // the next window's columns, behind this window's gathers
-        int4 nv[kT];
-        if (ws + kWin < e1) load(ws + kWin, nv);
-#pragma unroll
-        for (int t = 0; t < kT; ++t) {
-            if (t * kChunk < left) {
-                const int o = t * kChunk + lane * kVec;
-                const int64_t e = ws + o;
-                float4 p;
-                p.x = (e >= e0 && e < e1) ? g[t][0] : 0.0f;
-                p.y = (e + 1 >= e0 && e + 1 < e1) ? g[t][1] : 0.0f;
-                p.z = (e + 2 >= e0 && e + 2 < e1) ? g[t][2] : 0.0f;
-                p.w = (e + 3 >= e0 && e + 3 < e1) ? g[t][3] : 0.0f;
-                *reinterpret_cast<float4 *>(lds + o) = p;
-            }
-        }
-        dlr::wave_sync();
-        const int64_t lo = a > ws ? a : ws;
-        const int64_t hi = b < ws + kWin ? b : ws + kWin;
-        int o = (int)(lo - ws);
-        const int oe = (int)(hi - ws);
-        for (; o + 8 <= oe; o += 8) {
-            const float x0 = lds[o], x1 = lds[o + 1], x2 = lds[o + 2], x3 = lds[o + 3];
-            const float x4 = lds[o + 4], x5 = lds[o + 5], x6 = lds[o + 6], x7 = lds[o + 7];
-            acc = acc + x0;
-            acc = acc + x1;
-            acc = acc + x2;
-            acc = acc + x3;
-            acc = acc + x4;
-            acc = acc + x5;
-            acc = acc + x6;
-            acc = acc + x7;
-        }
-        for (; o < oe; ++o) acc = acc + lds[o];
-        dlr::wave_sync();
-#pragma unroll
-        for (int t = 0; t < kT; ++t) iv[t] = nv[t];
-    }
-    return acc;
 }
 
 // Persistent hot margin, software-pipelined ACROSS the wave's row blocks
