@@ -14,7 +14,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CASES = [
-    ("traffic.json", "r02c_pmc_c2", "D1000000_nnz50_B65536", "lds"),
+    ("traffic.json", "r02f_pmc_c2", "D1000000_nnz50_B65536", "lds"),
     ("traffic_c3.json", "r02_pmc_c3", "D16777216_nnz39_B-1", "classic"),
     ("traffic_c4.json", "r02_pmc_c4", "D4096_nnz4096_B65536", "dense"),
     ("traffic_c5.json", "r02_pmc_c5", "D268435456_nnz10_B1024", "touched"),
