@@ -694,8 +694,10 @@ constexpr int kBlkPad = kBlk + 8;  // product slab per wave: lane reads at o + [
 // right after its update -- stages the slice's weights in LDS and forms the
 // batch's products in the slice, writing them block by block into the
 // product array; pass 2 -- a wave per 64-row block -- copies the block's
-// products (one contiguous region) into LDS with 16-byte loads and each lane
-// adds its row's products in column order through a precomputed slot list.
+// products (one contiguous region) into LDS by 16-byte LDS-DMA and each
+// lane adds its row's products in column order through a precomputed slot
+// list.  Padding slots (chunks are whole 4-slot groups) hold w * 0 or any
+// value: no slot list points at them.
 // The products are the same fl32(w_j * x_ij) and each row's additions run in
 // the same (column) order from +0: bitwise k_margin_residual's residuals.
 
