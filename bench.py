@@ -418,10 +418,11 @@ def run_rank(args):
         "instrumented_ms_per_step": round(el_instr / args.steps * 1000.0, 5),
     }
     if streamed:
-        # bound by the host->device batch copies: dense, B rows x D fp32 +
-        # labels per step; sparse, the batch's CSR + column-major slices (at
-        # most one of the two device slots, train_bytes / 2)
-        h2d = B_eff * (4 * D + 4) if args.kind == "dense" else train_bytes // 2
+        # bound by the host->device batch copies: the engine's own count of
+        # the bytes one batch's copies move (dlr_stream_bytes: dense, the
+        # batch's rows; sparse, the coalesced CSR + block bases -- the LDS
+        # layout is built on the device and never crosses PCIe), epoch mean
+        h2d = eng.stream_bytes()[0]
         pcie = h2d / (el / args.steps) / 1e9
         roofline.update({"bound": "pcie", "kernel": "per-batch host->device staging (copy stream) overlapped "
                                                       "with the margin/gradient kernels of the previous batch",

@@ -7,6 +7,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -32,17 +33,26 @@ bool nccl_ok(ncclResult_t r, const char *what, std::string &err) {
 class RcclComm final : public Comm {
 public:
     RcclComm(ncclComm_t c, int world, int rank) : comm_(c), world_(world), rank_(rank) {}
-    ~RcclComm() override { ncclCommDestroy(comm_); }
+    ~RcclComm() override {
+        if (!aborted_) ncclCommDestroy(comm_);
+    }
+    void abort(const std::string &) override {
+        if (!aborted_) (void)ncclCommAbort(comm_);  // frees the communicator; peers' RCCL calls error out
+        aborted_ = true;
+    }
     int world() const override { return world_; }
     int rank() const override { return rank_; }
     const char *kind() const override { return "rccl"; }
     bool all_reduce_i64(int64_t *d, size_t n, bool max, hipStream_t s, std::string &err) override {
+        if (aborted_) return nccl_ok(ncclInvalidUsage, "aborted communicator", err);
         return nccl_ok(ncclAllReduce(d, d, n, ncclInt64, max ? ncclMax : ncclSum, comm_, s), "ncclAllReduce", err);
     }
     bool all_gather(const void *send, void *recv, size_t words, hipStream_t s, std::string &err) override {
+        if (aborted_) return nccl_ok(ncclInvalidUsage, "aborted communicator", err);
         return nccl_ok(ncclAllGather(send, recv, words, ncclUint32, comm_, s), "ncclAllGather", err);
     }
     bool all_to_all(const void *send, void *recv, size_t words, hipStream_t s, std::string &err) override {
+        if (aborted_) return nccl_ok(ncclInvalidUsage, "aborted communicator", err);
         return nccl_ok(ncclAllToAll(send, recv, words, ncclUint32, comm_, s), "ncclAllToAll", err);
     }
     int count() const {
@@ -53,6 +63,7 @@ public:
 private:
     ncclComm_t comm_;
     int world_, rank_;
+    bool aborted_ = false;
 };
 
 }  // namespace
@@ -86,23 +97,42 @@ Comm *make_rccl_comm(int world, int rank, const void *unique_id, std::string &er
 
 // ------------------------------------------------------------------ loopback
 
+// Seconds a loopback rank waits for its peers at a collective before the
+// group is declared broken: DLR_LOOPBACK_TIMEOUT_S (default 1,800 -- long
+// enough for W ranks building large layouts one after another on one GPU;
+// a rank that FAILS releases its peers at once through abort()).
+int loop_timeout_s() {
+    const char *v = getenv("DLR_LOOPBACK_TIMEOUT_S");
+    const int s = v ? atoi(v) : 0;
+    return s > 0 ? s : 1800;
+}
+
 struct LoopGroup {
-    explicit LoopGroup(int w) : W(w), send((size_t)w, nullptr), recv((size_t)w, nullptr) {}
+    explicit LoopGroup(int w) : W(w), timeout_s(loop_timeout_s()), send((size_t)w, nullptr), recv((size_t)w, nullptr) {}
     const int W;
+    const int timeout_s;
     std::mutex mu;
     std::condition_variable cv;
     int arrived = 0;
     uint64_t gen = 0;
-    bool broken = false;  // a rank timed out: every later barrier fails at once
+    bool broken = false;  // a rank timed out or aborted: every later barrier fails at once
+    std::string why;      // ... and why
     std::vector<const void *> send;
     std::vector<void *> recv;
     std::atomic<int> refs{0};
+
+    void abort(const std::string &reason) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!broken) why = reason;
+        broken = true;
+        cv.notify_all();
+    }
 
     // Generation barrier over the W ranks (each rank is one host thread).
     bool barrier(std::string &err) {
         std::unique_lock<std::mutex> lk(mu);
         if (broken) {
-            err = "loopback group: a peer failed earlier";
+            err = "loopback group: a peer failed earlier (" + why + ")";
             return false;
         }
         const uint64_t g = gen;
@@ -112,13 +142,14 @@ struct LoopGroup {
             cv.notify_all();
             return true;
         }
-        if (!cv.wait_for(lk, std::chrono::seconds(300), [&] { return gen != g || broken; }) || broken) {
+        if (!cv.wait_for(lk, std::chrono::seconds(timeout_s), [&] { return gen != g || broken; })) {
             broken = true;
+            why = "peers did not reach a collective within " + std::to_string(timeout_s) + " s";
             cv.notify_all();
-            err = "loopback group: peers did not reach the collective within 300 s";
-            return false;
         }
-        return true;
+        if (gen != g) return true;  // released by the last arriver (an abort after that does not undo it)
+        err = "loopback group: " + why;
+        return false;
     }
 };
 
@@ -133,6 +164,7 @@ public:
     int world() const override { return g_->W; }
     int rank() const override { return rank_; }
     const char *kind() const override { return "loopback"; }
+    void abort(const std::string &why) override { g_->abort("rank " + std::to_string(rank_) + ": " + why); }
 
     bool all_reduce_i64(int64_t *d, size_t n, bool max, hipStream_t s, std::string &err) override {
         const int W = g_->W;

@@ -40,6 +40,10 @@ public:
     virtual bool all_gather(const void *send, void *recv, size_t words, hipStream_t s, std::string &err) = 0;
     // recv[q * words ..] = rank q's send[rank * words ..).
     virtual bool all_to_all(const void *send, void *recv, size_t words, hipStream_t s, std::string &err) = 0;
+    // A rank that will not reach its next collective (it failed) releases
+    // its peers: their pending and later collectives fail with `why`
+    // instead of waiting (loopback), or the communicator is aborted (RCCL).
+    virtual void abort(const std::string &why) = 0;
 };
 
 // RCCL communicator for rank `rank` of `world` (unique_id: the 128-byte

@@ -1708,6 +1708,12 @@ int dlr_comm_info(const dlr_ctx *c, int *nranks, int *transport) {
     return DLR_OK;
 }
 
+int dlr_comm_abort(dlr_ctx *c, const char *why) {
+    if (!c) return DLR_E_ARG;
+    if (c->comm) c->comm->abort(why ? why : "aborted");
+    return DLR_OK;
+}
+
 void dlr_destroy(dlr_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
@@ -1874,10 +1880,17 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         if (c->residency == DLR_RESIDENCY_AUTO) {
             size_t fr = 0, tot = 0;
             HIPC(c, hipMemGetInfo(&fr, &tot));
-            stream = est + (double)((size_t)8 << 30) > (double)fr;
+            stream = !band && est + (double)((size_t)8 << 30) > (double)fr;
         }
-        if (stream && band)
-            return fail(c, DLR_E_ARG, "dlr_load_train: a band-mode batch (>= 2^21 rows) cannot be streamed per batch");
+        // only an explicit STREAM request can fail here; every rank learns
+        // of a failure on any rank (no rank is left waiting in a later load
+        // collective)
+        int64_t bad = stream && band ? 1 : 0;
+        if ((rc = coll_max_i64(c, &bad))) return rc;
+        if (bad)
+            return fail(c, DLR_E_ARG, stream && band ? "dlr_load_train: a band-mode batch (>= 2^21 rows) cannot be "
+                                                       "streamed per batch"
+                                                     : "dlr_load_train: another rank cannot stream its band-mode batch");
         t.sparse_stream = stream;
         if (stream) {
             if (!c->cstream) HIPC(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
@@ -2825,6 +2838,31 @@ int dlr_memory_info(dlr_ctx *c, int64_t *train_bytes, int64_t *test_bytes) {
     if (!c) return DLR_E_ARG;
     if (train_bytes) *train_bytes = c->train.loaded ? c->train.bytes : 0;
     if (test_bytes) *test_bytes = c->test.loaded ? c->test.bytes : 0;
+    return DLR_OK;
+}
+
+int dlr_stream_bytes(dlr_ctx *c, int64_t *mean_bytes, int64_t *max_bytes) {
+    if (!c) return DLR_E_ARG;
+    const TrainShard &t = c->train;
+    if (!t.loaded) return fail(c, DLR_E_STATE, "dlr_stream_bytes: no training shard loaded");
+    double sum = 0.0;
+    int64_t mx = 0;
+    const size_t nb = t.plan.size();
+    for (size_t b = 0; b < nb && (t.streamed || t.sparse_stream); ++b) {
+        int64_t n = 0;  // exactly what stage_dense / stage_sparse copy host -> device for batch b
+        if (t.streamed) {
+            n = t.plan[b].rows * c->D * 4;
+        } else if (t.shost) {
+            n = (int64_t)t.sbsz[b];
+        } else {
+            for (const StreamArr &a : t.sarr)
+                if (a.end[b] > a.beg[b]) n += (int64_t)(((size_t)(a.end[b] - a.beg[b]) + a.pad) * a.es);
+        }
+        sum += (double)n;
+        mx = std::max(mx, n);
+    }
+    if (mean_bytes) *mean_bytes = nb ? (int64_t)(sum / (double)nb + 0.5) : 0;
+    if (max_bytes) *max_bytes = mx;
     return DLR_OK;
 }
 

@@ -38,12 +38,12 @@ SYMBOLS = [
     "dlr_dense_free",
     "dlr_num_batches", "dlr_batch_rows",
     "dlr_init_weight", "dlr_format_model", "dlr_key_range",
-    "dlr_get_unique_id", "dlr_create", "dlr_create_group", "dlr_comm_info", "dlr_destroy", "dlr_last_error",
+    "dlr_get_unique_id", "dlr_create", "dlr_create_group", "dlr_comm_abort", "dlr_comm_info", "dlr_destroy", "dlr_last_error",
     "dlr_set_weights", "dlr_get_weights", "dlr_load_train", "dlr_load_test", "dlr_load_train_dense",
     "dlr_load_test_dense", "dlr_set_residency", "dlr_train_residency",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
     "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_train_band_rows", "dlr_train_relabeled", "dlr_train_unit_values", "dlr_train_product_margin",
-    "dlr_memory_info",
+    "dlr_memory_info", "dlr_stream_bytes",
 ]
 
 if not os.path.exists(LIB_PATH):
@@ -135,6 +135,7 @@ _sig("dlr_key_range", C.c_int, i64, C.c_int, C.c_int, C.POINTER(i64), C.POINTER(
 _sig("dlr_get_unique_id", C.c_int, P)
 _sig("dlr_create", C.c_int, C.c_int, C.c_int, C.c_int, P, i64, C.POINTER(P))
 _sig("dlr_create_group", C.c_int, C.c_int, C.c_int, i64, P)
+_sig("dlr_comm_abort", C.c_int, P, C.c_char_p)
 _sig("dlr_comm_info", C.c_int, P, C.POINTER(C.c_int), C.POINTER(C.c_int))
 _sig("dlr_destroy", None, P)
 _sig("dlr_last_error", C.c_char_p, P)
@@ -157,6 +158,7 @@ _sig("dlr_train_relabeled", C.c_int, P)
 _sig("dlr_train_unit_values", C.c_int, P)
 _sig("dlr_train_product_margin", C.c_int, P)
 _sig("dlr_memory_info", C.c_int, P, C.POINTER(i64), C.POINTER(i64))
+_sig("dlr_stream_bytes", C.c_int, P, C.POINTER(i64), C.POINTER(i64))
 
 
 class DLRError(RuntimeError):
@@ -448,6 +450,11 @@ class Engine:
         _check(lib.dlr_create_group(device, world, num_feature_dim, hs))
         return [cls(num_feature_dim, device, r, world, _handle=P(hs[r])) for r in range(world)]
 
+    def comm_abort(self, why: str = "aborted") -> None:
+        """This rank failed: release its peers' pending collectives
+        (dlr_comm_abort)."""
+        self._c(lib.dlr_comm_abort(self._h, why.encode()))
+
     def comm_info(self) -> Tuple[int, int]:
         """(ranks of the communicator, TRANSPORT_*) -- dlr_comm_info."""
         n, t = C.c_int(), C.c_int()
@@ -572,6 +579,13 @@ class Engine:
     def memory_info(self) -> Tuple[int, int]:
         a, b = i64(), i64()
         self._c(lib.dlr_memory_info(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def stream_bytes(self) -> Tuple[int, int]:
+        """(mean, max) host->device bytes staged per batch of a streamed
+        training shard (dlr_stream_bytes); (0, 0) when resident."""
+        a, b = i64(), i64()
+        self._c(lib.dlr_stream_bytes(self._h, C.byref(a), C.byref(b)))
         return a.value, b.value
 
     def close(self) -> None:

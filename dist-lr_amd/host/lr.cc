@@ -127,6 +127,13 @@ std::vector<KVWorker *> KVWorker::Group(int device, int world, float learning_ra
 
 KVWorker::~KVWorker() { dlr_destroy(ctx_); }
 
+void KVWorker::Abort(const std::string &why) {
+    if (ps_)
+        ps_->Abort(why);
+    else
+        (void)dlr_comm_abort(ctx_, why.c_str());
+}
+
 int KVWorker::mode() const {
     if (!sync_mode_) return DLR_MODE_ASYNC;
     const char *m = getenv("DISTLR_SYNC_MERGE");  // "last": main.cc:71 as written

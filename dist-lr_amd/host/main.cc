@@ -67,14 +67,17 @@ struct Config {
 };
 
 // main.cc:124-170 for one rank.
-void run_worker(const Config &cfg, int rank, distlr::KVWorker *kv, distlr::ParamServer *ps,
-                std::vector<int> *failed) {
+void run_worker(const Config &cfg, int rank, distlr::KVWorker *kv, std::vector<int> *failed) {
+    // The LR (which owns kv) outlives the try block, so a failing rank can
+    // still release its peers through kv in the handler.
+    std::unique_ptr<distlr::LR> owner;
     try {
         {
             std::lock_guard<std::mutex> g(g_out);
             std::cout << 0 << "I got a rank " << rank << std::endl;  // main.cc:134 (customer id 0)
         }
-        distlr::LR lr = distlr::LR(cfg.num_feature_dim);
+        owner.reset(new distlr::LR(cfg.num_feature_dim));
+        distlr::LR &lr = *owner;
         lr.SetKVWorker(kv);
         lr.SetRank(rank);
         {
@@ -97,7 +100,7 @@ void run_worker(const Config &cfg, int rank, distlr::KVWorker *kv, distlr::Param
         std::string modelfile = cfg.root + "/models/part-00" + std::to_string(rank + 1);
         lr.SaveModel(modelfile);
     } catch (const std::exception &e) {
-        if (ps) ps->Abort(std::string("worker ") + std::to_string(rank) + " failed");  // release its peers
+        kv->Abort(std::string("worker ") + std::to_string(rank) + " failed: " + e.what());  // release its peers
         std::lock_guard<std::mutex> g(g_out);
         std::cerr << "distlr: worker " << rank << ": " << e.what() << std::endl;
         (*failed)[(size_t)rank] = 1;
@@ -203,7 +206,7 @@ int main(int argc, char **argv) {
         return 4;
     }
     for (int r = 0; r < cfg.workers; ++r)
-        th.emplace_back(run_worker, std::cref(cfg), r, kvs[(size_t)r], ps.get(), &failed);
+        th.emplace_back(run_worker, std::cref(cfg), r, kvs[(size_t)r], &failed);
     for (auto &t : th) t.join();
     for (int f : failed)
         if (f) return 1;

@@ -65,6 +65,10 @@ class KVWorker {
     static std::vector<KVWorker *> Group(int device, int world, float learning_rate, bool sync_mode,
                                          int64_t num_feature_dim);
     ParamServer *ps() const { return ps_; }
+    // This worker failed and will not reach its next exchange: release its
+    // peers (ParamServer::Abort for the parameter-server topology,
+    // dlr_comm_abort for RCCL / loopback-group ranks).
+    void Abort(const std::string &why);
     ~KVWorker();
     KVWorker(const KVWorker &) = delete;
     KVWorker &operator=(const KVWorker &) = delete;

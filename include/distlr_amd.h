@@ -209,6 +209,12 @@ int dlr_create_group(int device, int world, int64_t num_feature_dim, dlr_ctx **o
 #define DLR_TRANSPORT_NONE 0
 #define DLR_TRANSPORT_RCCL 1
 #define DLR_TRANSPORT_LOOPBACK 2
+/* A rank that has failed and will not reach its next collective releases its
+ * peers (the parameter-server topology's ParamServer::Abort for the rank
+ * groups): their pending and later collectives fail with `why` instead of
+ * waiting -- loopback groups at once, RCCL by ncclCommAbort (this context's
+ * communicator is unusable afterwards).  No-op without a transport. */
+int dlr_comm_abort(dlr_ctx *ctx, const char *why);
 int dlr_comm_info(const dlr_ctx *ctx, int *nranks, int *transport);
 void dlr_destroy(dlr_ctx *ctx);
 const char *dlr_last_error(const dlr_ctx *ctx);
@@ -359,6 +365,13 @@ int dlr_train_product_margin(dlr_ctx *ctx);
 
 /* Device bytes resident for the loaded shards (for reporting). */
 int dlr_memory_info(dlr_ctx *ctx, int64_t *train_bytes, int64_t *test_bytes);
+
+/* Host -> device bytes staged per training batch of a STREAMED shard (K1):
+ * the mean and the maximum over the epoch's batches of exactly what one
+ * batch's copies move (dense: the batch's rows; sparse: the coalesced slices
+ * -- the CSR and block bases, not the column-major layout built on the
+ * device).  0 / 0 for a device-resident shard.  For bench's PCIe figure. */
+int dlr_stream_bytes(dlr_ctx *ctx, int64_t *mean_bytes, int64_t *max_bytes);
 
 #ifdef __cplusplus
 }

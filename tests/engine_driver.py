@@ -142,6 +142,7 @@ def run_group(shards: Sequence, D: int, num_iteration: int, batch_size: int, lea
             finals[r] = eng.get_weights()
         except BaseException as e:  # noqa: BLE001 -- re-raised in the caller
             errors[r] = e
+            eng.comm_abort(f"rank {r}: {e}")  # peers waiting in a collective fail now, not at the timeout
 
     try:
         th = [threading.Thread(target=rank_main, args=(r,)) for r in range(W)]

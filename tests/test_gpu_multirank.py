@@ -200,6 +200,48 @@ def test_rejected_shard_fails_on_every_rank():
         run_group([good, bad], D, 1, 64, 0.1)
 
 
+def test_failed_rank_releases_its_peers():
+    # a rank that fails (here: stops before its step) aborts the
+    # group; the peer blocked in the step's collective fails at once with
+    # the reason instead of waiting for the loopback timeout
+    import threading
+    import time
+    D = 30000
+    shards = [dlr.Dataset.generate(1000, D, 20, value_mode=1, seed=3, stream=r + 1) for r in range(2)]
+    engines = dlr.Engine.create_group(D, 2)
+    err = [None, None]
+    try:
+        for e, s in zip(engines, shards):
+            e.set_weights(dlr.init_weight(D))
+        ths = [threading.Thread(target=lambda r=r: engines[r].load_train(shards[r], 100)) for r in range(2)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+
+        def rank0():
+            try:
+                engines[0].train_step(0, 0.1)
+                engines[0].sync()
+            except dlr.DLRError as e:
+                err[0] = e
+
+        t0 = time.perf_counter()
+        th = threading.Thread(target=rank0)
+        th.start()
+        time.sleep(0.5)
+        engines[1].comm_abort("rank 1 cannot read its shard")
+        th.join(timeout=60)
+        assert not th.is_alive()
+        assert err[0] is not None and "cannot read its shard" in str(err[0])
+        assert time.perf_counter() - t0 < 30
+        with pytest.raises(dlr.DLRError, match="failed earlier"):
+            engines[1].train_step(0, 0.1)
+    finally:
+        for e in engines:
+            e.close()
+
+
 # ---------------------------------------------------------------- RCCL, one process per GPU
 
 
