@@ -75,6 +75,13 @@ CONFIGS = {
     "c2s": dict(rows=10_000_000, features=1_000_000, nnz=50, batch=65536, value_mode=1, steps=200, warmup=10,
                 label="C2 sparse LR, streamed from host", residency="stream"),
 }
+# C1 end to end: bin/distlr running examples/local.sh's
+# job (W = 2 workers, 100 epochs, B = -1, Test every 10; local.sh:12-19,
+# main.cc:157-169) as a child process, timed beside the reference-structure
+# CPU run of the same job on the same files -- handled by run_c1_e2e, before
+# this process touches the GPU.
+CONFIGS["c1e2e"] = dict(rows=8140, features=123, nnz=14, batch=-1, value_mode=0, steps=100, warmup=1,
+                        label="C1 local.sh job end to end (bin/distlr)", kind="e2e")
 PCIE_PEAK_GBS = 63.0  # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s (spec)
 
 
@@ -89,7 +96,8 @@ def make_shard(args, n_rows: int, stream: int):
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2",
+                    help="BASELINE config (c1e2e: local.sh's job end to end through bin/distlr)")
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--rows", type=int, default=None, help="training rows per GPU shard")
@@ -206,6 +214,94 @@ def cpu_baseline_build(args, D: int) -> dict:
                       f"OpenMP {cb.omp_threads()} threads (oracle/lr_cpu_omp.c)"}
 
 
+def run_c1_e2e(args) -> None:
+    """local.sh's job through the drop-in driver: `bin/distlr` with local.sh's
+    environment and 2 workers (two loopback ranks on GPU 0), args.steps
+    epochs, timed from process start to exit (parse, GPU init, training,
+    tests, model files) and over its epoch loops (DISTLR_TIMING), `warmup`
+    runs first; then the reference-structure CPU run of the same job on the
+    same files (oracle/ref_loop.cc, 2 worker threads).  value = training
+    samples (2 x rows x epochs) / end-to-end seconds."""
+    global dlr
+    import re
+    import tempfile
+    import distlr_amd as dlr  # noqa: F811  -- host-only entry points here (generator, model text): no GPU
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpu_baselines as cb  # baseline only, never the product
+    W, D, epochs = 2, args.features, args.steps
+    exe = os.path.join(ROOT, "dist-lr_amd", "bin", "distlr")
+    with tempfile.TemporaryDirectory() as d:
+        for sub_ in ("train", "test", "models"):
+            os.makedirs(os.path.join(d, sub_))
+        for p in range(W):
+            make_shard(args, args.rows, p + 1).write_libsvm(os.path.join(d, "train", f"part-00{p + 1}"))
+        make_shard(args, 16281, 100).write_libsvm(os.path.join(d, "test", "part-001"))
+        env = dict(os.environ, DATA_DIR=d, NUM_FEATURE_DIM=str(D), NUM_ITERATION=str(epochs), BATCH_SIZE="-1",
+                   TEST_INTERVAL="10", SYNC_MODE="1", LEARNING_RATE=str(args.lr), DMLC_NUM_WORKER=str(W),
+                   DISTLR_TIMING="1")
+        env.pop("DMLC_ROLE", None)
+        runs = []
+        for _ in range(args.warmup + 1):
+            t0 = time.perf_counter()
+            r = subprocess.run([exe], env=env, capture_output=True, text=True, timeout=600)
+            wall = time.perf_counter() - t0
+            if r.returncode != 0:
+                sys.exit(f"bin/distlr failed ({r.returncode}): {r.stderr[-2000:]}")
+            loops = [float(x) for x in re.findall(r"epoch loop ([0-9.eE+-]+) s", r.stderr)]
+            acc = re.findall(r"Iteration (\d+), accuracy: (\S+)", r.stdout)
+            runs.append((wall, max(loops) if loops else None, acc))
+        with open(os.path.join(d, "models", "part-001")) as f:
+            model0 = f.read()
+        w_ref, steps, sec, corr, n_test = cb.reference_local_run(d, W, D, epochs, -1, 10, args.lr, 0)
+    wall, loop, acc = runs[-1]
+    samples = W * args.rows * epochs
+    ref_acc = f"{cb_accuracy(corr, n_test)}"
+    line = {
+        "metric": "training samples/sec (whole node)",
+        "value": round(samples / wall, 1),
+        "unit": "samples/s",
+        "n_gpus": 1,
+        "steps": epochs,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall / epochs * 1000.0, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded gen_data.py-shaped a9a-like libsvm text files, binary values)",
+        "config": {"workload": f"{args.label}: examples/local.sh's job -- {W} workers x {args.rows} rows x {D} "
+                               f"features, {args.nnz} nnz/row, B = -1, {epochs} epochs, Test every 10 epochs on "
+                               f"16,281 rows, SYNC_MODE=1, LEARNING_RATE={args.lr}",
+                   "name": "c1e2e", "driver": "dist-lr_amd/bin/distlr (main.cc's drop-in), loopback group of 2 "
+                                              "ranks on GPU 0", "parallelism": "dp2 (one GPU)"},
+        "end_to_end_s": round(wall, 4),
+        "epoch_loop_s": loop,
+        "epoch_loop_samples_per_s": round(samples / loop, 1) if loop else None,
+        "first_run_s": round(runs[0][0], 4),
+        "step": "one epoch of local.sh's job = one B = -1 step per worker (+ a Test every 10 epochs)",
+        "accuracy_lines": [f"Iteration {i}, accuracy: {a}" for i, a in acc],
+        "reference_final_accuracy": ref_acc,
+        "final_accuracy_equal": bool(acc) and acc[-1][1] == ref_acc,
+        "model_part001_equals_reference_weights": model0 == dlr.format_model(w_ref),
+        "roofline": None,
+        "roofline_note": "latency-bound job (one 8,140-row step per worker per epoch): no HBM roofline; the "
+                         "kernels' own line is --config c1",
+        "cpu_baseline": {"value": round(steps / sec, 1), "unit": "samples/s", "cores": W, "host_cpus": os.cpu_count(),
+                         "kind": "port",
+                         "sample": f"the same job on the same files: {W} worker threads + in-process server, "
+                                   f"per-epoch re-parse, lr.cc/main.cc loop structure (oracle/ref_loop.cc), "
+                                   f"{epochs} epochs, {steps} sample-steps in {sec:.2f} s"},
+    }
+    print(json.dumps(line), flush=True)
+
+
+def cb_accuracy(correct: int, n: int) -> str:
+    """lr.cc:59-62's accuracy text (ostream %g of the float ratio)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # the checker's formatter
+    return oracle.format_g(oracle.accuracy(correct, n))
+
+
 def free_port() -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
         sk.bind(("127.0.0.1", 0))
@@ -260,6 +356,11 @@ def run_rank(args):
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if args.kind == "e2e":
+        if world != 1:
+            sys.exit("--config c1e2e runs bin/distlr's own 2-worker job: --gpus 1")
+        run_c1_e2e(args)  # before anything here touches the GPU (the child owns it)
+        return
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         sys.exit(f"--gpus {args.gpus} but WORLD_SIZE={world}")

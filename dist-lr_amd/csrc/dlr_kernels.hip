@@ -670,6 +670,14 @@ __global__ __launch_bounds__(256) void k_long_combine(const uint32_t *__restrict
 // s_memrealtime stamps at the kernel's phase boundaries.
 #ifdef DLR_STAMPS
 __device__ unsigned long long *g_stamp = nullptr;
+}  // namespace
+}  // namespace dlr
+// tools/c2_stamps.py (a DLR_STAMPS build of the library): where the stamps go
+extern "C" int dlr_debug_stamp_buffer(void *d) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(dlr::g_stamp), &d, sizeof(d));
+}
+namespace dlr {
+namespace {
 #define DLR_STAMP(slot)                                                                      \
     do {                                                                                     \
         if (threadIdx.x == 0) g_stamp[blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
@@ -943,6 +951,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     for (int p = 0; p < 2; ++p) {
         if (p >= P) break;  // uniform
         if (p > 0) {
+            DLR_STAMP(2);
             __syncthreads();  // every wave is done reading the previous phase
             DLR_STAMP(3);
             fill((int64_t)p * R);  // resid is padded to P*R floats
@@ -1031,8 +1040,14 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     if (PM) {
         pm.stage_offsets(reinterpret_cast<uint32_t *>(smem + kPmSlice));
         __syncthreads();
+        DLR_STAMP(6);
         pm.store(pn, smem, reinterpret_cast<const uint32_t *>(smem + kPmSlice), pm_p);
     }
+#ifdef DLR_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    DLR_STAMP(7);
+#endif
 }
 
 // ---------------------------------------------------------------------------

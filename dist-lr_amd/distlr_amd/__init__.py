@@ -17,6 +17,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 LIB_PATH = os.path.join(PKG, "lib", "libdistlr_amd.so")
+# diagnostic tools only (tools/c2_stamps.py): a variant build of the same library
+LIB_PATH = os.environ.get("DLR_LIB", LIB_PATH)
 
 MODE_SYNC_MEAN = 0
 MODE_SYNC_LAST = 1

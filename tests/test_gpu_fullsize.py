@@ -1,0 +1,133 @@
+"""Full-size parity of the reference summation orders, and the world > 1
+engine path at the north-star shapes ("Next round" items 1 and 3).
+
+* C3 (12.5M-row Criteo-shaped shard, B = -1) with DLR_LONG_COLUMN=0: every
+  column is ONE sequential fp32 sum in batch-row order (lr.cc:35-39), carried
+  across the 2^20-row bands -> the weights after each of two steps are
+  BITWISE the oracle's, with the centred init whose residuals are general
+  fp32 values (the default long-column phase tree is within tolerance
+  instead: test_gpu_c3_full.py).
+* C4 (D = 4,096, B = 65,536) with DLR_DENSE_GRAD=seq at the bench's lr 0.2:
+  a full epoch of 16 batches (the last wrapping to row 0), bitwise after
+  every step (margin: one chain per row in column order, lr.cc:108-112;
+  gradient: one chain per column in row order, lr.cc:35-39).
+* W = 8 ranks on the loopback group at C3's structure with 2.2M-row shards
+  (the default 2^20-row bands apply from 2^21 rows): relabeling from the
+  summed counts, bands, hot-weight margin, key-range all-to-all of 2^24
+  weights over 8 ranks (main.cc:57-78's merge in rank order), 2 steps --
+  bitwise with DLR_LONG_COLUMN=0, within 1e-5*|b| + 1e-6 by default.
+* The fused dense path (C4's default, D = 4,096, B = 65,536) on W = 2 and
+  W = 4 loopback ranks, within its tolerance of the oracle's W-worker run.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import distlr_amd as dlr
+import oracle
+from engine_driver import run_group
+from test_gpu_parity import assert_same_weights
+
+pytestmark = pytest.mark.gpu
+
+
+def within_bar(got, want, what=""):
+    a, b = got.astype(np.float64), want.astype(np.float64)
+    bad = np.abs(a - b) > 1e-5 * np.abs(b) + 1e-6
+    assert not bad.any(), f"{what}: {int(bad.sum())} weights outside 1e-5*|b| + 1e-6"
+
+
+def test_c3_full_size_reference_order_bitwise(monkeypatch):
+    monkeypatch.setenv("DLR_LONG_COLUMN", "0")
+    D, ROWS, LR = 1 << 24, 12_500_000, 0.2
+    ds = dlr.Dataset.generate_hashed(ROWS, D, 39, seed=10, stream=1)
+    rp, col, val, lab = ds.csr()
+    csr = (rp, col, val)
+    rows = oracle.batch_rows(ROWS, -1, 0)
+    w0 = dlr.init_weight(D)
+    w0 = ((w0 - np.float32(0.5)) / np.float32(5.0)).astype(np.float32)  # centred: general fp32 residuals
+    assert np.bincount(col, minlength=D).max() > 500_000  # the ~10^6-entry chains are there
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(w0)
+        assert eng.load_train(ds, -1) == 1
+        assert eng.train_band_rows() == 1 << 20 and eng.train_relabeled()
+        w = w0.copy()
+        for step in range(2):
+            eng.train_step(0, LR, 1.0)
+            oracle.server_update(w, [oracle.grad_csr(csr, lab, rows, w)], LR)
+            assert_same_weights(eng.get_weights(), w, f"C3 reference order, step {step}")
+    finally:
+        eng.close()
+
+
+def test_c4_full_epoch_reference_order_bitwise(monkeypatch):
+    monkeypatch.setenv("DLR_DENSE_GRAD", "seq")
+    D, B, lr = 4096, 65536, 0.2
+    dd = dlr.DenseDataset.generate(1_000_000, D, seed=10, stream=2)
+    X, y = dd.arrays()
+    w0 = dlr.init_weight(D)
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(w0)
+        nb = eng.load_train_dense(dd, B)
+        assert nb == 16
+        w = w0.copy()
+        for b in range(nb):
+            eng.train_step(b, lr, 1.0)
+            oracle.server_update(w, [oracle.grad_dense(X, y, oracle.batch_rows(len(y), B, b), w)], lr)
+            assert_same_weights(eng.get_weights(), w, f"C4 reference order, step {b}")
+    finally:
+        eng.close()
+
+
+def _c3_shards(W, rows):
+    return [dlr.Dataset.generate_hashed(rows, 1 << 24, 39, seed=10, stream=r + 1) for r in range(W)]
+
+
+def _csr(ds):
+    rp, col, val, lab = ds.csr()
+    return (rp, col, val), lab
+
+
+@pytest.fixture(scope="module")
+def c3_w8():
+    shards = _c3_shards(8, 2_200_000)
+    return shards, [_csr(s) for s in shards]
+
+
+@pytest.mark.parametrize("order", ["reference", "default"])
+def test_c3_eight_ranks_loopback(monkeypatch, c3_w8, order):
+    shards, csrs = c3_w8
+    if order == "reference":
+        monkeypatch.setenv("DLR_LONG_COLUMN", "0")
+    D = 1 << 24
+    eng = dlr.Engine(D)
+    try:  # the default choices at this shard size (one rank's view)
+        eng.set_weights(dlr.init_weight(D))
+        eng.load_train(shards[0], -1)
+        assert eng.train_band_rows() == 1 << 20 and eng.train_relabeled() and eng.train_unit_values()
+    finally:
+        eng.close()
+    got = run_group(shards, D, 2, -1, 0.2)
+    orc = oracle.run_worker(csrs, D, 2, -1, 0.2)
+    if order == "reference":
+        assert_same_weights(got.w, orc.w, "W = 8, reference order")
+    else:
+        within_bar(got.w, orc.w, "W = 8, long-column phases")
+
+
+@pytest.mark.parametrize("W", [2, 4])
+def test_fused_dense_c4_shape_ranks(W):
+    D, B, rows = 4096, 65536, 150_000  # 3 batches per epoch, the last wrapping
+    shards = [dlr.DenseDataset.generate(rows, D, seed=10, stream=r + 5) for r in range(W)]
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(dlr.init_weight(D))
+        assert eng.load_train_dense(shards[0], B) == 3
+    finally:
+        eng.close()
+    got = run_group(shards, D, 2, B, 0.2, dense=True)
+    orc = oracle.run_worker([s.arrays() for s in shards], D, 2, B, 0.2, sparse=False)
+    within_bar(got.w, orc.w, f"fused dense, W = {W}")

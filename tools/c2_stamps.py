@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Per-workgroup timeline of the C2 gradient kernel (k_grad_lds with the
+fused pass 1) from s_memrealtime stamps (100 MHz), on the bench's C2 shard
+shape.  Loads the DLR_STAMPS build of the library (make -C dist-lr_amd
+stamps) through DLR_LIB.  Development tool, never part of the product.
+
+  python tools/c2_stamps.py [--rows N] [--steps K] [--reps R]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("DLR_LIB", os.path.join(ROOT, "dist-lr_amd", "lib", "libdistlr_amd_stamps.so"))
+sys.path.insert(0, os.path.join(ROOT, "dist-lr_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (one HIP runtime: torch's)
+
+import distlr_amd as dlr  # noqa: E402
+
+SLOTS = {0: "start", 1: "ph0 go", 2: "ph0 done", 3: "fill1 out", 4: "ph1 go", 5: "compute end", 6: "pass1 go",
+         7: "end"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=2_000_000)
+    ap.add_argument("--features", type=int, default=1_000_000)
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    assert "stamps" in dlr.LIB_PATH, dlr.LIB_PATH
+    f = dlr.lib.dlr_debug_stamp_buffer
+    f.argtypes, f.restype = [C.c_void_p], C.c_int
+    D = a.features
+    G = (D + 4095) // 4096
+    buf = torch.zeros(G * 8, dtype=torch.int64, device="cuda")
+    assert f(buf.data_ptr()) == 0
+    ds = dlr.Dataset.generate(a.rows, D, 50, value_mode=1, seed=10, stream=1)
+    eng = dlr.Engine(D)
+    eng.set_weights(dlr.init_weight(D))
+    nb = eng.load_train(ds, a.batch)
+    print(f"layout {eng.train_layout()} product margin {eng.train_product_margin()} batches {nb} grid {G}")
+    k = 0
+    rel = {s: [] for s in SLOTS}
+    for rep in range(a.reps + 1):
+        for _ in range(a.steps):
+            eng.train_step(k % nb, 0.2, 1.0)
+            k += 1
+        eng.sync()
+        torch.cuda.synchronize()
+        st = buf.cpu().numpy().reshape(G, 8).astype(np.float64)
+        if rep == 0:
+            continue  # warm-up
+        t0 = st[:, 0].min()
+        for s in SLOTS:
+            if st[:, s].min() > 0:
+                rel[s].append((st[:, s] - t0) * 0.01)
+    print(f"{a.reps} launches, us from the first workgroup's start (percentiles over {G} workgroups)")
+    for s, nm in SLOTS.items():
+        if not rel[s]:
+            continue
+        v = np.concatenate(rel[s])
+        print("  %-12s min %6.2f  p10 %6.2f  med %6.2f  p90 %6.2f  max %6.2f" % (
+            nm, v.min(), np.percentile(v, 10), np.median(v), np.percentile(v, 90), v.max()))
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
