@@ -680,13 +680,25 @@ namespace dlr {
 namespace {
 #define DLR_STAMP(slot)                                                                      \
     do {                                                                                     \
-        if (threadIdx.x == 0) g_stamp[blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+        if (threadIdx.x == 0) g_stamp[blockIdx.x * 16 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define DLR_STAMP(slot) \
     do {                \
     } while (0)
 #endif
+// Timing-only ablations of the stamps build (tools/c2_stamps.py; WRONG
+// results): bit 0 no first residual fill, bit 1 no phase-0 window loads,
+// bit 2 no pass 1, bit 3 no weight loads.  Always 0 in the product library.
+// Bit 4 (a variant, same results): pass 1's product stores write-through
+// (sc1), so they leave L2 as they issue instead of in the kernel-end flush.
+#ifndef DLR_ABL
+#define DLR_ABL 0
+#endif
+#ifndef DLR_PM_SC1
+#define DLR_PM_SC1 ((DLR_ABL & 16) != 0)
+#endif
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kGradWaves = 16;  // waves per workgroup
 constexpr int kGradNG = 4;      // 64-column groups per wave
@@ -763,6 +775,8 @@ struct PmPass1 {
     __device__ __forceinline__ void store(const DevPm &pm, const float *s_w, const uint32_t *s_po,
                                           float *__restrict__ p) {
         const bool unit = pm.val == nullptr;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p, 0, 0x7FFFFFFF, 0x00020000);
+        (void)rs;
         for (uint32_t g0 = c0; g0 < c1; g0 += U * NT) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -775,7 +789,13 @@ struct PmPass1 {
                     q.y = s_w[(x >> 12) & 0xFFFu] * (unit ? 1.0f : v[u].y);
                     q.z = s_w[(x >> 24) | ((y & 0xFu) << 8)] * (unit ? 1.0f : v[u].z);
                     q.w = s_w[(y >> 4) & 0xFFFu] * (unit ? 1.0f : v[u].w);
-                    *reinterpret_cast<float4 *>(p + s_po[k] + j) = q;
+                    if (DLR_PM_SC1) {
+                        const u32x4 b = {__float_as_uint(q.x), __float_as_uint(q.y), __float_as_uint(q.z),
+                                         __float_as_uint(q.w)};
+                        __builtin_amdgcn_raw_buffer_store_b128(b, rs, (int)((s_po[k] + j) * 4u), 0, 16);
+                    } else {
+                        *reinterpret_cast<float4 *>(p + s_po[k] + j) = q;
+                    }
                 }
             }
             if (g0 + U * NT < c1) fetch(pm, g0 + U * NT);
@@ -895,7 +915,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
         const int64_t gc = gv ? g : ng - 1;
         const int64_t j = g * 64 + lane;
         const bool ok = gv && j < D;
-        wj[gi] = w[j < D ? j : D - 1];
+        wj[gi] = (DLR_ABL & 8) ? 0.0f : w[j < D ? j : D - 1];
         acc[gi] = 0.0f;
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
@@ -913,6 +933,11 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     auto windows = [&](int p) {
 #pragma unroll
         for (int gi = 0; gi < NG; ++gi) {
+            if ((DLR_ABL & 2) && p == 0) {
+                rq[gi][p] = ushort4{0, 0, 0, 0};
+                vq[gi][p] = make_float4(0.f, 0.f, 0.f, 0.f);
+                continue;
+            }
             const unsigned e = bs[gi][p] + lane * 4;  // entries are padded: always in bounds
             if (NTW) {
                 rq[gi][p] = load_stream(reinterpret_cast<const ushort4 *>(pc.row + e));
@@ -940,13 +965,19 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     // the rest of phase 0 computes instead of delaying its start.
     DLR_STAMP(0);
     windows(0);
-    fill(0);
-    if (PM) {
+    if (!(DLR_ABL & 1)) fill(0);
+    DLR_STAMP(8);
+#ifdef DLR_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    DLR_STAMP(9);
+#endif
+    if (PM && !(DLR_ABL & 4)) {
         // the next batch's slice list: in flight under the whole gradient
         asm volatile("" ::: "memory");
         pm.load(pn, blockIdx.x);
         asm volatile("" ::: "memory");
     }
+    DLR_STAMP(10);
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
         if (p >= P) break;  // uniform
@@ -1041,7 +1072,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
         pm.stage_offsets(reinterpret_cast<uint32_t *>(smem + kPmSlice));
         __syncthreads();
         DLR_STAMP(6);
-        pm.store(pn, smem, reinterpret_cast<const uint32_t *>(smem + kPmSlice), pm_p);
+        if (!(DLR_ABL & 4)) pm.store(pn, smem, reinterpret_cast<const uint32_t *>(smem + kPmSlice), pm_p);
     }
 #ifdef DLR_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

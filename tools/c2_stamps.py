@@ -22,8 +22,8 @@ import torch  # noqa: E402  (one HIP runtime: torch's)
 
 import distlr_amd as dlr  # noqa: E402
 
-SLOTS = {0: "start", 1: "ph0 go", 2: "ph0 done", 3: "fill1 out", 4: "ph1 go", 5: "compute end", 6: "pass1 go",
-         7: "end"}
+SLOTS = {0: "start", 8: "win0+fill0 out", 9: "w0 drained", 10: "pass1 ld out", 1: "ph0 go", 2: "ph0 done",
+         3: "fill1 out", 4: "ph1 go", 5: "compute end", 6: "pass1 go", 7: "end"}
 
 
 def main():
@@ -39,7 +39,7 @@ def main():
     f.argtypes, f.restype = [C.c_void_p], C.c_int
     D = a.features
     G = (D + 4095) // 4096
-    buf = torch.zeros(G * 8, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(G * 16, dtype=torch.int64, device="cuda")
     assert f(buf.data_ptr()) == 0
     ds = dlr.Dataset.generate(a.rows, D, 50, value_mode=1, seed=10, stream=1)
     eng = dlr.Engine(D)
@@ -54,13 +54,14 @@ def main():
             k += 1
         eng.sync()
         torch.cuda.synchronize()
-        st = buf.cpu().numpy().reshape(G, 8).astype(np.float64)
+        st = buf.cpu().numpy().reshape(G, 16).astype(np.float64)
         if rep == 0:
             continue  # warm-up
         t0 = st[:, 0].min()
         for s in SLOTS:
             if st[:, s].min() > 0:
                 rel[s].append((st[:, s] - t0) * 0.01)
+    print(os.path.basename(dlr.LIB_PATH))
     print(f"{a.reps} launches, us from the first workgroup's start (percentiles over {G} workgroups)")
     for s, nm in SLOTS.items():
         if not rel[s]:
@@ -68,6 +69,16 @@ def main():
         v = np.concatenate(rel[s])
         print("  %-12s min %6.2f  p10 %6.2f  med %6.2f  p90 %6.2f  max %6.2f" % (
             nm, v.min(), np.percentile(v, 10), np.median(v), np.percentile(v, 90), v.max()))
+    # the step itself (margin + this kernel + the boundaries): K steps between two syncs
+    import time
+    for _ in range(3):
+        eng.sync()
+        t0 = time.perf_counter()
+        for _ in range(500):
+            eng.train_step(k % nb, 0.2, 1.0)
+            k += 1
+        eng.sync()
+        print("  step %.2f us (500 steps, wall)" % ((time.perf_counter() - t0) / 500 * 1e6))
     eng.close()
 
 

@@ -1392,8 +1392,8 @@ int main(int argc, char **argv) {
         // the stamp buffer must be set before ANY launch of the stamped kernel
         const int G = (int)((ngr + 63) / 64);
         unsigned long long *d_st = nullptr;
-        CK(hipMalloc(&d_st, (size_t)G * 8 * 8));
-        CK(hipMemset(d_st, 0, (size_t)G * 8 * 8));
+        CK(hipMalloc(&d_st, (size_t)G * 16 * 8));  // dlr_kernels.hip DLR_STAMP: 16 slots per workgroup
+        CK(hipMemset(d_st, 0, (size_t)G * 16 * 8));
         CK(hipMemcpyToSymbol(HIP_SYMBOL(dlr::g_stamp), &d_st, sizeof(d_st)));
         CK(hipMemset(d_g2, 0, D * 4));
         t = time_us(reps, [&] { CK(dlr::launch_grad_lds(pc, D, B, d_rp, d_w, d_g2, 0.2f, 1.0f, false, 0)); });
@@ -1456,14 +1456,14 @@ int main(int argc, char **argv) {
             CK(hipFree(fo));
         }
         CK(hipDeviceSynchronize());
-        std::vector<unsigned long long> st((size_t)G * 8);
-        CK(hipMemcpy(st.data(), d_st, (size_t)G * 8 * 8, hipMemcpyDeviceToHost));
+        std::vector<unsigned long long> st((size_t)G * 16);
+        CK(hipMemcpy(st.data(), d_st, (size_t)G * 16 * 8, hipMemcpyDeviceToHost));
         unsigned long long t0 = ~0ull;
-        for (int g = 0; g < G; ++g) t0 = std::min(t0, st[g * 8]);
+        for (int g = 0; g < G; ++g) t0 = std::min(t0, st[g * 16]);
         const char *nm[6] = {"start", "ph0 go", "", "ph0 done", "ph1 go", "end"};
         for (int k : {0, 1, 3, 4, 5}) {
             std::vector<double> v;
-            for (int g = 0; g < G; ++g) v.push_back((st[g * 8 + k] - t0) * 0.01);
+            for (int g = 0; g < G; ++g) v.push_back((st[g * 16 + k] - t0) * 0.01);
             std::sort(v.begin(), v.end());
             printf("  stamp %-9s min %6.2f med %6.2f p90 %6.2f max %6.2f us\n", nm[k], v[0], v[G / 2], v[G * 9 / 10], v[G - 1]);
         }
