@@ -2471,11 +2471,13 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
     if (t.dblocked &&
         (rc = dev_alloc(c, (void **)&t.dpart, (size_t)dlr::dense_chunks(t.B) * (size_t)((D + 3) & ~int64_t(3)) * 4)))
         return rc;
-    if (c->resid_cap < t.B) {
+    // residuals: whole 4-row quads + 4 (the reference-order gradient reads them 16 bytes at a time)
+    const int64_t rneed = ((t.B + 3) & ~int64_t(3)) + 4;
+    if (c->resid_cap < rneed) {
         dev_free(c, c->resid);
         c->resid = nullptr;
-        if ((rc = dev_alloc(c, (void **)&c->resid, (size_t)t.B * 4))) return rc;
-        c->resid_cap = t.B;
+        if ((rc = dev_alloc(c, (void **)&c->resid, (size_t)rneed * 4))) return rc;
+        c->resid_cap = rneed;
     }
     t.bytes = (int64_t)(ds->X.size() * 4 + ds->label.size() * 4);
     t.loaded = true;

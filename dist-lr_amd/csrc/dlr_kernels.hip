@@ -32,6 +32,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "dlr_kernels.h"
 
@@ -50,6 +51,40 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a
+// workgroup-scope release + acquire, which on gfx950 waits vmcnt(0): it
+// drains every global load in flight (loads issued early for later phases,
+// LDS-DMA prefetches) at every barrier.  LDS-DMA data is published by the
+// issuing wave's own s_waitcnt vmcnt before the barrier.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// LDS accesses the compiler cannot see.  A compiler-issued LDS access that
+// may alias an in-flight LDS-DMA gets an s_waitcnt vmcnt(0) -- every global
+// load in flight drains first.  Callers order these after their DMA with
+// explicit vmcnt waits and use the results only after lds_wait*().
+typedef float v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+template <int OFF = 0>
+__device__ __forceinline__ float lds_rd32(uint32_t a) {
+    float v;
+    asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(a), "n"(OFF));
+    return v;
+}
+__device__ __forceinline__ void lds_wr128(uint32_t a, v4f v) {
+    asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void lds_wait1(float &a) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a)); }
+__device__ __forceinline__ void lds_wait4(float &a, float &b, float &c, float &d) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
 }
 
 template <typename T>
@@ -732,10 +767,6 @@ struct PmPass1 {
     float4 v[U];
     uint32_t po[NPO];
     uint32_t c0 = 0, c1 = 0;
-    // vector-memory instructions load() issues per thread, always (clamped
-    // addresses; the lists are padded): k_grad_lds waits for its fill with
-    // s_waitcnt vmcnt(kLoads) while these are still in flight
-    static constexpr int kLoads = NPO + 2 * U;
     __device__ __forceinline__ void fetch(const DevPm &pm, uint32_t g0) {
         // unit values: a dummy load (the list's own words, in range) keeps
         // the instruction count fixed
@@ -749,8 +780,15 @@ struct PmPass1 {
             v[u] = load_stream(vp + (gc >> vs));
         }
     }
-    __device__ __forceinline__ void load(const DevPm &pm, int s, int part = 0, int nparts = 1) {
-        const uint32_t b0 = pm.lbeg[s] / 4, b1 = pm.lbeg[s + 1] / 4;
+    // The slice's list range and chunk offsets (no dependence on anything):
+    // k_grad_lds issues these first, so the fetch() that needs c0 waits for
+    // them alone, not for the loads issued in between (vmcnt is in order).
+    __device__ __forceinline__ void bounds(const DevPm &pm, int s, int part = 0, int nparts = 1) {
+        // vector loads: a scalar load here made the compiler wait for it
+        // (lgkmcnt(0)) before issuing anything else of the prologue
+        int vz;  // a zero the compiler cannot prove uniform: keeps these loads in VGPRs
+        asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+        const uint32_t b0 = pm.lbeg[s + vz] / 4, b1 = pm.lbeg[s + 1 + vz] / 4;
         const uint32_t n = b1 - b0, per = (n + nparts - 1) / nparts;
         c0 = b0 + min(n, per * part);
         c1 = b0 + min(n, per * (part + 1));
@@ -760,6 +798,9 @@ struct PmPass1 {
             const int64_t i = u * NT + threadIdx.x;
             po[u] = pm.pofs[(int64_t)s * nb + (i < nb ? i : nb - 1)];
         }
+    }
+    __device__ __forceinline__ void load(const DevPm &pm, int s, int part = 0, int nparts = 1) {
+        bounds(pm, s, part, nparts);
         fetch(pm, c0);
     }
     __device__ __forceinline__ void stage_offsets(uint32_t *s_po) const {
@@ -900,10 +941,12 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // uniform: scalar block loads
     float *s_p = smem + R + wv * kBlkPad;
+    const uint32_t s_r_a = lds_addr(s_r), s_p_a = lds_addr(s_p);
     const int P = pc.phases;
     const int64_t ng = (D + 63) / 64;
     const int64_t gfirst = (int64_t)blockIdx.x * (kGradWaves * NG) + wv;
     PmPass1<kGradWaves * kWave, 4> pm;
+    if (PM && !(DLR_ABL & 4)) pm.bounds(pn, blockIdx.x);  // first (PmPass1::bounds)
     unsigned bs[NG][2], off[NG][2], cnt[NG][2], nblk[NG][2];
     float acc[NG], wj[NG];
     ushort4 rq[NG][2];
@@ -971,50 +1014,46 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     DLR_STAMP(9);
 #endif
-    if (PM && !(DLR_ABL & 4)) {
-        // the next batch's slice list: in flight under the whole gradient
-        asm volatile("" ::: "memory");
-        pm.load(pn, blockIdx.x);
-        asm volatile("" ::: "memory");
-    }
     DLR_STAMP(10);
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
         if (p >= P) break;  // uniform
         if (p > 0) {
             DLR_STAMP(2);
-            __syncthreads();  // every wave is done reading the previous phase
+            lds_barrier();  // every wave is done reading the previous phase
             DLR_STAMP(3);
             fill((int64_t)p * R);  // resid is padded to P*R floats
         }
-        if (PM && p == 0)  // the fill, not the pass-1 loads issued after it
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(decltype(pm)::kLoads) : "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA fill (not tracked by the compiler)
+        lds_barrier();
         DLR_STAMP(1 + 3 * p);
 #pragma unroll
         for (int gi = 0; gi < NG; ++gi) {
-            if (p == 0 && gi == 1 && P > 1) {
+            if (p == 0 && gi == 1) {
+                // phase 1's windows and the next batch's pass-1 slice list
+                // (its range was loaded first thing) stream while the rest of
+                // phase 0 computes: issued here, after the first group's
+                // compiler-placed waits, they do not delay phase 0's start
                 asm volatile("" ::: "memory");
-                windows(1);
+                if (P > 1) windows(1);
+                if (PM && !(DLR_ABL & 4)) pm.fetch(pn, pm.c0);
                 asm volatile("" ::: "memory");
             }
             if (gfirst + kGradWaves * gi >= ng) break;  // wave-uniform
             // products of the block's entries only: the window's other slots
             // (the next blocks' entries) are never read, so those lanes skip
             // their residual gathers (LDS bank cycles) and the slab write
+            // (LDS through lds_* asm: the pass-1 loads stay in flight)
             if ((unsigned)lane * 4 < nblk[gi][p]) {
                 const ushort4 r4 = rq[gi][p];
                 const float4 v4 = vq[gi][p];
-                float4 q;
-                q.x = s_r[r4.x] * v4.x;
-                q.y = s_r[r4.y] * v4.y;
-                q.z = s_r[r4.z] * v4.z;
-                q.w = s_r[r4.w] * v4.w;
-                *reinterpret_cast<float4 *>(s_p + lane * 4) = q;
+                float g0 = lds_rd32(s_r_a + 4u * r4.x), g1 = lds_rd32(s_r_a + 4u * r4.y);
+                float g2 = lds_rd32(s_r_a + 4u * r4.z), g3 = lds_rd32(s_r_a + 4u * r4.w);
+                lds_wait4(g0, g1, g2, g3);
+                const v4f q = {g0 * v4.x, g1 * v4.y, g2 * v4.z, g3 * v4.w};
+                lds_wr128(s_p_a + 16u * lane, q);
             }
-            wave_sync();
+            lds_wait();  // the slab is complete (one wave)
             // this lane's column: cnt products in order from off.  The first
             // eight are read at immediate offsets from s_p + o (the slab is
             // padded, so no clamping) and added while any lane still has one
@@ -1023,15 +1062,14 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
             // runs continue in a general loop.  Per product: compare, add,
             // select -- this loop is what bounds the kernel (VALU issue).
             const unsigned o = off[gi][p], c = cnt[gi][p];
-            const float *__restrict__ sp = s_p + o;
+            const uint32_t sp = s_p_a + 4u * o;
             float a = acc[gi];
+            // all eight reads issue together (one LDS round trip)
             float x[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) x[u] = sp[u];
-            // all eight reads issue together (one LDS round trip); without
-            // this the compiler sinks each read into its step of the loop
-            asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]),
-                         "v"(x[7]));
+            x[0] = lds_rd32<0>(sp), x[1] = lds_rd32<4>(sp), x[2] = lds_rd32<8>(sp), x[3] = lds_rd32<12>(sp);
+            x[4] = lds_rd32<16>(sp), x[5] = lds_rd32<20>(sp), x[6] = lds_rd32<24>(sp), x[7] = lds_rd32<28>(sp);
+            lds_wait4(x[0], x[1], x[2], x[3]);
+            lds_wait4(x[4], x[5], x[6], x[7]);
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const bool take = (unsigned)u < c;
@@ -1040,37 +1078,53 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
                 a = take ? t : a;
             }
             for (unsigned k = 8; __builtin_amdgcn_ballot_w64(k < c) != 0; ++k) {
-                const float xv = s_p[min(o + k, (unsigned)kBlk - 1)];
+                float xv = lds_rd32(s_p_a + 4u * min(o + k, (unsigned)kBlk - 1));
+                lds_wait1(xv);
                 if (k < c) a = a + xv;
             }
             acc[gi] = a;
             wave_sync();
         }
     }
+    // a wave with no column group left the loop before issuing its share
+    // of the pass-1 list (every thread takes part in pass 1)
+    if (PM && !(DLR_ABL & 4) && gfirst >= ng) pm.fetch(pn, pm.c0);
 #ifdef DLR_STAMPS
     __syncthreads();
     DLR_STAMP(5);
 #endif
-    if (PM) __syncthreads();  // every wave is done with s_r: pass 1 reuses it
+    if (PM) lds_barrier();  // every wave is done with s_r: pass 1 reuses it
+    // lr.cc:40 divides by B; for a power-of-two B a product with the exact
+    // reciprocal IS that correctly rounded quotient (C2: B = 65,536), and the
+    // f64 division sequence x 4 groups x 4 waves per SIMD costs ~1 us here
+    auto update = [&](auto pow2) {
+        constexpr bool P2 = decltype(pow2)::value;
+        const float rBf = P2 ? 1.0f / Bf : 0.0f;
+        const double rBd = P2 ? 1.0 / Bd : 0.0;
 #pragma unroll
-    for (int gi = 0; gi < NG; ++gi) {
-        const int64_t j = (gfirst + kGradWaves * gi) * 64 + lane;
-        if (gfirst + kGradWaves * gi >= ng || j >= D) continue;
-        const float cw = C * wj[gi];
-        const float l2 = cw / Bf;
-        const float g = (float)((double)acc[gi] / Bd + (double)l2);
-        if (FUSED) {
-            const float step = lr * g;
-            const float wn = wj[gi] - step;
-            w[j] = wn;
-            if (PM) smem[(wv + kGradWaves * gi) * 64 + lane] = wn;  // column j - kPmSlice*blockIdx.x
-        } else {
-            gout[j] = g;
+        for (int gi = 0; gi < NG; ++gi) {
+            const int64_t j = (gfirst + kGradWaves * gi) * 64 + lane;
+            if (gfirst + kGradWaves * gi >= ng || j >= D) continue;
+            const float cw = C * wj[gi];
+            const float l2 = P2 ? cw * rBf : cw / Bf;
+            const float g = (float)((P2 ? (double)acc[gi] * rBd : (double)acc[gi] / Bd) + (double)l2);
+            if (FUSED) {
+                const float step = lr * g;
+                const float wn = wj[gi] - step;
+                w[j] = wn;
+                if (PM) smem[(wv + kGradWaves * gi) * 64 + lane] = wn;  // column j - kPmSlice*blockIdx.x
+            } else {
+                gout[j] = g;
+            }
         }
-    }
+    };
+    if ((B & (B - 1)) == 0)
+        update(std::true_type{});
+    else
+        update(std::false_type{});
     if (PM) {
         pm.stage_offsets(reinterpret_cast<uint32_t *>(smem + kPmSlice));
-        __syncthreads();
+        lds_barrier();
         DLR_STAMP(6);
         if (!(DLR_ABL & 4)) pm.store(pn, smem, reinterpret_cast<const uint32_t *>(smem + kPmSlice), pm_p);
     }
@@ -1667,6 +1721,164 @@ __global__ __launch_bounds__(256) void k_dense_grad_seq(DevDense dd, int64_t fir
     }
 }
 
+// K6b, reference order at C4's scale ("chain"; D % 4 == 0): lr.cc:35-39's
+// per-column chain G_j = (((+0 + p_0j) + p_1j) + ...) over the batch rows in
+// order, p_ij = fl32(r_i * x_ij) -- bitwise k_dense_grad_seq -- but with the
+// chain as the ONLY work of its lane.  A column's 65,536 dependent adds are
+// the floor (~4 cycles each), so everything else moves off the chain lane:
+// workgroup = kChainCols columns (256 workgroups at D = 4,096: every CU),
+//   waves 1-3  stream the batch rows' kChainCols-column segments (64 B) and
+//              the residuals into an LDS ring by LDS-DMA, kChainAhead slots of
+//              kChainRows rows in flight, and turn each landed slot into the
+//              products, transposed: s_p[column][row];
+//   wave 0     lane c runs column c's chain over the slot with one 16-byte
+//              LDS read per 4 rows (stride kChainPad: conflict-free).
+// One workgroup barrier per slot hands slot t's products to the chain while
+// the helpers transform slot t + 1.  Rows past B get +0 products: G starts
+// at +0 and a round-to-nearest sum is -0 only if both addends are, so G is
+// never -0 and adding +0 leaves it unchanged.  Workgroups 2m, 2m+1 (the two
+// halves of a 128-byte row line) run on one XCD (blockIdx % 8) when the grid
+// is a multiple of 16, so the line is fetched into one L2 once.
+constexpr int kChainCols = 16;
+constexpr int kChainRows = 128;
+constexpr int kChainRing = 8;   // staging slots
+constexpr int kChainAhead = 7;  // slots in flight (<= kChainRing - 1)
+constexpr int kChainPad = 132;  // s_p column stride (floats)
+constexpr int kChainXInstr = kChainRows * kChainCols * 4 / 1024;  // 1 KiB LDS-DMA instructions per slot (x)
+static_assert(kChainXInstr == 8, "waves 1 and 2 issue 4 each");
+constexpr size_t kChainLds =
+    ((size_t)kChainRing * (kChainRows * kChainCols + 256) + 2 * kChainCols * kChainPad) * 4;
+
+template <bool FUSED>
+__global__ __launch_bounds__(256) void k_dense_grad_chain(DevDense dd, int64_t first, int64_t B,
+                                                          const float *__restrict__ resid, float *__restrict__ w,
+                                                          float *__restrict__ gout, float Bf, double Bd, float lr,
+                                                          float C) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float *s_x = smem;                                               // ring x [row][col]
+    float *s_r = s_x + kChainRing * kChainRows * kChainCols;         // ring r (256 per slot; 128 used)
+    float *s_p = s_r + kChainRing * 256;                             // 2 x [col][kChainPad]
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    unsigned cg = blockIdx.x;
+    if ((gridDim.x & 15) == 0) {
+        const unsigned k = blockIdx.x >> 3;
+        cg = ((k >> 1) << 4) | ((blockIdx.x & 7) << 1) | (k & 1);
+    }
+    const int64_t c0 = (int64_t)cg * kChainCols;
+    const int64_t nslot = (B + kChainRows - 1) / kChainRows;
+    // LDS-DMA of slot t (clamped past the last slot: the wait counts stay fixed)
+    auto issue = [&](int64_t t) {
+        const int64_t ts = t < nslot ? t : nslot - 1;
+        const int ring = (int)(t % kChainRing);
+        if (wv == 1 || wv == 2) {
+            const int64_t col = min(c0 + 4 * (lane & 3), dd.D - 4);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int blk = (wv - 1) * 4 + m;  // 16 rows per instruction
+                const int64_t i = min(ts * kChainRows + blk * 16 + (lane >> 2), B - 1);
+                const float *src = dd.X + wrap_row(first + i, dd.N) * dd.D + col;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                                 (__attribute__((address_space(3))) void *)(s_x + (ring * kChainRows + blk * 16) * kChainCols),
+                                                 16, 0, 0);
+            }
+        } else if (wv == 3) {
+            // resid is allocated to a multiple of 4 floats (+4): quads in bounds
+            const int64_t q = min(ts * kChainRows + 4 * (lane & 31), (B - 1) & ~int64_t(3));
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(resid + q),
+                                             (__attribute__((address_space(3))) void *)(s_r + ring * 256), 16, 0, 0);
+        }
+    };
+    // helpers: the products of slot t into s_p[t & 1], transposed; 128 groups
+    // of 4 rows x 4 columns, lanes of waves 1 and 2
+    // The staged bytes are read with asm ds_read_b128: a compiler-issued LDS
+    // read that may alias an in-flight LDS-DMA gets an s_waitcnt vmcnt(0),
+    // which would drain the whole ring every slot (the explicit waits above
+    // already order these reads after their slot's DMA).
+    auto transform = [&](int64_t t) {
+        const int g = (wv - 1) * kWave + lane;
+        if (wv < 1 || wv > 2) return;
+        const int k = g >> 2, q = g & 3;
+        const int ring = (int)(t % kChainRing);
+        const uint32_t xr = lds_addr(s_x + (ring * kChainRows + 4 * k) * kChainCols + 4 * q);
+        const uint32_t ra = lds_addr(s_r + ring * 256 + 4 * k);
+        v4f x4v[4], r4v;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(r4v) : "v"(ra));
+        asm volatile("ds_read_b128 %0, %1" : "=v"(x4v[0]) : "v"(xr));
+        asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(x4v[1]) : "v"(xr));
+        asm volatile("ds_read_b128 %0, %1 offset:128" : "=v"(x4v[2]) : "v"(xr));
+        asm volatile("ds_read_b128 %0, %1 offset:192" : "=v"(x4v[3]) : "v"(xr));
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r4v), "+v"(x4v[0]), "+v"(x4v[1]), "+v"(x4v[2]), "+v"(x4v[3]));
+        static_assert(kChainCols * 4 == 64, "row stride of the staged slot");
+        const float rr[4] = {r4v.x, r4v.y, r4v.z, r4v.w};
+        float p[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float4 x4 = make_float4(x4v[u].x, x4v[u].y, x4v[u].z, x4v[u].w);
+            const bool ok = t * kChainRows + 4 * k + u < B;
+            p[u][0] = ok ? rr[u] * x4.x : 0.0f;
+            p[u][1] = ok ? rr[u] * x4.y : 0.0f;
+            p[u][2] = ok ? rr[u] * x4.z : 0.0f;
+            p[u][3] = ok ? rr[u] * x4.w : 0.0f;
+        }
+        // (asm writes too: a compiler-issued LDS write would wait for the ring)
+        const uint32_t pd = lds_addr(s_p + (int)(t & 1) * kChainCols * kChainPad + 4 * q * kChainPad + 4 * k);
+        static_assert(kChainPad * 4 == 528, "s_p column stride in the offsets below");
+        const v4f o0 = {p[0][0], p[1][0], p[2][0], p[3][0]}, o1 = {p[0][1], p[1][1], p[2][1], p[3][1]};
+        const v4f o2 = {p[0][2], p[1][2], p[2][2], p[3][2]}, o3 = {p[0][3], p[1][3], p[2][3], p[3][3]};
+        asm volatile("ds_write_b128 %0, %1" ::"v"(pd), "v"(o0) : "memory");
+        asm volatile("ds_write_b128 %0, %1 offset:528" ::"v"(pd), "v"(o1) : "memory");
+        asm volatile("ds_write_b128 %0, %1 offset:1056" ::"v"(pd), "v"(o2) : "memory");
+        asm volatile("ds_write_b128 %0, %1 offset:1584" ::"v"(pd), "v"(o3) : "memory");
+    };
+    float acc = 0.0f;
+    const float *pc = s_p + (lane & (kChainCols - 1)) * kChainPad;
+    auto chain = [&](int64_t t) {
+        const float *ps = pc + (int)(t & 1) * kChainCols * kChainPad;
+#pragma unroll 8
+        for (int k = 0; k < kChainRows / 4; ++k) {
+            const float4 v = *reinterpret_cast<const float4 *>(ps + 4 * k);
+            acc = acc + v.x;
+            acc = acc + v.y;
+            acc = acc + v.z;
+            acc = acc + v.w;
+        }
+    };
+    for (int64_t t = 0; t < kChainAhead; ++t) issue(t);
+    for (int64_t t = 0; t <= nslot; ++t) {
+        if (t < nslot) {  // uniform: slot t's own loads have landed (kChainAhead - 1 later slots still in flight)
+            if (wv == 1 || wv == 2)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (kChainAhead - 1)) : "memory");
+            else if (wv == 3)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kChainAhead - 1) : "memory");
+        }
+        // slot t staged for every helper; s_p[t & 1] no longer read by the chain
+        lds_barrier();
+        if (wv == 0) {
+            if (t > 0) chain(t - 1);
+        } else if (t < nslot) {
+            transform(t);
+            issue(t + kChainAhead);  // into the ring slot transformed in the previous iteration
+        }
+    }
+    if (wv != 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives its wave
+        return;
+    }
+    const int64_t j = c0 + lane;
+    if (lane >= kChainCols || j >= dd.D) return;
+    const float wj = w[j];
+    const float cw = C * wj;
+    const float l2 = cw / Bf;
+    const float g = (float)((double)acc / Bd + (double)l2);
+    if (FUSED) {
+        const float step = lr * g;
+        w[j] = wj - step;
+    } else {
+        gout[j] = g;
+    }
+}
+
 // K6b, blocked: workgroup (k, c) sums batch rows [k*R, (k+1)*R) of columns
 // [c*1024, (c+1)*1024) -- per column sequential in row order, 4 columns per
 // lane (16-byte loads along the row: every row read once, coalesced) --
@@ -1735,15 +1947,10 @@ __global__ __launch_bounds__(256) void k_dense_grad_blocked(DevDense dd, int64_t
 // register, where LDS-DMA pieces make it drain every load before each LDS
 // read).  k_dense_combine then adds the chunk partials and applies the
 // update.  Instantiated for D = 512, 1,024, 2,048 and 4,096 (BASELINE C4).
-typedef float v4f __attribute__((ext_vector_type(4)));  // staging registers (SROA-friendly)
+// (v4f: the staging registers, SROA-friendly)
 constexpr int kFuseRows = 4;       // rows per sub-chunk: one margin wave each
 constexpr int kFuseThreads = 512;  // 4 margin + 4 gradient waves
 
-__device__ __forceinline__ void lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
 
 template <int DQ>  // D / 4
 __global__ __launch_bounds__(kFuseThreads) void k_dense_fused(DevDense dd, int64_t first, int64_t B,
@@ -2460,6 +2667,16 @@ hipError_t launch_dense_grad(const DevDense &dd, int64_t first, int64_t B, const
     if (B <= 0) return hipSuccess;
     const float Bf = (float)B;
     const double Bd = (double)B;
+    if (!blocked && dd.D % 4 == 0) {
+        const unsigned grid = (unsigned)((dd.D + kChainCols - 1) / kChainCols);
+        if (fused)
+            hipLaunchKernelGGL(k_dense_grad_chain<true>, dim3(grid), dim3(256), kChainLds, s, dd, first, B, resid, w,
+                               gout, Bf, Bd, lr, C);
+        else
+            hipLaunchKernelGGL(k_dense_grad_chain<false>, dim3(grid), dim3(256), kChainLds, s, dd, first, B, resid, w,
+                               gout, Bf, Bd, lr, C);
+        return hipGetLastError();
+    }
     if (!blocked) {
         if (fused)
             hipLaunchKernelGGL(k_dense_grad_seq<true>, dim3(grid_for(dd.D, 256)), dim3(256), 0, s, dd, first, B, resid,
