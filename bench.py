@@ -82,6 +82,14 @@ CONFIGS = {
 # this process touches the GPU.
 CONFIGS["c1e2e"] = dict(rows=8140, features=123, nnz=14, batch=-1, value_mode=0, steps=100, warmup=1,
                         label="C1 local.sh job end to end (bin/distlr)", kind="e2e")
+# The reference summation orders at C3 / C4 scale: the
+# same workloads with every column of the gradient summed as ONE chain in
+# batch-row order and every margin as one chain in column order (lr.cc:35-40,
+# 108-112) -- bitwise the oracle -- instead of the deterministic reordered
+# sums the defaults use for ~10^5-10^6-add chains.
+CONFIGS["c3x"] = dict(CONFIGS["c3"], label="C3 Criteo-shaped hashed LR, reference summation order",
+                      env={"DLR_LONG_COLUMN": "0"})
+CONFIGS["c4x"] = dict(CONFIGS["c4"], label="C4 dense LR, reference summation order", env={"DLR_DENSE_GRAD": "seq"})
 PCIE_PEAK_GBS = 63.0  # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s (spec)
 
 
@@ -129,6 +137,7 @@ def parse_args():
     args.label = cfg["label"]
     args.kind = cfg.get("kind", "uniform")
     args.residency = cfg.get("residency", "auto")
+    args.env = cfg.get("env", {})
     return args
 
 
@@ -380,6 +389,7 @@ def run_rank(args):
         if distributed:
             dist.destroy_process_group()
         return
+    os.environ.update(args.env)  # the engine reads its order switches at load
     D, B = args.features, args.batch
     mode = {"mean": dlr.MODE_SYNC_MEAN, "last": dlr.MODE_SYNC_LAST, "async": dlr.MODE_ASYNC}[args.mode]
 
@@ -409,6 +419,21 @@ def run_rank(args):
     layout = "dense" if args.kind == "dense" else \
         {dlr.LAYOUT_CLASSIC: "classic", dlr.LAYOUT_LDS: "lds", dlr.LAYOUT_TOUCHED: "touched"}[eng.train_layout()]
     band_rows = eng.train_band_rows() if args.kind != "dense" else 0
+    # which summation order the numbers below are for
+    if args.kind == "dense":
+        dg = os.environ.get("DLR_DENSE_GRAD", "")
+        big = B * D > (1 << 24)
+        fused = dg == "fused" or (not dg and big and D in (512, 1024, 2048, 4096))
+        blocked = fused or dg == "blocked" or (not dg and big)
+        order = ("blocked (deterministic, within tolerance): margins as 64 lane partials + butterfly, gradient per "
+                 "256-row chunk + chunk order (DESIGN.md 3.3)" if fused else
+                 "blocked gradient (deterministic, within tolerance; DESIGN.md 3.2)" if blocked else
+                 "reference: one chain per row (margin) and per column (gradient), lr.cc:35-40/108-112 -- bitwise")
+    elif band_rows and os.environ.get("DLR_LONG_COLUMN", "1") != "0":
+        order = ("reference, except long columns (> 4,096 entries): 16,384-row phase pieces combined by a fixed "
+                 "tree (deterministic, within tolerance; DESIGN.md 3.1)")
+    else:
+        order = "reference: one chain per row (margin) and per column (gradient), lr.cc:35-40/108-112 -- bitwise"
     margin_kind = "dense rows" if args.kind == "dense" else \
         ["gathers", "product margin (pass 1 separate)",
          "product margin (pass 1 fused into the previous step's gradient)"][eng.train_product_margin()]
@@ -509,6 +534,9 @@ def run_rank(args):
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
+        "traffic_source": (f"stored figure, not measured in this run: {os.path.relpath(args.traffic_json, ROOT)} "
+                           "(rocprofv3 --pmc passes of this workload, tools/pmc_pass.sh + tools/pmc_traffic.py)")
+                          if traffic is not None else None,
         "alg_bytes_per_step": step_bytes,
         "kernel_avg_us": {k: round(v, 3) for k, v in stage_us.items()},
         "step_breakdown_us": {k: round(v, 3) for k, v in avg_us.items()},
@@ -565,6 +593,7 @@ def run_rank(args):
                        "name": args.config, "gradient_layout": layout + (f"+bands({band_rows} rows)" if band_rows else ""),
                        "values": "unit (all 1.0f, not stored)" if unit else "fp32",
                        "margin": margin_kind,
+                       "summation_order": order,
                        "rows_per_gpu": args.rows, "num_feature_dim": D, "nnz_per_row": args.nnz,
                        "batch_size": B, "parallelism": f"dp{world}"},
             "roofline": roofline,

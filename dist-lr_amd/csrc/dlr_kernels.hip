@@ -1060,7 +1060,9 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
             // (a wave-uniform exit: the sum stops at the wave's largest count,
             // ~5 at C2's 1.6 entries per column and phase); the rare longer
             // runs continue in a general loop.  Per product: compare, add,
-            // select -- this loop is what bounds the kernel (VALU issue).
+            // select.  Not the bound: the SQ counters put VALU issue at <= ~20%
+            // busy (profiles/r02f_c2_sq_counters.txt); the kernel is bound by
+            // its chain of dependent memory phases (tools/c2_stamps.py).
             const unsigned o = off[gi][p], c = cnt[gi][p];
             const uint32_t sp = s_p_a + 4u * o;
             float a = acc[gi];

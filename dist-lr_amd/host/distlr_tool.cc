@@ -6,6 +6,8 @@
 //   distlr_tool parse <libsvm-file> <D>
 //   distlr_tool batches <libsvm-file> <D> <B>
 //   distlr_tool debuginfo <libsvm-file> <D>   (Sample::DebugInfo per sample)
+//   distlr_tool lrdebug <D> [random_state]      (LR::DebugInfo of a new LR: its
+//                                               initial weights, lr.cc:84-90)
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -15,6 +17,7 @@
 #include <vector>
 
 #include "distlr/data_iter.h"
+#include "distlr/lr.h"
 #include "distlr/sample.h"
 #include "distlr/util.h"
 
@@ -52,6 +55,11 @@ int main(int argc, char **argv) {
                 }
                 std::printf("\n");
             }
+            return 0;
+        }
+        if (mode == "lrdebug") {  // host only: no KVWorker, no GPU
+            distlr::LR lr(std::atoi(argv[2]), 0.001f, 1.0f, argc > 3 ? std::atoi(argv[3]) : 0);
+            std::printf("%s", lr.DebugInfo().c_str());
             return 0;
         }
         if (argc < 4) return 2;

@@ -84,3 +84,13 @@ def test_dataiter_binary_cache(tmp_path):
     # a cache for another D is ignored (and replaced)
     assert subprocess.run([TOOL, "parse", q, "12"], check=True, capture_output=True,
                           env=env).stdout.decode("latin-1") == tool("parse", q, 12)
+
+
+def test_lr_debuginfo_format():
+    # lr.cc:84-90: every weight of weight_ through ostream's default float
+    # formatting (%g, precision 6), each followed by one space; a new LR's
+    # weight_ is InitWeight_'s (lr.cc:92-98: srand(random_state), rand())
+    import oracle
+    for D, rs in ((123, 0), (7, 3), (1, 0)):
+        w = oracle.init_weight(D, rs)
+        assert tool("lrdebug", D, rs) == "".join(oracle.format_g(x) + " " for x in w), (D, rs)
