@@ -981,7 +981,11 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
                 vq[gi][p] = make_float4(0.f, 0.f, 0.f, 0.f);
                 continue;
             }
-            const unsigned e = bs[gi][p] + lane * 4;  // entries are padded: always in bounds
+            // lanes past the block re-read its last 4 entries: the wave's
+            // addresses then span the block only (the next blocks' lines are
+            // not pulled into this CU), and a duplicate address costs nothing
+            const unsigned nb4 = nblk[gi][p];
+            const unsigned e = bs[gi][p] + min((unsigned)lane * 4, nb4 ? nb4 - 4 : 0u);  // padded: in bounds
             if (NTW) {
                 rq[gi][p] = load_stream(reinterpret_cast<const ushort4 *>(pc.row + e));
                 vq[gi][p] = load_stream(reinterpret_cast<const float4 *>(pc.val + e));
@@ -1834,18 +1838,50 @@ __global__ __launch_bounds__(256) void k_dense_grad_chain(DevDense dd, int64_t f
         asm volatile("ds_write_b128 %0, %1 offset:1584" ::"v"(pd), "v"(o3) : "memory");
     };
     float acc = 0.0f;
-    const float *pc = s_p + (lane & (kChainCols - 1)) * kChainPad;
-    auto chain = [&](int64_t t) {
-        const float *ps = pc + (int)(t & 1) * kChainCols * kChainPad;
-#pragma unroll 8
-        for (int k = 0; k < kChainRows / 4; ++k) {
-            const float4 v = *reinterpret_cast<const float4 *>(ps + 4 * k);
-            acc = acc + v.x;
-            acc = acc + v.y;
-            acc = acc + v.z;
-            acc = acc + v.w;
+    // chain: the slot's 128 rows as 4 blocks of 8 16-byte reads (asm: the
+    // compiler kept only one read in flight), block b+1 in flight while
+    // block b is added
+    const uint32_t pc = lds_addr(s_p + (lane & (kChainCols - 1)) * kChainPad);
+    static_assert(kChainRows == 128, "4 blocks of 32 rows below");
+    auto rd8 = [&](v4f (&d)[8], uint32_t a) {
+        asm volatile("ds_read_b128 %0, %1" : "=v"(d[0]) : "v"(a));
+        asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(d[1]) : "v"(a));
+        asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(d[2]) : "v"(a));
+        asm volatile("ds_read_b128 %0, %1 offset:48" : "=v"(d[3]) : "v"(a));
+        asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(d[4]) : "v"(a));
+        asm volatile("ds_read_b128 %0, %1 offset:80" : "=v"(d[5]) : "v"(a));
+        asm volatile("ds_read_b128 %0, %1 offset:96" : "=v"(d[6]) : "v"(a));
+        asm volatile("ds_read_b128 %0, %1 offset:112" : "=v"(d[7]) : "v"(a));
+    };
+    auto add8 = [&](const v4f (&d)[8]) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            acc = acc + d[u].x;
+            acc = acc + d[u].y;
+            acc = acc + d[u].z;
+            acc = acc + d[u].w;
         }
     };
+#define DLR_CHAIN_WAIT(N, d)                                                                                   \
+    asm volatile("s_waitcnt lgkmcnt(" #N ")"                                                                  \
+                 : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]), "+v"(d[6]), "+v"(d[7]))
+    auto chain = [&](int64_t t) {
+        const uint32_t ps = pc + (uint32_t)((t & 1) * kChainCols * kChainPad * 4);
+        v4f a[8], b[8];
+        rd8(a, ps);
+        rd8(b, ps + 128);
+        DLR_CHAIN_WAIT(8, a);
+        add8(a);
+        rd8(a, ps + 256);
+        DLR_CHAIN_WAIT(8, b);
+        add8(b);
+        rd8(b, ps + 384);
+        DLR_CHAIN_WAIT(8, a);
+        add8(a);
+        DLR_CHAIN_WAIT(0, b);
+        add8(b);
+    };
+#undef DLR_CHAIN_WAIT
     for (int64_t t = 0; t < kChainAhead; ++t) issue(t);
     for (int64_t t = 0; t <= nslot; ++t) {
         if (t < nslot) {  // uniform: slot t's own loads have landed (kChainAhead - 1 later slots still in flight)
