@@ -494,12 +494,29 @@ def run_rank(args):
         digests = [None] * world
         dist.all_gather_object(digests, digest)
     nranks, transport = eng.comm_info()
+    # N > 1 with the product margin: the same K steps once more with the
+    # exchange NOT overlapped with the next batch's pass 1 (plain all-gather,
+    # pass 1 in the next margin), so the line shows what the overlap buys
+    overlap = eng.exchange_overlap() if world > 1 else False
+    no_overlap = None
+    if overlap:
+        eng.set_exchange_overlap(False)
+        el_off = timed(args.warmup + 2 * args.steps, False)
+        eng.timing(True)
+        timed(args.warmup + 3 * args.steps, True)
+        ex_off = eng.kernel_time(dlr.TIMER_EXCHANGE)
+        mg_off = eng.kernel_time(dlr.TIMER_MARGIN)
+        eng.timing(False)
+        eng.set_exchange_overlap(True)
+        no_overlap = {"ms_per_step": round(el_off / args.steps * 1000.0, 5),
+                      "exchange_us_per_step": round(ex_off[0] / max(1, ex_off[1]) * 1000.0, 3),
+                      "margin_us_per_step": round(mg_off[0] / max(1, mg_off[1]) * 1000.0, 3)}
     # Pass 3 (the roofline): each kernel stage over K consecutive batches
     # between ONE event pair (no per-launch event overhead, comparable with
     # rocprofv3's kernel durations).  Runs after the measured passes: the
     # stages run without their partners and change the weights.
     # (A streamed shard is bound by the batch copies instead: no stage pass.)
-    k0 = args.warmup + 2 * args.steps
+    k0 = args.warmup + (4 if overlap else 2) * args.steps
     stage_us = {}
     if not streamed:
         stage_us = {"margin": eng.stage_time(dlr.STAGE_MARGIN, k0 % nb, args.steps, args.lr) * 1000.0,
@@ -605,6 +622,10 @@ def run_rank(args):
                             ("torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else
                              ("external" if distributed else "single process")),
                 "us_per_step": round(avg_us["exchange"], 3),
+                "overlap": ("the all-gather in 4 pieces, the next batch's pass 1 formed slice group by slice group "
+                            "as its weights land (us_per_step includes that pass 1; the margin then runs pass 2 only)"
+                            if overlap else None),
+                "without_overlap": no_overlap,
                 "merge_us_per_step": round(avg_us["merge"], 3) if world > 1 else 0.0,
                 "protocol": ("touched-list all-gather + rank-ordered merge" if layout == "touched" else
                              "key-range all-to-all + rank-ordered merge + in-place all-gather") if world > 1 else

@@ -55,6 +55,22 @@ public:
         if (aborted_) return nccl_ok(ncclInvalidUsage, "aborted communicator", err);
         return nccl_ok(ncclAllToAll(send, recv, words, ncclUint32, comm_, s), "ncclAllToAll", err);
     }
+    bool all_gather_part(void *buf, size_t chunk, size_t off, size_t count, hipStream_t s,
+                         std::string &err) override {
+        if (aborted_) return nccl_ok(ncclInvalidUsage, "aborted communicator", err);
+        if (world_ == 1 || count == 0) return true;
+        // point to point: the piece of every peer's block, strided by chunk
+        uint32_t *b = static_cast<uint32_t *>(buf);
+        if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
+        bool ok = true;
+        for (int q = 0; q < world_ && ok; ++q) {
+            if (q == rank_) continue;
+            ok = nccl_ok(ncclSend(b + (size_t)rank_ * chunk + off, count, ncclUint32, q, comm_, s), "ncclSend", err) &&
+                 nccl_ok(ncclRecv(b + (size_t)q * chunk + off, count, ncclUint32, q, comm_, s), "ncclRecv", err);
+        }
+        const bool ended = nccl_ok(ncclGroupEnd(), "ncclGroupEnd", err);
+        return ok && ended;
+    }
     int count() const {
         int n = 0;
         return ncclCommCount(comm_, &n) == ncclSuccess ? n : -1;
@@ -196,6 +212,20 @@ public:
             if (dst == g_->send[(size_t)q] || bytes == 0) continue;  // in place
             ok = hip_ok(hipMemcpyAsync(dst, g_->send[(size_t)q], bytes, hipMemcpyDeviceToDevice, s),
                         "loopback all_gather", err);
+        }
+        return finish(ok, s, err);
+    }
+
+    bool all_gather_part(void *buf, size_t chunk, size_t off, size_t count, hipStream_t s,
+                         std::string &err) override {
+        if (!publish(buf, buf, s, err)) return false;
+        bool ok = true;
+        for (int q = 0; q < g_->W && ok && count; ++q) {
+            if (q == rank_) continue;
+            const size_t at = ((size_t)q * chunk + off) * 4;
+            ok = hip_ok(hipMemcpyAsync(static_cast<char *>(buf) + at, static_cast<const char *>(g_->send[(size_t)q]) + at,
+                                       count * 4, hipMemcpyDeviceToDevice, s),
+                        "loopback all_gather_part", err);
         }
         return finish(ok, s, err);
     }

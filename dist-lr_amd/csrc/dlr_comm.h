@@ -40,6 +40,13 @@ public:
     virtual bool all_gather(const void *send, void *recv, size_t words, hipStream_t s, std::string &err) = 0;
     // recv[q * words ..] = rank q's send[rank * words ..).
     virtual bool all_to_all(const void *send, void *recv, size_t words, hipStream_t s, std::string &err) = 0;
+    // One piece of an in-place all-gather whose rank blocks are `chunk`
+    // words apart: buf[q * chunk + off, + count) = rank q's same words, for
+    // every rank q (the caller's own block is already in place).  Pieces of
+    // one gather may be issued one after another so that work on the pieces
+    // that have landed overlaps the rest (the exchange / next-margin overlap).
+    virtual bool all_gather_part(void *buf, size_t chunk, size_t off, size_t count, hipStream_t s,
+                                 std::string &err) = 0;
     // A rank that will not reach its next collective (it failed) releases
     // its peers: their pending and later collectives fail with `why`
     // instead of waiting (loopback), or the communicator is aborted (RCCL).

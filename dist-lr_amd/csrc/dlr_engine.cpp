@@ -28,6 +28,7 @@
 namespace {
 
 constexpr int kTimers = 5;  // 0 margin, 1 gradient, 2 update, 3 exchange, 4 step
+constexpr int kXPieces = 4;  // pieces of the overlapped all-gather (exchange_overlapped)
 constexpr int64_t kPad = 64;  // padding entries after col/val (16-B tail loads)
 
 struct DeviceBuf {
@@ -102,6 +103,16 @@ struct TrainShard {
     float *pm_val = nullptr, *pm_p = nullptr;
     uint16_t *pm_qs = nullptr;
     std::vector<int64_t> pmo_list, pmo_pofs, pmo_rg, pmo_qs;
+    // world > 1: the exchange / next-margin overlap (dlr_train_step).  The
+    // in-place all-gather of the updated weights runs in kXPieces pieces on
+    // the exchange stream; after piece k the next batch's pass 1 forms the
+    // slices whose weights have all landed.  xslices: slice ids grouped by
+    // the piece that completes them (group 0: inside this rank's own key
+    // range, ready after the merge; group k + 1: after piece k), group g at
+    // [xgofs[g], xgofs[g + 1]).
+    uint32_t *xslices = nullptr;
+    std::vector<int64_t> xgofs;
+    int64_t xsub = 0;  // words per piece of a rank's key range
     // touched-column layout (huge D, small batches): per batch the touched
     // columns tcols[tcoff[b] .. +tncols[b]), segment pointers in cptr at
     // tpoff[b] (tncols[b]+1 entries), entries at coff[b] in crow/cval
@@ -213,6 +224,12 @@ struct dlr_ctx {
     double *h_ll = nullptr;                   // pinned
     TrainShard train;
     TestShard test;
+    // exchange / next-margin overlap (TrainShard::xslices): on unless
+    // dlr_set_exchange_overlap(0); its stream and events
+    bool xoverlap = true;
+    hipStream_t xstream = nullptr;
+    hipEvent_t ev_xmerged = nullptr;
+    hipEvent_t ev_xpiece[kXPieces] = {};
     // product margin: the batch whose products pm_p holds, formed from the
     // CURRENT weights by the last step's fused gradient (-1: none; every
     // entry point that changes w or the shard resets it)
@@ -342,7 +359,7 @@ void free_train(dlr_ctx *c) {
                     (void *)t.bws, t.brow, (void *)t.bval, (void *)t.gacc, (void *)t.lpdesc, (void *)t.lpptr,
                     (void *)t.lpslot, (void *)t.lpws, (void *)t.lprow, (void *)t.lpval, (void *)t.pm_lbeg,
                     (void *)t.pm_list, (void *)t.pm_pofs, (void *)t.pm_rg, (void *)t.pm_qoff, (void *)t.pm_val,
-                    (void *)t.pm_p, (void *)t.pm_qs})
+                    (void *)t.pm_p, (void *)t.pm_qs, (void *)t.xslices})
         dev_free(c, p);
     t = TrainShard();
     c->pm_ready = -1;
@@ -1720,6 +1737,7 @@ void dlr_destroy(dlr_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->cstream) (void)hipStreamSynchronize(ctx->cstream);
     if (ctx->gstream) (void)hipStreamSynchronize(ctx->gstream);
+    if (ctx->xstream) (void)hipStreamSynchronize(ctx->xstream);
     free_train(ctx);  // unregisters a streamed shard's host rows
     delete ctx->comm;  // RCCL: ncclCommDestroy; loopback: drops the group reference
     for (void *p : ctx->allocs) (void)hipFree(p);
@@ -1734,6 +1752,10 @@ void dlr_destroy(dlr_ctx *ctx) {
     if (ctx->ev_bstart) (void)hipEventDestroy(ctx->ev_bstart);
     if (ctx->ev_bdone) (void)hipEventDestroy(ctx->ev_bdone);
     if (ctx->gstream) (void)hipStreamDestroy(ctx->gstream);
+    if (ctx->ev_xmerged) (void)hipEventDestroy(ctx->ev_xmerged);
+    for (hipEvent_t e : ctx->ev_xpiece)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->xstream) (void)hipStreamDestroy(ctx->xstream);
     if (ctx->cstream) (void)hipStreamDestroy(ctx->cstream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -1766,6 +1788,66 @@ int dlr_get_weights(dlr_ctx *c, float *w, int64_t D) {
     HIPC(c, hipMemcpyAsync(tmp.data(), c->w, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     for (int64_t j = 0; j < D; ++j) w[j] = tmp[(size_t)c->perm[(size_t)j]];
+    return DLR_OK;
+}
+
+// TrainShard::xslices for this rank: slice s (columns [4096 s, 4096 s +
+// 4096) of the padded key space) is complete once every key range it
+// overlaps has delivered its part -- this rank's own part at once, rank q's
+// part [q chunk, q chunk + o] with piece o / xsub.
+int build_overlap_groups(dlr_ctx *c) {
+    TrainShard &t = c->train;
+    const int64_t S = t.pmS, chunk = c->chunk, W = c->world;
+    t.xsub = (chunk + kXPieces - 1) / kXPieces;
+    std::vector<std::vector<uint32_t>> g((size_t)kXPieces + 1);
+    for (int64_t s = 0; s < S; ++s) {
+        const int64_t a = s * dlr::kPmSlice, b = std::min((s + 1) * dlr::kPmSlice, c->D);
+        int grp = 0;
+        for (int64_t q = a / chunk; q < W && q * chunk < b; ++q) {
+            if (q == c->rank) continue;
+            const int64_t last = std::min(b, (q + 1) * chunk) - 1 - q * chunk;  // last word of q's part
+            grp = std::max(grp, (int)(last / t.xsub) + 1);
+        }
+        g[(size_t)grp].push_back((uint32_t)s);
+    }
+    std::vector<uint32_t> all;
+    t.xgofs.assign(1, 0);
+    for (auto &v : g) {
+        all.insert(all.end(), v.begin(), v.end());
+        t.xgofs.push_back((int64_t)all.size());
+    }
+    return upload(c, &t.xslices, all.data(), all.size());
+}
+
+// world > 1, product margin: the all-gather of the merged weights in pieces
+// on the exchange stream, the next batch's pass 1 slice group by slice group
+// on the engine stream as their weights land (the exchange
+// overlapped with the next batch's margin).  Ends with the engine stream
+// past every piece.
+int exchange_overlapped(dlr_ctx *c, int64_t b) {
+    TrainShard &t = c->train;
+    if (!c->xstream) {
+        HIPC(c, hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
+        HIPC(c, hipEventCreateWithFlags(&c->ev_xmerged, hipEventDisableTiming));
+        for (hipEvent_t &e : c->ev_xpiece) HIPC(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    const int64_t nx = (b + 1) % (int64_t)t.plan.size();
+    const dlr::DevPm pm = pm_view(c, nx);
+    HIPC(c, hipEventRecord(c->ev_xmerged, c->stream));
+    HIPC(c, hipStreamWaitEvent(c->xstream, c->ev_xmerged, 0));
+    auto pass1 = [&](int grp) -> hipError_t {
+        const int64_t n = t.xgofs[(size_t)grp + 1] - t.xgofs[(size_t)grp];
+        return dlr::launch_pm_products(pm, c->w, c->D, t.pm_p, c->stream, t.xslices + t.xgofs[(size_t)grp], n);
+    };
+    HIPC(c, pass1(0));  // inside this rank's own key range: ready now
+    for (int k = 0; k < kXPieces; ++k) {
+        const int64_t off = k * t.xsub, cnt = std::max<int64_t>(0, std::min(t.xsub, c->chunk - off));
+        COMMC(c, all_gather_part(c->w, (size_t)c->chunk, (size_t)off, (size_t)cnt, c->xstream, e_));
+        HIPC(c, hipEventRecord(c->ev_xpiece[k], c->xstream));
+        HIPC(c, hipStreamWaitEvent(c->stream, c->ev_xpiece[k], 0));
+        HIPC(c, pass1(k + 1));
+    }
+    c->pm_ready = nx;
     return DLR_OK;
 }
 
@@ -2088,6 +2170,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 t.pm = true;
                 const char *pf = getenv("DLR_PM_FUSED");
                 t.pm_fused = !c->comm && !(pf && strcmp(pf, "0") == 0);
+                if (c->comm && (rc = build_overlap_groups(c))) return rc;
             } else if (pme && strcmp(pme, "1") == 0) {
                 return fail(c, DLR_E_ARG, "dlr_load_train: DLR_PM=1 but the batches do not fit the product margin");
             }
@@ -2606,7 +2689,13 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
         HIPC(c, dlr::launch_merge_update(c->recv, c->world, c->chunk, ke - kb, c->w + kb, lr, mode, c->stream));
         time_end(c, 2, t0);
         time_begin(c, &t0);
-        COMMC(c, all_gather(c->w + (int64_t)c->rank * c->chunk, c->w, (size_t)c->chunk, c->stream, e_));
+        if (c->train.pm && c->xoverlap && !c->train.sparse_stream) {
+            // (the exchange interval then includes the next batch's pass 1)
+            int rc = exchange_overlapped(c, b);
+            if (rc) return rc;
+        } else {
+            COMMC(c, all_gather(c->w + (int64_t)c->rank * c->chunk, c->w, (size_t)c->chunk, c->stream, e_));
+        }
         time_end(c, 3, t0);
     }
     if (c->train.sparse_stream) HIPC(c, sparse_batch_done(c, b));
@@ -2834,6 +2923,20 @@ int dlr_train_layout(dlr_ctx *c) {
     if (!c) return DLR_E_ARG;
     if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_layout: no training shard loaded");
     return c->train.touched ? DLR_LAYOUT_TOUCHED : c->train.pcsc ? DLR_LAYOUT_LDS : DLR_LAYOUT_CLASSIC;
+}
+
+int dlr_set_exchange_overlap(dlr_ctx *c, int on) {
+    if (!c) return DLR_E_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->xoverlap = on != 0;
+    c->pm_ready = -1;  // products formed under the other setting are not assumed
+    return DLR_OK;
+}
+
+int dlr_exchange_overlap(dlr_ctx *c) {
+    if (!c) return DLR_E_ARG;
+    return c->comm && c->train.loaded && c->train.pm && c->xoverlap && !c->train.sparse_stream ? 1 : 0;
 }
 
 int dlr_memory_info(dlr_ctx *c, int64_t *train_bytes, int64_t *test_bytes) {

@@ -198,7 +198,9 @@ hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float 
                            float lr, float C, bool fused, hipStream_t s);
 // Product margin: pass 1 (the products of pm's batch from w), pass 2 (the
 // margins, sigmoid and residuals of bt's rows from those products).
-hipError_t launch_pm_products(const DevPm &pm, const float *w, int64_t D, float *p, hipStream_t s);
+// slices (optional): form only these nslices slices (device array).
+hipError_t launch_pm_products(const DevPm &pm, const float *w, int64_t D, float *p, hipStream_t s,
+                              const uint32_t *slices = nullptr, int64_t nslices = 0);
 hipError_t launch_pm_margin(const DevPm &pm, const DevBatch &bt, const float *p, float *resid, hipStream_t s);
 // k_grad_lds (fused update) that also forms the products of the NEXT batch
 // (next: its product-margin view) from the weights it has just updated:

@@ -848,13 +848,17 @@ struct PmPass1 {
 // slice's XCD (workgroup x runs on XCD x % 8): slice s = (x/8/SPLIT)*8 + x%8,
 // so each XCD's L2 serves its 1/8 of w and the region chunks it writes are
 // adjacent (a region's chunks are ordered by XCD).
+// sl (optional): the slices to form, nsl of them (the exchange overlap forms
+// the slices whose weights have landed, group by group).
 __global__ __launch_bounds__(1024) void k_pm_products(DevPm pm, const float *__restrict__ w, int64_t D,
-                                                      float *__restrict__ p) {
+                                                      float *__restrict__ p, const uint32_t *__restrict__ sl,
+                                                      int64_t nsl) {
     __shared__ __attribute__((aligned(16))) float s_w[kPmSlice];
     __shared__ uint32_t s_po[kPmMaxBlocks];
     const int x = blockIdx.x, xcd = x & 7, k = x >> 3;
-    const int s = (k / pm.split) * 8 + xcd, part = k % pm.split;
-    if (s >= pm.S) return;  // whole workgroup
+    const int i = (k / pm.split) * 8 + xcd, part = k % pm.split;
+    if (i >= (sl ? nsl : pm.S)) return;  // whole workgroup
+    const int s = sl ? (int)sl[i] : i;
     PmPass1<1024, 4> pp;
     const int64_t j = (int64_t)s * kPmSlice + 4 * threadIdx.x;  // one float4 per thread
     const float4 wv = j + 3 < D ? *reinterpret_cast<const float4 *>(w + j)
@@ -1746,24 +1750,35 @@ __global__ __launch_bounds__(256) void k_dense_grad_seq(DevDense dd, int64_t fir
 // halves of a 128-byte row line) run on one XCD (blockIdx % 8) when the grid
 // is a multiple of 16, so the line is fetched into one L2 once.
 constexpr int kChainCols = 16;
-constexpr int kChainRows = 128;
-constexpr int kChainRing = 8;   // staging slots
-constexpr int kChainAhead = 7;  // slots in flight (<= kChainRing - 1)
-constexpr int kChainPad = 132;  // s_p column stride (floats)
-constexpr int kChainXInstr = kChainRows * kChainCols * 4 / 1024;  // 1 KiB LDS-DMA instructions per slot (x)
-static_assert(kChainXInstr == 8, "waves 1 and 2 issue 4 each");
-constexpr size_t kChainLds =
-    ((size_t)kChainRing * (kChainRows * kChainCols + 256) + 2 * kChainCols * kChainPad) * 4;
+template <int R>
+struct ChainCfg {
+    static constexpr int kRing = R == 128 ? 8 : 6;        // staging slots
+    static constexpr int kAhead = kRing - 1;               // slots in flight
+    static constexpr int kPad = R + 4;                     // s_p column stride (floats): conflict-free 16-B reads
+    static constexpr int kXI = R * kChainCols * 4 / 1024;  // 1 KiB LDS-DMA instructions per slot (x)
+    // wave h (1..3) issues x blocks h-1, h+2, ... and wave 3 also the residuals
+    static constexpr int count(int h) { return (kXI - (h - 1) + 2) / 3 + (h == 3 ? 1 : 0); }
+    static constexpr size_t kLds = ((size_t)kRing * (R * kChainCols + 256) + 2 * kChainCols * kPad) * 4;
+};
+int dense_chain_rows() {
+    static const int r = [] {
+        const char *e = getenv("DLR_CHAIN_ROWS");  // A/B: batch rows per staging slot
+        return e && atoi(e) == 128 ? 128 : 256;
+    }();
+    return r;
+}
 
-template <bool FUSED>
+template <bool FUSED, int R>
 __global__ __launch_bounds__(256) void k_dense_grad_chain(DevDense dd, int64_t first, int64_t B,
                                                           const float *__restrict__ resid, float *__restrict__ w,
                                                           float *__restrict__ gout, float Bf, double Bd, float lr,
                                                           float C) {
+    using Cfg = ChainCfg<R>;
+    constexpr int NS = Cfg::kRing, A = Cfg::kAhead, PAD = Cfg::kPad;
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    float *s_x = smem;                                               // ring x [row][col]
-    float *s_r = s_x + kChainRing * kChainRows * kChainCols;         // ring r (256 per slot; 128 used)
-    float *s_p = s_r + kChainRing * 256;                             // 2 x [col][kChainPad]
+    float *s_x = smem;                                    // ring x [row][col]
+    float *s_r = s_x + NS * R * kChainCols;               // ring r (256 per slot)
+    float *s_p = s_r + NS * 256;                          // 2 x [col][PAD]
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     unsigned cg = blockIdx.x;
@@ -1772,77 +1787,81 @@ __global__ __launch_bounds__(256) void k_dense_grad_chain(DevDense dd, int64_t f
         cg = ((k >> 1) << 4) | ((blockIdx.x & 7) << 1) | (k & 1);
     }
     const int64_t c0 = (int64_t)cg * kChainCols;
-    const int64_t nslot = (B + kChainRows - 1) / kChainRows;
+    const int64_t nslot = (B + R - 1) / R;
+    const int64_t col = min(c0 + 4 * (lane & 3), dd.D - 4);
     // LDS-DMA of slot t (clamped past the last slot: the wait counts stay fixed)
     auto issue = [&](int64_t t) {
         const int64_t ts = t < nslot ? t : nslot - 1;
-        const int ring = (int)(t % kChainRing);
-        if (wv == 1 || wv == 2) {
-            const int64_t col = min(c0 + 4 * (lane & 3), dd.D - 4);
+        const int ring = (int)(t % NS);
+        if (wv >= 1) {
+            const int64_t r0 = wrap_row(first + ts * R, dd.N);  // uniform; rows past it wrap at most once when N >= R
 #pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const int blk = (wv - 1) * 4 + m;  // 16 rows per instruction
-                const int64_t i = min(ts * kChainRows + blk * 16 + (lane >> 2), B - 1);
-                const float *src = dd.X + wrap_row(first + i, dd.N) * dd.D + col;
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                                 (__attribute__((address_space(3))) void *)(s_x + (ring * kChainRows + blk * 16) * kChainCols),
+            for (int blk = wv - 1; blk < Cfg::kXI; blk += 3) {  // 16 rows per instruction
+                const int64_t i = min(ts * R + blk * 16 + (lane >> 2), B - 1) - ts * R;
+                int64_t row = r0 + i;
+                if (dd.N >= R) {
+                    if (row >= dd.N) row -= dd.N;
+                } else {
+                    row = wrap_row(row, dd.N);
+                }
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(dd.X + row * dd.D + col),
+                                                 (__attribute__((address_space(3))) void *)(s_x + (ring * R + blk * 16) * kChainCols),
                                                  16, 0, 0);
             }
-        } else if (wv == 3) {
+        }
+        if (wv == 3) {
             // resid is allocated to a multiple of 4 floats (+4): quads in bounds
-            const int64_t q = min(ts * kChainRows + 4 * (lane & 31), (B - 1) & ~int64_t(3));
+            const int64_t q = min(ts * R + 4 * (lane & (R / 4 - 1)), (B - 1) & ~int64_t(3));
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(resid + q),
                                              (__attribute__((address_space(3))) void *)(s_r + ring * 256), 16, 0, 0);
         }
     };
-    // helpers: the products of slot t into s_p[t & 1], transposed; 128 groups
-    // of 4 rows x 4 columns, lanes of waves 1 and 2
-    // The staged bytes are read with asm ds_read_b128: a compiler-issued LDS
-    // read that may alias an in-flight LDS-DMA gets an s_waitcnt vmcnt(0),
-    // which would drain the whole ring every slot (the explicit waits above
-    // already order these reads after their slot's DMA).
+    // helpers (waves 1, 2): the products of slot t into s_p[t & 1],
+    // transposed; R groups of 4 rows x 4 columns, R / 128 per lane.  The
+    // staged bytes are read with asm ds_read_b128 (and s_p written with asm):
+    // a compiler-issued LDS access that may alias an in-flight LDS-DMA gets
+    // an s_waitcnt vmcnt(0), which would drain the whole ring every slot (the
+    // explicit waits below order these after their slot's DMA).
     auto transform = [&](int64_t t) {
-        const int g = (wv - 1) * kWave + lane;
         if (wv < 1 || wv > 2) return;
-        const int k = g >> 2, q = g & 3;
-        const int ring = (int)(t % kChainRing);
-        const uint32_t xr = lds_addr(s_x + (ring * kChainRows + 4 * k) * kChainCols + 4 * q);
-        const uint32_t ra = lds_addr(s_r + ring * 256 + 4 * k);
-        v4f x4v[4], r4v;
-        asm volatile("ds_read_b128 %0, %1" : "=v"(r4v) : "v"(ra));
-        asm volatile("ds_read_b128 %0, %1" : "=v"(x4v[0]) : "v"(xr));
-        asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(x4v[1]) : "v"(xr));
-        asm volatile("ds_read_b128 %0, %1 offset:128" : "=v"(x4v[2]) : "v"(xr));
-        asm volatile("ds_read_b128 %0, %1 offset:192" : "=v"(x4v[3]) : "v"(xr));
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r4v), "+v"(x4v[0]), "+v"(x4v[1]), "+v"(x4v[2]), "+v"(x4v[3]));
-        static_assert(kChainCols * 4 == 64, "row stride of the staged slot");
-        const float rr[4] = {r4v.x, r4v.y, r4v.z, r4v.w};
-        float p[4][4];
+        const int ring = (int)(t % NS);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const float4 x4 = make_float4(x4v[u].x, x4v[u].y, x4v[u].z, x4v[u].w);
-            const bool ok = t * kChainRows + 4 * k + u < B;
-            p[u][0] = ok ? rr[u] * x4.x : 0.0f;
-            p[u][1] = ok ? rr[u] * x4.y : 0.0f;
-            p[u][2] = ok ? rr[u] * x4.z : 0.0f;
-            p[u][3] = ok ? rr[u] * x4.w : 0.0f;
+        for (int h = 0; h < R / 128; ++h) {
+            const int g = h * 128 + (wv - 1) * kWave + lane;
+            const int k = g >> 2, q = g & 3;
+            const uint32_t xr = lds_addr(s_x + (ring * R + 4 * k) * kChainCols + 4 * q);
+            const uint32_t ra = lds_addr(s_r + ring * 256 + 4 * k);
+            v4f x4v[4], r4v;
+            asm volatile("ds_read_b128 %0, %1" : "=v"(r4v) : "v"(ra));
+            asm volatile("ds_read_b128 %0, %1" : "=v"(x4v[0]) : "v"(xr));
+            asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(x4v[1]) : "v"(xr));
+            asm volatile("ds_read_b128 %0, %1 offset:128" : "=v"(x4v[2]) : "v"(xr));
+            asm volatile("ds_read_b128 %0, %1 offset:192" : "=v"(x4v[3]) : "v"(xr));
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r4v), "+v"(x4v[0]), "+v"(x4v[1]), "+v"(x4v[2]), "+v"(x4v[3]));
+            static_assert(kChainCols * 4 == 64, "row stride of the staged slot");
+            const float rr[4] = {r4v.x, r4v.y, r4v.z, r4v.w};
+            float p[4][4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const bool ok = t * R + 4 * k + u < B;
+                p[u][0] = ok ? rr[u] * x4v[u].x : 0.0f;
+                p[u][1] = ok ? rr[u] * x4v[u].y : 0.0f;
+                p[u][2] = ok ? rr[u] * x4v[u].z : 0.0f;
+                p[u][3] = ok ? rr[u] * x4v[u].w : 0.0f;
+            }
+            const uint32_t pd = lds_addr(s_p + (int)(t & 1) * kChainCols * PAD + 4 * q * PAD + 4 * k);
+            const v4f o0 = {p[0][0], p[1][0], p[2][0], p[3][0]}, o1 = {p[0][1], p[1][1], p[2][1], p[3][1]};
+            const v4f o2 = {p[0][2], p[1][2], p[2][2], p[3][2]}, o3 = {p[0][3], p[1][3], p[2][3], p[3][3]};
+            asm volatile("ds_write_b128 %0, %1" ::"v"(pd), "v"(o0) : "memory");
+            asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(pd), "v"(o1), "n"(PAD * 4) : "memory");
+            asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(pd), "v"(o2), "n"(PAD * 8) : "memory");
+            asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(pd), "v"(o3), "n"(PAD * 12) : "memory");
         }
-        // (asm writes too: a compiler-issued LDS write would wait for the ring)
-        const uint32_t pd = lds_addr(s_p + (int)(t & 1) * kChainCols * kChainPad + 4 * q * kChainPad + 4 * k);
-        static_assert(kChainPad * 4 == 528, "s_p column stride in the offsets below");
-        const v4f o0 = {p[0][0], p[1][0], p[2][0], p[3][0]}, o1 = {p[0][1], p[1][1], p[2][1], p[3][1]};
-        const v4f o2 = {p[0][2], p[1][2], p[2][2], p[3][2]}, o3 = {p[0][3], p[1][3], p[2][3], p[3][3]};
-        asm volatile("ds_write_b128 %0, %1" ::"v"(pd), "v"(o0) : "memory");
-        asm volatile("ds_write_b128 %0, %1 offset:528" ::"v"(pd), "v"(o1) : "memory");
-        asm volatile("ds_write_b128 %0, %1 offset:1056" ::"v"(pd), "v"(o2) : "memory");
-        asm volatile("ds_write_b128 %0, %1 offset:1584" ::"v"(pd), "v"(o3) : "memory");
     };
     float acc = 0.0f;
-    // chain: the slot's 128 rows as 4 blocks of 8 16-byte reads (asm: the
-    // compiler kept only one read in flight), block b+1 in flight while
-    // block b is added
-    const uint32_t pc = lds_addr(s_p + (lane & (kChainCols - 1)) * kChainPad);
-    static_assert(kChainRows == 128, "4 blocks of 32 rows below");
+    // chain: the slot's rows as blocks of 8 16-byte reads (asm: the compiler
+    // kept only one read in flight), block b+1 in flight while block b is added
+    const uint32_t pc = lds_addr(s_p + (lane & (kChainCols - 1)) * PAD);
     auto rd8 = [&](v4f (&d)[8], uint32_t a) {
         asm volatile("ds_read_b128 %0, %1" : "=v"(d[0]) : "v"(a));
         asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(d[1]) : "v"(a));
@@ -1866,29 +1885,33 @@ __global__ __launch_bounds__(256) void k_dense_grad_chain(DevDense dd, int64_t f
     asm volatile("s_waitcnt lgkmcnt(" #N ")"                                                                  \
                  : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]), "+v"(d[6]), "+v"(d[7]))
     auto chain = [&](int64_t t) {
-        const uint32_t ps = pc + (uint32_t)((t & 1) * kChainCols * kChainPad * 4);
+        const uint32_t ps = pc + (uint32_t)((t & 1) * kChainCols * PAD * 4);
         v4f a[8], b[8];
         rd8(a, ps);
-        rd8(b, ps + 128);
-        DLR_CHAIN_WAIT(8, a);
-        add8(a);
-        rd8(a, ps + 256);
-        DLR_CHAIN_WAIT(8, b);
-        add8(b);
-        rd8(b, ps + 384);
-        DLR_CHAIN_WAIT(8, a);
-        add8(a);
-        DLR_CHAIN_WAIT(0, b);
-        add8(b);
+#pragma unroll
+        for (int blk = 0; blk < R / 32; blk += 2) {
+            rd8(b, ps + 128 * (blk + 1));
+            DLR_CHAIN_WAIT(8, a);
+            add8(a);
+            if (blk + 2 < R / 32) {
+                rd8(a, ps + 128 * (blk + 2));
+                DLR_CHAIN_WAIT(8, b);
+            } else {
+                DLR_CHAIN_WAIT(0, b);
+            }
+            add8(b);
+        }
     };
 #undef DLR_CHAIN_WAIT
-    for (int64_t t = 0; t < kChainAhead; ++t) issue(t);
+    for (int64_t t = 0; t < A; ++t) issue(t);
     for (int64_t t = 0; t <= nslot; ++t) {
-        if (t < nslot) {  // uniform: slot t's own loads have landed (kChainAhead - 1 later slots still in flight)
-            if (wv == 1 || wv == 2)
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (kChainAhead - 1)) : "memory");
+        if (t < nslot) {  // uniform: slot t's own loads have landed (A - 1 later slots still in flight)
+            if (wv == 1)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Cfg::count(1) * (A - 1)) : "memory");
+            else if (wv == 2)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Cfg::count(2) * (A - 1)) : "memory");
             else if (wv == 3)
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kChainAhead - 1) : "memory");
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Cfg::count(3) * (A - 1)) : "memory");
         }
         // slot t staged for every helper; s_p[t & 1] no longer read by the chain
         lds_barrier();
@@ -1896,7 +1919,7 @@ __global__ __launch_bounds__(256) void k_dense_grad_chain(DevDense dd, int64_t f
             if (t > 0) chain(t - 1);
         } else if (t < nslot) {
             transform(t);
-            issue(t + kChainAhead);  // into the ring slot transformed in the previous iteration
+            issue(t + A);  // into the ring slot transformed in the previous iteration
         }
     }
     if (wv != 0) {
@@ -2460,11 +2483,13 @@ hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float 
     return hipGetLastError();
 }
 
-hipError_t launch_pm_products(const DevPm &pm, const float *w, int64_t D, float *p, hipStream_t s) {
-    if (pm.S <= 0) return hipSuccess;
+hipError_t launch_pm_products(const DevPm &pm, const float *w, int64_t D, float *p, hipStream_t s,
+                              const uint32_t *slices, int64_t nslices) {
+    const int64_t n = slices ? nslices : pm.S;
+    if (n <= 0) return hipSuccess;
     if (pm.nblk > kPmMaxBlocks || pm.split < 1) return hipErrorInvalidValue;
-    const unsigned grid = (unsigned)(((pm.S + 7) / 8) * 8 * pm.split);
-    hipLaunchKernelGGL(k_pm_products, dim3(grid), dim3(1024), 0, s, pm, w, D, p);
+    const unsigned grid = (unsigned)(((n + 7) / 8) * 8 * pm.split);
+    hipLaunchKernelGGL(k_pm_products, dim3(grid), dim3(1024), 0, s, pm, w, D, p, slices, n);
     return hipGetLastError();
 }
 
@@ -2707,12 +2732,19 @@ hipError_t launch_dense_grad(const DevDense &dd, int64_t first, int64_t B, const
     const double Bd = (double)B;
     if (!blocked && dd.D % 4 == 0) {
         const unsigned grid = (unsigned)((dd.D + kChainCols - 1) / kChainCols);
-        if (fused)
-            hipLaunchKernelGGL(k_dense_grad_chain<true>, dim3(grid), dim3(256), kChainLds, s, dd, first, B, resid, w,
-                               gout, Bf, Bd, lr, C);
-        else
-            hipLaunchKernelGGL(k_dense_grad_chain<false>, dim3(grid), dim3(256), kChainLds, s, dd, first, B, resid, w,
-                               gout, Bf, Bd, lr, C);
+#define DLR_CH(R)                                                                                                   \
+    if (fused)                                                                                                      \
+        hipLaunchKernelGGL((k_dense_grad_chain<true, R>), dim3(grid), dim3(256), ChainCfg<R>::kLds, s, dd, first, B, \
+                           resid, w, gout, Bf, Bd, lr, C);                                                          \
+    else                                                                                                            \
+        hipLaunchKernelGGL((k_dense_grad_chain<false, R>), dim3(grid), dim3(256), ChainCfg<R>::kLds, s, dd, first,   \
+                           B, resid, w, gout, Bf, Bd, lr, C);
+        if (dense_chain_rows() == 128) {
+            DLR_CH(128)
+        } else {
+            DLR_CH(256)
+        }
+#undef DLR_CH
         return hipGetLastError();
     }
     if (!blocked) {

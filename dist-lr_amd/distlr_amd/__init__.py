@@ -45,6 +45,7 @@ SYMBOLS = [
     "dlr_load_test_dense", "dlr_set_residency", "dlr_train_residency",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
     "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_train_band_rows", "dlr_train_relabeled", "dlr_train_unit_values", "dlr_train_product_margin",
+    "dlr_set_exchange_overlap", "dlr_exchange_overlap",
     "dlr_memory_info", "dlr_stream_bytes",
 ]
 
@@ -159,6 +160,8 @@ _sig("dlr_train_band_rows", C.c_int, P)
 _sig("dlr_train_relabeled", C.c_int, P)
 _sig("dlr_train_unit_values", C.c_int, P)
 _sig("dlr_train_product_margin", C.c_int, P)
+_sig("dlr_set_exchange_overlap", C.c_int, P, C.c_int)
+_sig("dlr_exchange_overlap", C.c_int, P)
 _sig("dlr_memory_info", C.c_int, P, C.POINTER(i64), C.POINTER(i64))
 _sig("dlr_stream_bytes", C.c_int, P, C.POINTER(i64), C.POINTER(i64))
 
@@ -577,6 +580,16 @@ class Engine:
         rc = lib.dlr_train_product_margin(self._h)
         self._c(min(rc, 0))
         return rc
+
+    def set_exchange_overlap(self, on: bool) -> None:
+        """World > 1, product margin: all-gather in pieces overlapped with
+        the next batch's pass 1 (dlr_set_exchange_overlap; default on)."""
+        self._c(lib.dlr_set_exchange_overlap(self._h, 1 if on else 0))
+
+    def exchange_overlap(self) -> bool:
+        rc = lib.dlr_exchange_overlap(self._h)
+        self._c(min(rc, 0))
+        return rc == 1
 
     def memory_info(self) -> Tuple[int, int]:
         a, b = i64(), i64()

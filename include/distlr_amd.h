@@ -363,6 +363,20 @@ int dlr_train_unit_values(dlr_ctx *ctx);
  * Sigmoid_ dot product for these shards (same arithmetic). */
 int dlr_train_product_margin(dlr_ctx *ctx);
 
+/* World > 1 with the product margin: the exchange overlapped with the next
+ * batch's margin (BASELINE north_star).  The in-place all-gather of the
+ * merged weights (lr.cc:122's Pull) runs in 4 pieces on a second stream --
+ * RCCL grouped send/recv of each rank's piece, or device copies on the
+ * loopback group -- and the next batch's pass 1 forms each 4,096-column
+ * slice as soon as every weight in it has landed (the slices of this rank's
+ * own key range right after the merge).  The step's results are unchanged
+ * (the same products; tests/test_gpu_pm.py).  On by default;
+ * dlr_set_exchange_overlap(ctx, 0) uses the plain all-gather and forms the
+ * products at the next margin.  dlr_exchange_overlap reports 1 when the
+ * loaded shard's steps use it. */
+int dlr_set_exchange_overlap(dlr_ctx *ctx, int on);
+int dlr_exchange_overlap(dlr_ctx *ctx);
+
 /* Device bytes resident for the loaded shards (for reporting). */
 int dlr_memory_info(dlr_ctx *ctx, int64_t *train_bytes, int64_t *test_bytes);
 

@@ -143,6 +143,45 @@ def test_pm_world_gt_1(pm_on, W, mode):
     assert_same_weights(eng.w, orc.w)
 
 
+@pytest.mark.parametrize("W", [2, 5])
+def test_pm_exchange_overlap_on_off(monkeypatch, W):
+    # the all-gather in pieces with the next batch's pass 1 formed slice
+    # group by slice group as the weights land (default), against the plain
+    # all-gather: the same bits, the oracle's; D = 300,000 gives key ranges
+    # that cut 4,096-column slices (a slice completes only when every range
+    # it overlaps has delivered its piece)
+    monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
+    monkeypatch.setenv("DLR_PM", "1")
+    D = 300_000
+    shards = [dlr.Dataset.generate(1500, D, 20, value_mode=1, seed=19, stream=r + 1) for r in range(W)]
+    seen = []
+
+    def setup(on):
+        def f(eng):
+            eng.set_exchange_overlap(on)
+            seen.append((eng.train_product_margin(), eng.exchange_overlap()))
+        return f
+
+    got = {on: run_group(shards, D, 2, 250, 0.2, setup=setup(on)) for on in (True, False)}
+    assert (1, True) in seen and (1, False) in seen
+    orc = oracle.run_worker([oracle_shard(s, D) for s in shards], D, 2, 250, 0.2)
+    assert_same_weights(got[True].w, orc.w, "overlapped exchange")
+    assert_same_weights(got[False].w, orc.w, "plain all-gather")
+
+
+def test_pm_overlap_through_rccl_one_rank(monkeypatch):
+    # the RCCL transport's pieced all-gather (grouped send/recv; no peers at
+    # one rank) with every slice in this rank's own range: the same bits
+    monkeypatch.setenv("DLR_FORCE_COLLECTIVES", "1")
+    monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
+    monkeypatch.setenv("DLR_PM", "1")
+    D = 300_000
+    ds = dlr.Dataset.generate(1500, D, 20, value_mode=1, seed=23, stream=1)
+    eng = run_engine([ds], D, 2, 250, 0.2)
+    orc = oracle.run_worker([oracle_shard(ds, D)], D, 2, 250, 0.2)
+    compare_runs(eng, orc)
+
+
 def test_pm_parameter_server_topology(pm_on):
     # W workers through dlr_worker_gradient / dlr_server_apply
     D = 200_000
