@@ -164,6 +164,7 @@ struct TrainShard {
         int64_t pair, ptr, ent, ws, nwaves;  // offsets into bcols, bptr, brow/bval, bws
     };
     int band_shift = 0;
+    bool band_longrun = false;  // band mode without the long-column split: runs of 10^5 entries in a band
     // margin with the hot (lowest, frequency-ordered) weights in LDS
     bool margin_hot = false;
     std::vector<Band> bands;
@@ -1544,7 +1545,7 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
             const TrainShard::Band &bd = t.bands[(size_t)k];
             dlr::DevBand dv{t.bcols + bd.pair, t.bptr + bd.ptr, t.bws + bd.ws, (const char *)t.brow + esz * (size_t)bd.ent,
                             t.bval ? t.bval + bd.ent : nullptr, bd.nwaves, t.row16};
-            e = dlr::launch_grad_band(dv, c->resid, t.gacc, c->stream);
+            e = dlr::launch_grad_band(dv, c->resid, t.gacc, c->stream, t.band_longrun);
         }
     } else {
         e = dlr::launch_grad(csc_view(c, b), c->D, c->resid, c->w, gout, B, lr, C, fused, c->stream);
@@ -1613,7 +1614,7 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
             const TrainShard::Band &bd = t.bands[(size_t)(t.bfirst[bb] + k)];
             dlr::DevBand dv{t.bcols + bd.pair, t.bptr + bd.ptr, t.bws + bd.ws, (const char *)t.brow + esz * (size_t)bd.ent,
                             t.bval ? t.bval + bd.ent : nullptr, bd.nwaves, t.row16};
-            e = dlr::launch_grad_band(dv, c->resid, t.gacc, c->gstream);
+            e = dlr::launch_grad_band(dv, c->resid, t.gacc, c->gstream, t.band_longrun);
         }
     }
     if (e == hipSuccess) e = hipEventRecord(c->ev_bdone, c->gstream);
@@ -2361,6 +2362,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             BandBuild<RowT> bb;
             build_bands(cptr, crow, cval, t.coff, nb, D, t.B, shift, t.unit, nthreads, bb);
             t.band_shift = shift;
+            t.band_longrun = long_min == 0;
             t.bands = std::move(bb.bands);
             t.bfirst = std::move(bb.bfirst);
             if ((r = upload(c, &t.bcols, bb.cols.data(), bb.cols.size(), 64))) return r;

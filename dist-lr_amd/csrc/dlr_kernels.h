@@ -182,7 +182,9 @@ hipError_t launch_grad_long(const DevLong &lg, int64_t B, const float *resid, fl
                             float lr, float C, bool fused, hipStream_t s, float *graw = nullptr);
 // Row bands: one launch per band, in band order, continuing gacc (zeroed
 // before the first band); then the update of every column from gacc.
-hipError_t launch_grad_band(const DevBand &bd, const float *resid, float *gacc, hipStream_t s);
+// longrun: the band holds runs of >= 64 entries of one column (band mode
+// without the long-column split, DLR_LONG_COLUMN=0): 16-byte LDS reads.
+hipError_t launch_grad_band(const DevBand &bd, const float *resid, float *gacc, hipStream_t s, bool longrun = false);
 // Long columns in row phases: piece partials part[slot], then the fixed
 // combine of each column's partials [cseg[l], cseg[l+1]) into graw[j].
 hipError_t launch_long_phase(const DevLPhase &lp, const uint32_t *cols, const uint32_t *cseg, int64_t ncols,

@@ -252,7 +252,7 @@ __device__ __forceinline__ float ordered_segment_dot(int64_t e0, int64_t e1, int
 // k < K (empty: a == b), each summed in order from acc[k]; the wave's
 // entries are [e0, e1).  Same loads, gathers and products as
 // ordered_segment_dot.
-template <typename IdxT, bool UNIT, int K>
+template <typename IdxT, bool UNIT, int K, bool LONGRUN = false>
 __device__ __forceinline__ void ordered_segments_dot(int64_t e0, int64_t e1, const int64_t (&a)[K],
                                                      const int64_t (&b)[K], float (&acc)[K], int lane,
                                                      const IdxT *__restrict__ idx, const float *__restrict__ val,
@@ -313,6 +313,25 @@ __device__ __forceinline__ void ordered_segments_dot(int64_t e0, int64_t e1, con
             int o = (int)(lo - ws);
             const int oe = (int)(hi - ws);
             float s = acc[k];
+            if (LONGRUN && oe - o >= 64) {
+                // a long run (DLR_LONG_COLUMN=0 in band mode: C3's hot
+                // columns put ~125,000 entries of one column in a band, so a
+                // whole window is one lane's run): 16-byte reads, 32 products
+                // per LDS wait instead of 4, same order
+                for (; o & 3; ++o) s = s + lds[o];
+                for (; o + 32 <= oe; o += 32) {
+                    float4 q[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) q[u] = *reinterpret_cast<const float4 *>(lds + o + 4 * u);
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        s = s + q[u].x;
+                        s = s + q[u].y;
+                        s = s + q[u].z;
+                        s = s + q[u].w;
+                    }
+                }
+            }
             for (; o + 4 <= oe; o += 4) {
                 const float x0 = lds[o], x1 = lds[o + 1], x2 = lds[o + 2], x3 = lds[o + 3];
                 s = s + x0;
@@ -1202,7 +1221,7 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad_touched(DevCsc cs, const
 // band after band IS lr.cc:37's sequential order: bitwise the classic
 // kernel's result.  Each column appears at most once per band, so a launch
 // has no write conflicts; the kernel boundary orders the bands.
-template <typename RowT, bool UNIT = false>
+template <typename RowT, bool UNIT = false, bool LONGRUN = false>
 __global__ __launch_bounds__(kWaves *kWave) void k_grad_band(DevBand bd, const RowT *__restrict__ brow,
                                                              const float *__restrict__ resid,
                                                              float *__restrict__ gacc) {
@@ -1231,7 +1250,7 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad_band(DevBand bd, const R
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = s0 + lane + (int64_t)k * kWave < sl ? __builtin_nontemporal_load(gacc + j[k]) : 0.0f;
-    ordered_segments_dot<RowT, UNIT, K>(e0, e1, a, b, acc, lane, brow, bd.val, resid, s_p[wv]);
+    ordered_segments_dot<RowT, UNIT, K, LONGRUN>(e0, e1, a, b, acc, lane, brow, bd.val, resid, s_p[wv]);
 #pragma unroll
     for (int k = 0; k < K; ++k)
         if (s0 + lane + (int64_t)k * kWave < sl) __builtin_nontemporal_store(acc[k], gacc + j[k]);
@@ -2632,22 +2651,29 @@ hipError_t launch_grad_long(const DevLong &lg, int64_t B, const float *resid, fl
     return hipGetLastError();
 }
 
-hipError_t launch_grad_band(const DevBand &bd, const float *resid, float *gacc, hipStream_t s) {
+hipError_t launch_grad_band(const DevBand &bd, const float *resid, float *gacc, hipStream_t s, bool longrun) {
     if (bd.nwaves <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((bd.nwaves + kWaves - 1) / kWaves);
     const dim3 blk(kWaves * kWave);
-    if (bd.row16 && bd.val == nullptr)
-        hipLaunchKernelGGL((k_grad_band<uint16_t, true>), dim3(grid), blk, 0, s, bd,
-                           static_cast<const uint16_t *>(bd.row), resid, gacc);
-    else if (bd.row16)
-        hipLaunchKernelGGL((k_grad_band<uint16_t, false>), dim3(grid), blk, 0, s, bd,
-                           static_cast<const uint16_t *>(bd.row), resid, gacc);
-    else if (bd.val == nullptr)
-        hipLaunchKernelGGL((k_grad_band<uint32_t, true>), dim3(grid), blk, 0, s, bd,
-                           static_cast<const uint32_t *>(bd.row), resid, gacc);
-    else
-        hipLaunchKernelGGL((k_grad_band<uint32_t, false>), dim3(grid), blk, 0, s, bd,
-                           static_cast<const uint32_t *>(bd.row), resid, gacc);
+#define DLR_GB(RT, U, L)                                                                                     \
+    hipLaunchKernelGGL((k_grad_band<RT, U, L>), dim3(grid), blk, 0, s, bd, static_cast<const RT *>(bd.row), resid, \
+                       gacc)
+#define DLR_GBL(RT, U)      \
+    if (longrun)            \
+        DLR_GB(RT, U, true); \
+    else                    \
+        DLR_GB(RT, U, false);
+    if (bd.row16 && bd.val == nullptr) {
+        DLR_GBL(uint16_t, true)
+    } else if (bd.row16) {
+        DLR_GBL(uint16_t, false)
+    } else if (bd.val == nullptr) {
+        DLR_GBL(uint32_t, true)
+    } else {
+        DLR_GBL(uint32_t, false)
+    }
+#undef DLR_GBL
+#undef DLR_GB
     return hipGetLastError();
 }
 
