@@ -252,7 +252,114 @@ __device__ __forceinline__ float ordered_segment_dot(int64_t e0, int64_t e1, int
 // k < K (empty: a == b), each summed in order from acc[k]; the wave's
 // entries are [e0, e1).  Same loads, gathers and products as
 // ordered_segment_dot.
-template <typename IdxT, bool UNIT, int K, bool LONGRUN = false>
+// ordered_segments_dot for bands that hold long runs (DLR_LONG_COLUMN=0 in
+// band mode: a Zipf-head column puts ~125,000 entries into each 2^20-row
+// band, so whole windows are one lane's run and that lane's serial chain is
+// the band's critical path).  Same loads, gathers, products and order of
+// additions as ordered_segments_dot; the window loop is software-pipelined
+// so the chain never waits for memory: while the lanes sum window w, the
+// residual gathers of window w+1 and the entry loads of window w+2 are in
+// flight (issue order gathers(w+1), loads(w+2): the in-order vmcnt makes
+// each stage's wait exact).  Runs of >= 64 products are read 16 bytes at a
+// time, 32 per LDS wait.
+template <typename IdxT, bool UNIT, int K>
+__device__ __forceinline__ void ordered_segments_dot_piped(int64_t e0, int64_t e1, const int64_t (&a)[K],
+                                                           const int64_t (&b)[K], float (&acc)[K], int lane,
+                                                           const IdxT *__restrict__ idx, const float *__restrict__ val,
+                                                           const float *__restrict__ table, float *lds) {
+    using IV = typename Vec4<IdxT>::type;
+    constexpr int kT = kWin / (kVec * kWave);
+    constexpr int kChunk = kVec * kWave;
+    const int64_t base = e0 & ~int64_t(kVec - 1);
+    struct Win {
+        IV iv[kT];
+        float4 v[kT];
+    };
+    // loads: always issued (clamped to the last window): fixed vmcnt counts
+    auto load = [&](int64_t ws, Win &w) {
+        const int64_t wc = ws < e1 ? ws : base;
+#pragma unroll
+        for (int t = 0; t < kT; ++t) {
+            const int64_t e = wc + t * kChunk + lane * kVec;
+            const int64_t ec = e < e1 ? e : base;
+            w.iv[t] = load_stream(reinterpret_cast<const IV *>(idx + ec));
+            if constexpr (UNIT)
+                w.v[t] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+            else
+                w.v[t] = load_stream(reinterpret_cast<const float4 *>(val + ec));
+        }
+    };
+    auto gather = [&](int64_t ws, const Win &w, float (&g)[kT][kVec]) {
+#pragma unroll
+        for (int t = 0; t < kT; ++t) {
+            const int64_t e = ws + t * kChunk + lane * kVec;
+            g[t][0] = table[(e >= e0 && e < e1) ? (unsigned)w.iv[t].x : 0u];
+            g[t][1] = table[(e + 1 >= e0 && e + 1 < e1) ? (unsigned)w.iv[t].y : 0u];
+            g[t][2] = table[(e + 2 >= e0 && e + 2 < e1) ? (unsigned)w.iv[t].z : 0u];
+            g[t][3] = table[(e + 3 >= e0 && e + 3 < e1) ? (unsigned)w.iv[t].w : 0u];
+        }
+    };
+    Win wa, wb;
+    float ga[kT][kVec];
+    load(base, wa);
+    gather(base, wa, ga);
+    load(base + kWin, wb);
+    for (int64_t ws = base; ws < e1; ws += kWin) {
+        // park window ws's products (its gathers were issued an iteration ago)
+#pragma unroll
+        for (int t = 0; t < kT; ++t) {
+            const int o = t * kChunk + lane * kVec;
+            const int64_t e = ws + o;
+            float4 p;
+            p.x = (e >= e0 && e < e1) ? ga[t][0] * wa.v[t].x : 0.0f;
+            p.y = (e + 1 >= e0 && e + 1 < e1) ? ga[t][1] * wa.v[t].y : 0.0f;
+            p.z = (e + 2 >= e0 && e + 2 < e1) ? ga[t][2] * wa.v[t].z : 0.0f;
+            p.w = (e + 3 >= e0 && e + 3 < e1) ? ga[t][3] * wa.v[t].w : 0.0f;
+            *reinterpret_cast<float4 *>(lds + o) = p;
+        }
+        wave_sync();
+        // window ws+1: its entries landed during the previous sums; issue its
+        // gathers, then the loads of window ws+2, all in flight under the sums
+        wa = wb;
+        gather(ws + kWin, wa, ga);
+        load(ws + 2 * kWin, wb);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t lo = a[k] > ws ? a[k] : ws;
+            const int64_t hi = b[k] < ws + kWin ? b[k] : ws + kWin;
+            int o = (int)(lo - ws);
+            const int oe = (int)(hi - ws);
+            float s = acc[k];
+            if (oe - o >= 64) {
+                for (; o & 3; ++o) s = s + lds[o];
+                for (; o + 32 <= oe; o += 32) {
+                    float4 q[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) q[u] = *reinterpret_cast<const float4 *>(lds + o + 4 * u);
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        s = s + q[u].x;
+                        s = s + q[u].y;
+                        s = s + q[u].z;
+                        s = s + q[u].w;
+                    }
+                }
+            }
+            for (; o + 4 <= oe; o += 4) {
+                const float x0 = lds[o], x1 = lds[o + 1], x2 = lds[o + 2], x3 = lds[o + 3];
+                s = s + x0;
+                s = s + x1;
+                s = s + x2;
+                s = s + x3;
+            }
+            for (; o < oe; ++o) s = s + lds[o];
+            acc[k] = s;
+        }
+        wave_sync();
+    }
+}
+
+template <typename IdxT, bool UNIT, int K>
 __device__ __forceinline__ void ordered_segments_dot(int64_t e0, int64_t e1, const int64_t (&a)[K],
                                                      const int64_t (&b)[K], float (&acc)[K], int lane,
                                                      const IdxT *__restrict__ idx, const float *__restrict__ val,
@@ -313,25 +420,6 @@ __device__ __forceinline__ void ordered_segments_dot(int64_t e0, int64_t e1, con
             int o = (int)(lo - ws);
             const int oe = (int)(hi - ws);
             float s = acc[k];
-            if (LONGRUN && oe - o >= 64) {
-                // a long run (DLR_LONG_COLUMN=0 in band mode: C3's hot
-                // columns put ~125,000 entries of one column in a band, so a
-                // whole window is one lane's run): 16-byte reads, 32 products
-                // per LDS wait instead of 4, same order
-                for (; o & 3; ++o) s = s + lds[o];
-                for (; o + 32 <= oe; o += 32) {
-                    float4 q[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) q[u] = *reinterpret_cast<const float4 *>(lds + o + 4 * u);
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        s = s + q[u].x;
-                        s = s + q[u].y;
-                        s = s + q[u].z;
-                        s = s + q[u].w;
-                    }
-                }
-            }
             for (; o + 4 <= oe; o += 4) {
                 const float x0 = lds[o], x1 = lds[o + 1], x2 = lds[o + 2], x3 = lds[o + 3];
                 s = s + x0;
@@ -1250,7 +1338,10 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad_band(DevBand bd, const R
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = s0 + lane + (int64_t)k * kWave < sl ? __builtin_nontemporal_load(gacc + j[k]) : 0.0f;
-    ordered_segments_dot<RowT, UNIT, K, LONGRUN>(e0, e1, a, b, acc, lane, brow, bd.val, resid, s_p[wv]);
+    if constexpr (LONGRUN)
+        ordered_segments_dot_piped<RowT, UNIT, K>(e0, e1, a, b, acc, lane, brow, bd.val, resid, s_p[wv]);
+    else
+        ordered_segments_dot<RowT, UNIT, K>(e0, e1, a, b, acc, lane, brow, bd.val, resid, s_p[wv]);
 #pragma unroll
     for (int k = 0; k < K; ++k)
         if (s0 + lane + (int64_t)k * kWave < sl) __builtin_nontemporal_store(acc[k], gacc + j[k]);
