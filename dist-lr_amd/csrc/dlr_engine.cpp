@@ -103,6 +103,16 @@ struct TrainShard {
     float *pm_val = nullptr, *pm_p = nullptr;
     uint16_t *pm_qs = nullptr;
     std::vector<int64_t> pmo_list, pmo_pofs, pmo_rg, pmo_qs;
+    // row-round gradient (dlr_kernels.h DevRt) of every product-margin batch:
+    // gq / val at rtoff[b] (pmS * rt_rounds * rt_cap[b] entries), cend at
+    // b*pmS*kPmSlice; rt_rounds rounds per batch
+    bool rt = false;
+    int rt_rounds = 0;
+    uint32_t *rt_gq = nullptr;
+    float *rt_val = nullptr;
+    uint16_t *rt_cend = nullptr;
+    std::vector<int64_t> rtoff;
+    std::vector<uint32_t> rt_cap;
     // world > 1: the exchange / next-margin overlap (dlr_train_step).  The
     // in-place all-gather of the updated weights runs in kXPieces pieces on
     // the exchange stream; after piece k the next batch's pass 1 forms the
@@ -334,6 +344,10 @@ int place(dlr_ctx *c, T **field, const T *src, size_t n, size_t pad, const Range
 
 void free_train(dlr_ctx *c) {
     TrainShard &t = c->train;
+    // a reload frees what the last steps' kernels and copies may still read
+    // (hipFree alone is not relied on to order them)
+    for (hipStream_t s : {c->stream, c->cstream, c->gstream, c->xstream})
+        if (s) (void)hipStreamSynchronize(s);
     if (t.sparse_stream) {
         if (c->cstream) (void)hipStreamSynchronize(c->cstream);
         for (StreamArr &a : t.sarr) {
@@ -360,7 +374,8 @@ void free_train(dlr_ctx *c) {
                     (void *)t.bws, t.brow, (void *)t.bval, (void *)t.gacc, (void *)t.lpdesc, (void *)t.lpptr,
                     (void *)t.lpslot, (void *)t.lpws, (void *)t.lprow, (void *)t.lpval, (void *)t.pm_lbeg,
                     (void *)t.pm_list, (void *)t.pm_pofs, (void *)t.pm_rg, (void *)t.pm_qoff, (void *)t.pm_val,
-                    (void *)t.pm_p, (void *)t.pm_qs, (void *)t.xslices})
+                    (void *)t.pm_p, (void *)t.pm_qs, (void *)t.xslices, (void *)t.rt_gq, (void *)t.rt_val,
+                    (void *)t.rt_cend})
         dev_free(c, p);
     t = TrainShard();
     c->pm_ready = -1;
@@ -1104,9 +1119,87 @@ struct PmBatch {
     std::vector<uint16_t> qs;
     int groups = 0;
     int64_t maxslice = 0;
+    // the row-round gradient's view of the same batch (dlr_kernels.h DevRt);
+    // empty when a slice holds more than kRtCap entries
+    std::vector<uint32_t> gq;
+    std::vector<float> rval;
+    std::vector<uint16_t> cend;
+    uint32_t rtcap = 0;  // entries per (slice, round)
 };
 
-bool pm_batch(const CsrView &ds, const dlr::BatchSpan &sp, int64_t D, bool unit, PmBatch &o) {
+// DevRt arrays of one product-margin batch, from its (unpacked) list words
+// (column | block << 12 | rank << 22), each entry's batch row and value (list
+// order): slots in column-major order within each slice, column runs, and
+// the entries of each (slice, round) at a fixed stride (o.rtcap) so that a
+// workgroup computes where its rounds are without loading anything first.
+void rt_batch(const std::vector<uint32_t> &words, const std::vector<uint16_t> &rows, const std::vector<float> &vals,
+              const std::vector<uint32_t> &slice_n, const std::vector<uint32_t> &cnt, int64_t S, int64_t nblk,
+              int64_t R, PmBatch &o) {
+    const int64_t T = (R + dlr::kRtRows - 1) / dlr::kRtRows;
+    const bool unit = vals.empty();
+    std::vector<uint32_t> gq(words.size(), 0), rb((size_t)(S * (T + 1)));
+    o.cend.assign((size_t)(S * dlr::kPmSlice), 0);
+    std::vector<uint32_t> cur(dlr::kPmSlice);
+    uint32_t cap = 4;
+    auto drop = [&] {
+        o.gq.clear();
+        o.rval.clear();
+        o.cend.clear();
+        o.rtcap = 0;
+    };
+    for (int64_t q = 0; q < S; ++q) {
+        const uint32_t l0 = slice_n[(size_t)q], l1 = slice_n[(size_t)q + 1];
+        auto real = [&](uint32_t li) {
+            const uint32_t wd = words[li];
+            return (wd >> 22) < cnt[(size_t)(((wd >> 12) & 1023u) * S + q)];
+        };
+        std::fill(cur.begin(), cur.end(), 0u);
+        for (uint32_t li = l0; li < l1; ++li)
+            if (real(li)) ++cur[words[li] & 0xFFFu];
+        uint32_t at = 0;
+        uint16_t *ce = o.cend.data() + (size_t)q * dlr::kPmSlice;
+        for (int c = 0; c < dlr::kPmSlice; ++c) {
+            const uint32_t n = cur[(size_t)c];
+            cur[(size_t)c] = at;
+            at += n;
+            ce[c] = (uint16_t)std::min<uint32_t>(at, 0xFFFFu);
+        }
+        if (at > (uint32_t)dlr::kRtCap) return drop();  // does not fit LDS
+        // list order is (block, row, column): each column's slots take its
+        // rows in ascending order
+        for (uint32_t li = l0; li < l1; ++li) {
+            const uint32_t row = rows[li];
+            gq[li] = row << 16 | (real(li) ? cur[words[li] & 0xFFFu]++ : (uint32_t)dlr::kRtCap);
+        }
+        // round t starts at the chunk of block t * kRtRows / 64
+        uint32_t li = l0;
+        int64_t k = 0;
+        for (int64_t t = 0; t <= T; ++t) {
+            const int64_t kt = std::min<int64_t>(nblk, t * (dlr::kRtRows / dlr::kPmRows));
+            for (; k < kt; ++k) li += (cnt[(size_t)(k * S + q)] + 3) & ~3u;
+            rb[(size_t)(q * (T + 1) + t)] = li;
+            if (t > 0) cap = std::max(cap, li - rb[(size_t)(q * (T + 1) + t - 1)]);
+        }
+    }
+    if (cap > (uint32_t)dlr::kRtMaxRound) return drop();  // one 4-entry group per thread and round
+    // (slice, round) q * T + t holds its entries at [(q * T + t) * cap, + cap):
+    // the round's list entries, then sinks (row t * kRtRows, slot kRtCap)
+    o.rtcap = cap;
+    o.gq.assign((size_t)(S * T * cap), 0);
+    if (!unit) o.rval.assign((size_t)(S * T * cap), 0.0f);
+    for (int64_t q = 0; q < S; ++q)
+        for (int64_t t = 0; t < T; ++t) {
+            const uint32_t a = rb[(size_t)(q * (T + 1) + t)], b = rb[(size_t)(q * (T + 1) + t + 1)];
+            const size_t d = (size_t)((q * T + t) * cap);
+            for (uint32_t e = 0; e < cap; ++e) {
+                const bool in = a + e < b;
+                o.gq[d + e] = in ? gq[a + e] : (uint32_t)(t * dlr::kRtRows) << 16 | (uint32_t)dlr::kRtCap;
+                if (!unit) o.rval[d + e] = in ? vals[a + e] : 0.0f;
+            }
+        }
+}
+
+bool pm_batch(const CsrView &ds, const dlr::BatchSpan &sp, int64_t D, bool unit, bool rt, PmBatch &o) {
     const int64_t N = ds.n_rows, R = sp.rows;
     const int64_t S = (D + dlr::kPmSlice - 1) / dlr::kPmSlice, nblk = (R + dlr::kPmRows - 1) / dlr::kPmRows;
     if (nblk > dlr::kPmMaxBlocks) return false;
@@ -1149,12 +1242,17 @@ bool pm_batch(const CsrView &ds, const dlr::BatchSpan &sp, int64_t D, bool unit,
     o.pofs.assign((size_t)(S * nblk), 0);
     for (int64_t q = 0; q < S; ++q)
         for (int64_t k = 0; k < nblk; ++k) o.pofs[(size_t)(q * nblk + k)] = cofs[(size_t)(k * S + q)];
-    // padding entries: column 0, value 0, the group's block and rank
+    // padding entries: column 0, value 0, the group's block and rank (and,
+    // for the row-round gradient, the block's first row)
+    std::vector<uint16_t> lrow(rt ? E : 0);
     for (int64_t q = 0; q < S; ++q) {
         uint32_t li = slice_n[(size_t)q];
         for (int64_t k = 0; k < nblk; ++k) {
             const uint32_t n = cnt[(size_t)(k * S + q)], np = (n + 3) & ~3u;
-            for (uint32_t j = n; j < np; ++j) o.list[li + j] = (uint32_t)k << 12 | j << 22;
+            for (uint32_t j = n; j < np; ++j) {
+                o.list[li + j] = (uint32_t)k << 12 | j << 22;
+                if (rt) lrow[li + j] = (uint16_t)(k * dlr::kPmRows);
+            }
             li += np;
         }
     }
@@ -1188,12 +1286,14 @@ bool pm_batch(const CsrView &ds, const dlr::BatchSpan &sp, int64_t D, bool unit,
                 const uint32_t j = slot - cofs[(size_t)(k * S + q)];
                 const uint32_t li = lcur[(size_t)(k * S + q)]++;
                 o.list[li] = (uint32_t)(ds.col[e] % dlr::kPmSlice) | (uint32_t)k << 12 | j << 22;
+                if (rt) lrow[li] = (uint16_t)i;
                 if (!unit) o.val[li] = ds.val[e];
                 o.qs[q0 + (size_t)(kk / 8) * 512 + (size_t)l * 8 + (size_t)(kk % 8)] = (uint16_t)(slot - o.rg[(size_t)k]);
             }
         }
     }
     o.qoff[(size_t)nblk] = (uint32_t)o.qs.size();
+    if (rt) rt_batch(o.list, lrow, o.val, slice_n, cnt, S, nblk, R, o);
     // pack the entries in groups of four (dlr_kernels.h DevPm)
     for (size_t g = 0; g < E / 4; ++g) {
         const uint32_t *e = o.list.data() + 4 * g;
@@ -1522,6 +1622,20 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
                                                   c->stream);
         if (e == hipSuccess) e = dense_batch_done(c, b);
         return e;
+    }
+    if (t.pcsc && t.rt) {
+        const dlr::DevRt rt{t.rt_gq + t.rtoff[(size_t)b], t.rt_val ? t.rt_val + t.rtoff[(size_t)b] : nullptr,
+                            t.rt_cend + (size_t)b * (size_t)t.pmS * dlr::kPmSlice, (int)t.rt_cap[(size_t)b],
+                            t.rt_rounds};
+        if (t.pm_fused && fused) {
+            const int64_t nx = (b + 1) % (int64_t)t.plan.size();
+            const dlr::DevPm next = pm_view(c, nx);
+            const hipError_t e =
+                dlr::launch_grad_rt(rt, c->D, B, c->resid, c->w, nullptr, lr, C, true, &next, t.pm_p, c->stream);
+            if (e == hipSuccess) c->pm_ready = nx;
+            return e;
+        }
+        return dlr::launch_grad_rt(rt, c->D, B, c->resid, c->w, gout, lr, C, fused, nullptr, nullptr, c->stream);
     }
     if (t.pcsc) {
         if (t.pm_fused && fused) {
@@ -2101,8 +2215,16 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         if (!t.sparse_stream && !(pme && strcmp(pme, "0") == 0) && ((pme && strcmp(pme, "1") == 0) || S >= 128)) {
             std::vector<PmBatch> pm((size_t)nb);
             std::atomic<bool> ok{true};
+            // the row-round gradient: by default for batches of <= 2 rounds
+            // (C2 at B = 8,192: 7.5 vs 10.0 us for k_grad_lds); at 8 rounds
+            // (B = 65,536) k_grad_lds is faster.  DLR_GRAD_RT=1
+            // takes it for every batch that fits, =0 never.
+            const char *rte = getenv("DLR_GRAD_RT");
+            const int64_t rounds = (t.B + dlr::kRtRows - 1) / dlr::kRtRows;
+            const bool want_rt = rounds <= dlr::kRtMaxRounds &&
+                                 (rte ? strcmp(rte, "0") != 0 : rounds <= 2);
             for_batches(nb, nthreads, [&](int64_t b) {
-                if (ok && !pm_batch(src, t.plan[(size_t)b], D, t.unit, pm[(size_t)b])) ok = false;
+                if (ok && !pm_batch(src, t.plan[(size_t)b], D, t.unit, want_rt, pm[(size_t)b])) ok = false;
             });
             if (ok) {
                 // only where it leaves the headroom the residency choice keeps
@@ -2110,7 +2232,8 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 int64_t need = 0;
                 for (const PmBatch &q : pm)
                     need += (int64_t)(q.list.size() * 4 + q.val.size() * 4 + q.pofs.size() * 4 + q.rg.size() * 8 +
-                                      q.qs.size() * 2 + q.lbeg.size() * 4);
+                                      q.qs.size() * 2 + q.lbeg.size() * 4 + q.gq.size() * 4 + q.rval.size() * 4 +
+                                      q.cend.size() * 2);
                 size_t fr = 0, tot = 0;
                 HIPC(c, hipMemGetInfo(&fr, &tot));
                 if ((double)need + (double)((size_t)8 << 30) > (double)fr) {
@@ -2164,6 +2287,25 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 if ((rc = cat_upload(&PmBatch::rg, &t.pm_rg, t.pmo_rg, 1, 0))) return rc;
                 if ((rc = cat_upload(&PmBatch::qoff, &t.pm_qoff, t.pmo_rg, 1, 0))) return rc;
                 if ((rc = cat_upload(&PmBatch::qs, &t.pm_qs, t.pmo_qs, 1, 8))) return rc;
+                bool rt_all = want_rt;
+                for (const PmBatch &q : pm) rt_all = rt_all && !q.gq.empty();
+                if (rt_all) {
+                    std::vector<int64_t> ceoff((size_t)nb + 1);
+                    t.rtoff.assign((size_t)nb + 1, 0);
+                    t.rt_cap.assign((size_t)nb, 0);
+                    for (int64_t b = 0; b < nb; ++b) {
+                        t.rtoff[(size_t)b + 1] = t.rtoff[(size_t)b] + (int64_t)pm[(size_t)b].gq.size();
+                        t.rt_cap[(size_t)b] = pm[(size_t)b].rtcap;
+                    }
+                    for (int64_t b = 0; b <= nb; ++b) ceoff[(size_t)b] = b * S * dlr::kPmSlice;
+                    if ((rc = cat_upload(&PmBatch::gq, &t.rt_gq, t.rtoff, 1, 0))) return rc;
+                    if (!t.unit && (rc = cat_upload(&PmBatch::rval, &t.rt_val, t.rtoff, 1, 0))) return rc;
+                    if ((rc = cat_upload(&PmBatch::cend, &t.rt_cend, ceoff, 1, 0))) return rc;
+                    t.rt = true;
+                    t.rt_rounds = (int)((t.B + dlr::kRtRows - 1) / dlr::kRtRows);
+                    resid_need = std::max(resid_need, (int64_t)t.rt_rounds * dlr::kRtRows);
+                    csc_bytes += (int64_t)(t.rtoff.back() * (t.unit ? 4 : 8) + ceoff.back() * 2);
+                }
                 if ((rc = dev_alloc(c, (void **)&t.pm_p, (size_t)(pcap + 64) * 4))) return rc;
                 HIPC(c, hipMemsetAsync(t.pm_p, 0, (size_t)(pcap + 64) * 4, c->stream));
                 csc_bytes += (int64_t)(lbeg_n * 4 + t.pmo_list.back() * (t.unit ? 2 : 6) +

@@ -148,6 +148,28 @@ struct DevPm {
     int split;             // pass-1 workgroups per slice (standalone pass)
 };
 
+// ROW-ROUND gradient (RT) of a product-margin batch (dlr_kernels.hip
+// "Row-round gradient").  Round t covers batch rows [t * kRtRows, (t + 1) *
+// kRtRows).  The entries of slice s in round t are gq / val [(s * rounds +
+// t) * cap, + cap), in pass 1's order (64-row blocks ascending, rows
+// ascending within a block): gq = batch row << 16 | slot, where slot is the
+// entry's place in the slice's COLUMN-MAJOR order (columns ascending, rows
+// ascending within a column); padding entries (the rest of each (slice,
+// round) and each chunk's padding) carry the round's first row and slot
+// kRtCap, a sink.  cend[s * kPmSlice + c] = the end of local column c's run
+// in column-major order (its start is the previous column's end).
+constexpr int kRtRows = 8192;       // rows per round: 32 KB of residuals in LDS
+constexpr int kRtMaxRounds = 8;     // batches of up to 65,536 rows
+constexpr int kRtCap = 20480;       // entries of one slice (their products live in LDS)
+constexpr int kRtMaxRound = 4096;   // entries of one (slice, round): a 4-entry group per thread
+struct DevRt {
+    const uint32_t *gq;
+    const float *val;  // null: unit values
+    const uint16_t *cend;
+    int cap;     // entries per (slice, round), a multiple of 4
+    int rounds;
+};
+
 // Dense rows (row-major N x D fp32) and 0/1 labels as floats.
 struct DevDense {
     const float *X;
@@ -209,6 +231,11 @@ hipError_t launch_pm_margin(const DevPm &pm, const DevBatch &bt, const float *p,
 // pass 1 for free in the gradient's workgroups (slice s = workgroup s).
 hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const float *resid, float *w, float lr,
                               float C, const DevPm &next, float *p, hipStream_t s);
+// The row-round gradient (DevRt): the update (fused) or the pushed gradient
+// (gout); next != null (fused only): also the next batch's products, as
+// launch_grad_lds_pm.  resid must hold rounds * kRtRows floats.
+hipError_t launch_grad_rt(const DevRt &rt, int64_t D, int64_t B, const float *resid, float *w, float *gout, float lr,
+                          float C, bool fused, const DevPm *next, float *p, hipStream_t s);
 // Touched-column layout (dlr_kernels.hip "Touched-column layout"): cs.ptr
 // spans the ncols touched columns cols[] of the batch.
 hipError_t launch_grad_touched(const DevCsc &cs, const uint32_t *cols, int64_t ncols, const float *resid,

@@ -33,6 +33,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
 
 #include "dlr_kernels.h"
 
@@ -874,18 +875,21 @@ struct PmPass1 {
     float4 v[U];
     uint32_t po[NPO];
     uint32_t c0 = 0, c1 = 0;
-    __device__ __forceinline__ void fetch(const DevPm &pm, uint32_t g0) {
+    // group set u of the round starting at g0 (k_grad_rt spreads the sets
+    // over its rounds)
+    __device__ __forceinline__ void fetch_one(const DevPm &pm, uint32_t g0, int u) {
         // unit values: a dummy load (the list's own words, in range) keeps
         // the instruction count fixed
         const float4 *vp = pm.val ? reinterpret_cast<const float4 *>(pm.val) : reinterpret_cast<const float4 *>(pm.list);
         const uint32_t vs = pm.val ? 0u : 1u;
+        const uint32_t g = g0 + u * NT + threadIdx.x;
+        const uint32_t gc = g < c1 ? g : c0;
+        pk[u] = load_stream(reinterpret_cast<const uint2 *>(pm.list) + gc);
+        v[u] = load_stream(vp + (gc >> vs));
+    }
+    __device__ __forceinline__ void fetch(const DevPm &pm, uint32_t g0) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t g = g0 + u * NT + threadIdx.x;
-            const uint32_t gc = g < c1 ? g : c0;
-            pk[u] = load_stream(reinterpret_cast<const uint2 *>(pm.list) + gc);
-            v[u] = load_stream(vp + (gc >> vs));
-        }
+        for (int u = 0; u < U; ++u) fetch_one(pm, g0, u);
     }
     // The slice's list range and chunk offsets (no dependence on anything):
     // k_grad_lds issues these first, so the fetch() that needs c0 waits for
@@ -1249,6 +1253,198 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     DLR_STAMP(7);
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// Row-round gradient (RT; product-margin batches, dlr_kernels.h DevRt).
+// k_grad_lds stages the residuals of a whole 32,768-row phase before it can
+// multiply anything (its column-major windows span the phase), so each CU
+// waits for two 128 KB fills in turn and every phase ends at a barrier.
+// Here the workgroup of slice s reads its entries in ROW order -- pass 1's
+// list order -- so the batch is consumed in rounds of kRtRows rows: round
+// t needs only rows [t*R, (t+1)*R) of the residuals (32 KB).  Every round's
+// entries (one 4-entry group per thread, at a fixed stride: no offsets to
+// load first) are in flight from the start, the residuals of rounds t+1 and
+// t+2 while round t computes.  Each entry's product fl32(r_i * x_ij) goes to
+// its slot in the slice's column-major order in LDS; after the last round
+// each lane adds its column's run of products in order (rows ascending)
+// from +0: the same products and the same additions as lr.cc:35-39, bitwise
+// k_grad_lds's sums.  The update and the fused pass 1 are k_grad_lds's.
+template <typename F, int... I>
+__device__ __forceinline__ void unroll_seq(F &&f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+
+template <bool FUSED, bool PM, bool UNIT>
+__global__ __launch_bounds__(kGradWaves *kWave) void k_grad_rt(DevRt rt, int64_t D, const float *__restrict__ resid,
+                                                               float *__restrict__ w, float *__restrict__ gout,
+                                                               float Bf, double Bd, float lr, float C,
+                                                               DevPm pn = DevPm{}, float *__restrict__ pm_p = nullptr) {
+    constexpr int NT = kGradWaves * kWave;
+    constexpr int NG = kGradNG;
+    constexpr int kSink = 16;  // the sink slot kRtCap and the chain's unclamped reads past a run
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float *s_prod = smem;
+    float *s_r = smem + kRtCap + kSink;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int s = blockIdx.x;
+    const int64_t ng = (D + 63) / 64;
+    const int64_t gfirst = (int64_t)s * (kGradWaves * NG) + wv;
+    DLR_STAMP(0);
+    const int T = rt.rounds;
+    // residuals: three register sets, always indexed by compile-time
+    // constants (rounds are unrolled by unroll_seq; a runtime-indexed set
+    // goes to scratch).  Native vectors: a float4 struct copied to LDS goes
+    // through a stack temporary.
+    struct Rnd {
+        v4f r0, r1;  // rows 4*tid and 4*(tid + NT) of the round
+    };
+    Rnd rr[3];
+    auto issue = [&](int t, Rnd &x) __attribute__((always_inline)) {
+        const v4f *src = reinterpret_cast<const v4f *>(resid + (int64_t)t * kRtRows);
+        x.r0 = src[threadIdx.x];
+        x.r1 = src[NT + threadIdx.x];
+    };
+    // round t's entries: thread i takes group i of (s, t) if i < cap / 4
+    const unsigned ngrp = (unsigned)rt.cap / 4;
+    const bool mine = threadIdx.x < ngrp;
+    const uint4 *gq4 = reinterpret_cast<const uint4 *>(rt.gq);
+    const float4 *val4 = reinterpret_cast<const float4 *>(rt.val);
+    uint4 eq[kRtMaxRounds];
+    float4 ev[kRtMaxRounds];
+    auto entries = [&](auto tc) __attribute__((always_inline)) {
+        constexpr int t = decltype(tc)::value;
+        if (t >= T) return;  // uniform
+        const int64_t g = ((int64_t)s * T + t) * ngrp + (mine ? threadIdx.x : 0u);
+        eq[t] = load_stream(gq4 + g);
+        ev[t] = UNIT ? make_float4(1.f, 1.f, 1.f, 1.f) : load_stream(val4 + g);
+    };
+    // the memory pipeline is in order: what round 0 needs first, then the
+    // rest of the first rounds; rounds 4+ are issued four rounds ahead
+    issue(0, rr[0]);
+    entries(std::integral_constant<int, 0>{});
+    if (T > 1) issue(1, rr[1]);
+    entries(std::integral_constant<int, 1>{});
+    if (T > 2) issue(2, rr[2]);
+    entries(std::integral_constant<int, 2>{});
+    entries(std::integral_constant<int, 3>{});
+    // this lane's columns (as k_grad_lds): weights and column-major runs
+    float wj[NG];
+    unsigned cb[NG], ce[NG];
+    const uint16_t *cs = rt.cend + (int64_t)s * kPmSlice;
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+        const int64_t j = (gfirst + kGradWaves * gi) * 64 + lane;
+        wj[gi] = w[j < D ? j : D - 1];
+        const int c = (wv + kGradWaves * gi) * 64 + lane;
+        ce[gi] = cs[c];
+        const unsigned p = cs[c ? c - 1 : 0];
+        cb[gi] = c ? p : 0u;
+    }
+    PmPass1<NT, 4> pm;
+    if (PM) pm.bounds(pn, s);
+    DLR_STAMP(1);
+    auto products = [&](const uint4 &q, const float4 &v, const float *br, uint32_t row0) __attribute__((always_inline)) {
+        const uint32_t qq[4] = {q.x, q.y, q.z, q.w};
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+        float r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) r[u] = br[(qq[u] >> 16) - row0];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s_prod[qq[u] & 0xFFFFu] = UNIT ? r[u] : r[u] * vv[u];
+    };
+    auto round = [&](auto tc) __attribute__((always_inline)) {
+        constexpr int t = decltype(tc)::value;
+        if (t >= T) return;  // uniform
+        Rnd &x = rr[t % 3];
+        float *br = s_r + (t & 1) * kRtRows;
+        // buffer t & 1 was last read in round t - 2: every wave has passed
+        // round t - 1's barrier since
+        reinterpret_cast<v4f *>(br)[threadIdx.x] = x.r0;
+        reinterpret_cast<v4f *>(br)[NT + threadIdx.x] = x.r1;
+        lds_barrier();
+        DLR_STAMP(2 + t);
+        if (mine) products(eq[t], ev[t], br, (uint32_t)t * kRtRows);
+        if (t + 3 < T) issue(t + 3, x);
+        if constexpr (t + 4 < kRtMaxRounds) entries(std::integral_constant<int, t + 4>{});
+        // the next batch's pass-1 list, one group set per round from round 4
+        // (all at once stalls the issue of the round loads behind it)
+        if constexpr (t >= 4) {
+            if (PM) pm.fetch_one(pn, pm.c0, t - 4);
+        }
+    };
+    unroll_seq(round, std::make_integer_sequence<int, kRtMaxRounds>{});
+    if (PM) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (4 + u >= T) pm.fetch_one(pn, pm.c0, u);  // the sets the rounds did not issue
+    }
+    lds_barrier();  // every product is in s_prod
+    DLR_STAMP(10);
+    float acc[NG];
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+        acc[gi] = 0.0f;
+        if (gfirst + kGradWaves * gi >= ng) break;  // wave-uniform
+        const unsigned o = cb[gi], c = ce[gi] - cb[gi];
+        const float *sp = s_prod + o;
+        float a = 0.0f;
+        float x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = sp[u];  // o + 7 < kRtCap + kSink
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const bool take = (unsigned)u < c;
+            if (__builtin_amdgcn_ballot_w64(take) == 0) break;  // wave-uniform
+            const float tt = a + x[u];
+            a = take ? tt : a;
+        }
+        for (unsigned k = 8; __builtin_amdgcn_ballot_w64(k < c) != 0; ++k) {
+            const float xv = s_prod[min(o + k, (unsigned)(kRtCap + kSink - 1))];
+            if (k < c) a = a + xv;
+        }
+        acc[gi] = a;
+    }
+    DLR_STAMP(11);
+    if (PM) lds_barrier();  // every wave is done with s_prod: pass 1 reuses it
+    auto update = [&](auto pow2) {
+        constexpr bool P2 = decltype(pow2)::value;
+        const float rBf = P2 ? 1.0f / Bf : 0.0f;
+        const double rBd = P2 ? 1.0 / Bd : 0.0;
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) {
+            const int64_t j = (gfirst + kGradWaves * gi) * 64 + lane;
+            if (gfirst + kGradWaves * gi >= ng || j >= D) continue;
+            const float cw = C * wj[gi];
+            const float l2 = P2 ? cw * rBf : cw / Bf;
+            const float g = (float)((P2 ? (double)acc[gi] * rBd : (double)acc[gi] / Bd) + (double)l2);
+            if (FUSED) {
+                const float step = lr * g;
+                const float wn = wj[gi] - step;
+                w[j] = wn;
+                if (PM) smem[(wv + kGradWaves * gi) * 64 + lane] = wn;
+            } else {
+                gout[j] = g;
+            }
+        }
+    };
+    const int64_t Bi = (int64_t)Bd;
+    if ((Bi & (Bi - 1)) == 0)
+        update(std::true_type{});
+    else
+        update(std::false_type{});
+    if (PM) {
+        pm.stage_offsets(reinterpret_cast<uint32_t *>(smem + kPmSlice));
+        lds_barrier();
+        DLR_STAMP(12);
+        pm.store(pn, smem, reinterpret_cast<const uint32_t *>(smem + kPmSlice), pm_p);
+    }
+#ifdef DLR_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    DLR_STAMP(13);
 #endif
 }
 
@@ -2645,6 +2841,41 @@ hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const flo
             return hipErrorInvalidValue;
     }
 #undef DLR_GLP
+    return hipGetLastError();
+}
+
+hipError_t launch_grad_rt(const DevRt &rt, int64_t D, int64_t B, const float *resid, float *w, float *gout, float lr,
+                          float C, bool fused, const DevPm *next, float *p, hipStream_t s) {
+    if (D <= 0) return hipSuccess;
+    if (rt.rounds < 1 || rt.rounds > kRtMaxRounds || (next && !fused)) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)((D + kPmSlice - 1) / kPmSlice);
+    static_assert(kGradWaves * kGradNG * 64 == kPmSlice, "a gradient workgroup's columns are one slice");
+    if (next && ((int64_t)grid != next->S || next->nblk > kPmMaxBlocks)) return hipErrorInvalidValue;
+    const dim3 blk(kGradWaves * kWave);
+    const float Bf = (float)B;
+    const double Bd = (double)B;
+    const size_t lds = std::max((size_t)(kRtCap + 16 + 2 * kRtRows) * 4, (size_t)(kPmSlice + kPmMaxBlocks) * 4);
+    const bool unit = rt.val == nullptr;
+#define DLR_GRT(F, PMX, U)                                                                                     \
+    hipLaunchKernelGGL((k_grad_rt<F, PMX, U>), dim3(grid), blk, lds, s, rt, D, resid, w, gout, Bf, Bd, lr, C, \
+                       next ? *next : DevPm{}, p)
+    if (next) {
+        if (unit)
+            DLR_GRT(true, true, true);
+        else
+            DLR_GRT(true, true, false);
+    } else if (fused) {
+        if (unit)
+            DLR_GRT(true, false, true);
+        else
+            DLR_GRT(true, false, false);
+    } else {
+        if (unit)
+            DLR_GRT(false, false, true);
+        else
+            DLR_GRT(false, false, false);
+    }
+#undef DLR_GRT
     return hipGetLastError();
 }
 

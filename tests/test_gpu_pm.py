@@ -212,3 +212,31 @@ def test_pm_default_on_c2_shape():
         assert_same_weights(eng.get_weights(), w)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("rt", ["1", "0"])
+@pytest.mark.parametrize("B", [8192, 20000, 40000, 65536])
+def test_pm_row_round_gradient(monkeypatch, rt, B):
+    # the row-round gradient (k_grad_rt: 1 to 8 rounds of 8,192 rows; the
+    # pass-1 list issued by rounds 4+ or after the last of <= 3 rounds)
+    # against k_grad_lds and the oracle's sparse step: bitwise either way,
+    # fused pass 1, wrapping batches
+    monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
+    monkeypatch.setenv("DLR_PM", "1")
+    monkeypatch.setenv("DLR_GRAD_RT", rt)
+    D = 1 << 20
+    ds = dlr.Dataset.generate(70_000, D, 20, value_mode=1, seed=11, stream=1)
+    rp, col, val, lab = ds.csr()
+    w = dlr.init_weight(D)
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(w)
+        nb = eng.load_train(ds, B)
+        assert eng.train_product_margin() == 2
+        for b in range(nb + 1):  # an epoch (the last batch wraps) + the next epoch's first
+            eng.train_step(b % nb, 0.2, 1.0)
+            g = oracle.grad_csr((rp, col, val), lab, oracle.batch_rows(len(lab), B, b % nb), w)
+            oracle.server_update(w, [g], 0.2)
+        assert_same_weights(eng.get_weights(), w)
+    finally:
+        eng.close()

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Per-workgroup timeline of the C2 gradient kernel (k_grad_lds with the
-fused pass 1) from s_memrealtime stamps (100 MHz), on the bench's C2 shard
+"""Per-workgroup timeline of the C2 gradient kernel (k_grad_rt, or
+k_grad_lds with --lds; both with the fused pass 1) from s_memrealtime stamps
+(100 MHz), on the bench's C2 shard
 shape.  Loads the DLR_STAMPS build of the library (make -C dist-lr_amd
 stamps) through DLR_LIB.  Development tool, never part of the product.
 
@@ -24,6 +25,9 @@ import distlr_amd as dlr  # noqa: E402
 
 SLOTS = {0: "start", 8: "win0+fill0 out", 9: "w0 drained", 10: "pass1 ld out", 1: "ph0 go", 2: "ph0 done",
          3: "fill1 out", 4: "ph1 go", 5: "compute end", 6: "pass1 go", 7: "end"}
+# the row-round kernel (k_grad_rt, the default for product-margin batches)
+SLOTS_RT = {0: "start", 1: "issued", **{2 + t: f"round {t} go" for t in range(8)}, 10: "rounds done",
+            11: "col sums done", 12: "pass1 go", 13: "end"}
 
 
 def main():
@@ -33,7 +37,13 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--lds", action="store_true", help="time k_grad_lds (DLR_GRAD_RT=0) instead of k_grad_rt")
     a = ap.parse_args()
+    global SLOTS
+    if a.lds:
+        os.environ["DLR_GRAD_RT"] = "0"
+    else:
+        SLOTS = SLOTS_RT
     assert "stamps" in dlr.LIB_PATH, dlr.LIB_PATH
     f = dlr.lib.dlr_debug_stamp_buffer
     f.argtypes, f.restype = [C.c_void_p], C.c_int
