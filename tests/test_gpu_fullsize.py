@@ -139,7 +139,9 @@ def test_dense_c4_shape_ranks(monkeypatch, W, order):
         assert eng.load_train_dense(shards[0], B) == 3
     finally:
         eng.close()
-    for lr in ([0.2] if order == "reference" else [0.05, 0.2]):
+    # (the informational lr 0.2 run of the fused order on W = 2 only: it is
+    # the suite's longest case at W = 4)
+    for lr in ([0.2] if order == "reference" else [0.05, 0.2] if W == 2 else [0.05]):
         got = run_group(shards, D, 2, B, lr, dense=True)
         orc = oracle.run_worker(arrays, D, 2, B, lr, sparse=False)
         if order == "reference":
