@@ -583,6 +583,32 @@ int column_order(dlr_ctx *c, const dlr_dataset &ds, std::vector<int32_t> &np) {
         for (int64_t k = 0; k < top; ++k) hot += cnt[(size_t)(key[(size_t)k] & (((uint64_t)1 << 25) - 1))];
         if (2 * hot <= total) return DLR_OK;
     }
+    // The rare columns (the 60 MB tail of C3's table: each seen a few times)
+    // miss L2 in the margin's gathers whatever their order among equals; in
+    // order of FIRST OCCURRENCE (row-major, this rank's shard) instead of id,
+    // the rare columns that rows close together introduce sit on the same
+    // cache lines (DLR_RELABEL_TAIL=0: by id).
+    const char *rt = getenv("DLR_RELABEL_TAIL");
+    const int tail_mode = rt ? atoi(rt) : 2;  // 0 by id, 1 by first occurrence among equal counts, 2 by it alone
+    if (tail_mode > 0) {
+        const char *rr = getenv("DLR_RELABEL_RARE");
+        const int64_t kRare = rr ? atoll(rr) : 16;
+        // -first, reduced by max over the ranks: every rank numbers alike
+        std::vector<int64_t> first((size_t)D, -INT64_MAX);
+        const int64_t nnz = (int64_t)ds.col.size();
+        for (int64_t e = nnz - 1; e >= 0; --e) first[(size_t)ds.col[(size_t)e]] = -e;
+        if ((rc = coll_reduce_i64(c, first.data(), first.size(), true))) return rc;
+        for (auto &f : first) f = -f;
+        int64_t k0 = 0;
+        while (k0 < D && cnt[(size_t)(key[(size_t)k0] & (((uint64_t)1 << 25) - 1))] > kRare) ++k0;
+        // [k0, D): counts <= kRare, descending; within each count, by first occurrence
+        auto cid = [&](uint64_t kk) { return (int64_t)(kk & (((uint64_t)1 << 25) - 1)); };
+        std::stable_sort(key.begin() + k0, key.end(), [&](uint64_t a, uint64_t b) {
+            const int64_t ca = cnt[(size_t)cid(a)], cb = cnt[(size_t)cid(b)];
+            if (tail_mode == 1 && ca != cb) return ca > cb;
+            return first[(size_t)cid(a)] < first[(size_t)cid(b)];
+        });
+    }
     np.assign((size_t)D, 0);
     for (int64_t k = 0; k < D; ++k) np[(size_t)(key[(size_t)k] & (((uint64_t)1 << 25) - 1))] = (int32_t)k;
     return DLR_OK;

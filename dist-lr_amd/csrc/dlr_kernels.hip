@@ -2661,7 +2661,8 @@ hipError_t launch_margin_hot(const DevBatch &bt, const float *w, int64_t D, floa
     // measured on C3: 16,384 x 8 (2.01 ms), 24,576 x 8 (2.00), 4,096 x 8
     // (2.04), 2,048 x 8 (1.87), 8,192 x 4 (1.79), 4,096 x 4 (2.22).
     // DLR_MARGIN_HOT_SHAPE (A/B only): 1 = 8,192 x 8, 2 = 16,384 x 8,
-    // 3 = 24,576 x 8 (each only when D >= its hot count).
+    // 3 = 24,576 x 8, 4 = 24,576 x 16, 5 = 20,480 x 16 (each only when D >=
+    // its hot count).
     static const int shape = [] {
         const char *e = getenv("DLR_MARGIN_HOT_SHAPE");
         return e ? atoi(e) : 0;
@@ -2671,6 +2672,8 @@ hipError_t launch_margin_hot(const DevBatch &bt, const float *w, int64_t D, floa
     if (shape == 0 && D >= 16384) return launch_mh<16384, 16>(bt, w, resid, (unsigned)ncu, s);
     if (shape == 2 && D >= 16384) return launch_mh<16384, 8>(bt, w, resid, (unsigned)ncu, s);
     if (shape == 3 && D >= 24576) return launch_mh<24576, 8>(bt, w, resid, (unsigned)ncu, s);
+    if (shape == 4 && D >= 24576) return launch_mh<24576, 16>(bt, w, resid, (unsigned)ncu, s);
+    if (shape == 5 && D >= 20480) return launch_mh<20480, 16>(bt, w, resid, (unsigned)ncu, s);
     return launch_mh<kMarginHot, kMarginHotWaves>(bt, w, resid, (unsigned)ncu * 2, s);
 }
 
