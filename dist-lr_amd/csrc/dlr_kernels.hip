@@ -2656,20 +2656,24 @@ hipError_t launch_margin_hot(const DevBatch &bt, const float *w, int64_t D, floa
             n = 256;
         return n > 0 ? n : 256;
     }();
-    // 16,384 hot weights x 16 waves, one workgroup per CU, when D allows (C3
-    // margin 1.749 ms), else 8,192 x 8, two per CU (1.779 ms).  Also
+    // 24,576 (below) or 16,384 hot weights x 16 waves, one workgroup per CU,
+    // when D allows (C3 margin 1.749 ms with 16,384, round 2), else 8,192 x
+    // 8, two per CU (1.779 ms).  Also
     // measured on C3: 16,384 x 8 (2.01 ms), 24,576 x 8 (2.00), 4,096 x 8
     // (2.04), 2,048 x 8 (1.87), 8,192 x 4 (1.79), 4,096 x 4 (2.22).
     // DLR_MARGIN_HOT_SHAPE (A/B only): 1 = 8,192 x 8, 2 = 16,384 x 8,
-    // 3 = 24,576 x 8, 4 = 24,576 x 16, 5 = 20,480 x 16 (each only when D >=
-    // its hot count).
+    // 3 = 24,576 x 8, 4 = 24,576 x 16, 5 = 20,480 x 16, 6 = 16,384 x 16
+    // (each only when D >= its hot count).
     static const int shape = [] {
         const char *e = getenv("DLR_MARGIN_HOT_SHAPE");
         return e ? atoi(e) : 0;
     }();
     // (a compacted-cold-gather variant -- ballot + list of the cold entries
     // -- measured slower: 1.90 vs 1.76 ms, profiles/r02_c3_margin_ab.txt)
-    if (shape == 0 && D >= 16384) return launch_mh<16384, 16>(bt, w, resid, (unsigned)ncu, s);
+    // 24,576 x 16 (LDS: exactly 160 KiB) since the rare-column order: C3
+    // margin 1.579 vs 1.601 ms for 16,384 x 16 (profiles/r03j_bench_c3_*.json)
+    if (shape == 0 && D >= 24576) return launch_mh<24576, 16>(bt, w, resid, (unsigned)ncu, s);
+    if ((shape == 0 || shape == 6) && D >= 16384) return launch_mh<16384, 16>(bt, w, resid, (unsigned)ncu, s);
     if (shape == 2 && D >= 16384) return launch_mh<16384, 8>(bt, w, resid, (unsigned)ncu, s);
     if (shape == 3 && D >= 24576) return launch_mh<24576, 8>(bt, w, resid, (unsigned)ncu, s);
     if (shape == 4 && D >= 24576) return launch_mh<24576, 16>(bt, w, resid, (unsigned)ncu, s);
