@@ -147,3 +147,22 @@ def test_hot_margin_c3_equals_plain(monkeypatch):
         monkeypatch.setenv("DLR_MARGIN_HOT", flag)
         out.append(run_engine([ds], D, 2, 4096, 0.2).w)
     assert_same_weights(out[1], out[0])
+
+
+@pytest.mark.parametrize("W", [1, 2])
+def test_rare_column_order_is_a_renaming(monkeypatch, W):
+    # the rare columns (<= 16 entries) numbered by first occurrence
+    # (DLR_RELABEL_TAIL=2, the default), among equal counts (1) or by id (0):
+    # every numbering gives the same bits; at W = 2 the first occurrences
+    # are reduced over the ranks, so both ranks number alike (a mismatch
+    # would scramble the key-range exchange)
+    from engine_driver import run_group
+    D = 1 << 24
+    shards = [dlr.Dataset.generate_hashed(30_000, D, 39, seed=12, stream=r + 1) for r in range(W)]
+    out = {}
+    for mode in ("0", "1", "2"):
+        monkeypatch.setenv("DLR_RELABEL_TAIL", mode)
+        run = run_engine(shards, D, 2, 4096, 0.2) if W == 1 else run_group(shards, D, 2, 4096, 0.2)
+        out[mode] = run.w
+    assert_same_weights(out["1"], out["0"])
+    assert_same_weights(out["2"], out["0"])
