@@ -277,3 +277,4 @@ def test_long_phase_order_bitwise(monkeypatch, piece):
     # and the short columns stay the reference's sequential sums
     short = counts <= 4096
     assert_same_weights(got[short], g_orc[short], "short-column gradient")
+

@@ -14,17 +14,21 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CASES = [
-    ("traffic.json", "r02f_pmc_c2", "D1000000_nnz50_B65536", "lds"),
-    ("traffic_c3.json", "r02_pmc_c3", "D16777216_nnz39_B-1", "classic"),
-    ("traffic_c4.json", "r02_pmc_c4", "D4096_nnz4096_B65536", "dense"),
-    ("traffic_c5.json", "r02_pmc_c5", "D268435456_nnz10_B1024", "touched"),
+    ("traffic.json", "r02f_pmc_c2", "D1000000_nnz50_B65536", "lds", 0),
+    # round 3: the band-pipelined margin is dispatched per band; 20 step-
+    # equivalents (bench --steps 6 --warmup 2: 2 + 6 timed + 6 + 6 stage and
+    # breakdown steps)
+    ("traffic_c3.json", "r03_pmc_c3", "D16777216_nnz39_B-1", "classic", 20),
+    ("traffic_c4.json", "r02_pmc_c4", "D4096_nnz4096_B65536", "dense", 0),
+    ("traffic_c5.json", "r02_pmc_c5", "D268435456_nnz10_B1024", "touched", 0),
 ]
 
 
-@pytest.mark.parametrize("name,raw,key,layout", CASES)
-def test_traffic_reproducible_from_raw_counters(name, raw, key, layout):
+@pytest.mark.parametrize("name,raw,key,layout,steps", CASES)
+def test_traffic_reproducible_from_raw_counters(name, raw, key, layout, steps):
     out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"),
-                          os.path.join(ROOT, "profiles", raw), "--workload-key", key, "--layout", layout],
+                          os.path.join(ROOT, "profiles", raw), "--workload-key", key, "--layout", layout,
+                          "--steps", str(steps)],
                          check=True, capture_output=True, text=True).stdout
     got = json.loads(out)
     with open(os.path.join(ROOT, "profiles", name)) as f:

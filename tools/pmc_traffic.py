@@ -13,8 +13,8 @@ corrected figure.
 
     python tools/pmc_traffic.py gpurun_out/pmc  [--out profiles/traffic.json]
     python tools/pmc_traffic.py profiles/r02_pmc_c2      # the committed raw CSVs of profiles/traffic.json
-    python tools/pmc_traffic.py gpurun_out/pmc_c3 --workload-key D16777216_nnz39_B-1 --layout classic \
-        --out profiles/traffic_c3.json
+    python tools/pmc_traffic.py profiles/r03_pmc_c3 --workload-key D16777216_nnz39_B-1 --layout classic \
+        --steps 20 --out profiles/traffic_c3.json   # (bench --config c3 --steps 6 --warmup 2)
 """
 from __future__ import annotations
 
@@ -55,6 +55,9 @@ def main() -> int:
     ap.add_argument("--out", default=None)
     ap.add_argument("--workload-key", default="D1000000_nnz50_B65536")
     ap.add_argument("--layout", default="lds", help="gradient layout the passes ran with (bench.py reports it)")
+    ap.add_argument("--steps", type=int, default=0,
+                    help="step-equivalents of the bench run (default: its margin dispatches; a band-pipelined "
+                         "margin is dispatched once per band -- C3: warm-up + timed + stage-timing + breakdown steps)")
     args = ap.parse_args()
     d = args.pmc_dir
     # calibration: mb_stream reads 25 MiB and writes n4*4 bytes per launch
@@ -88,7 +91,8 @@ def main() -> int:
     roles = [("margin", ["k_margin", "k_pm_margin", "k_pm_products", "k_dense_fused", "k_dense_margin"]),
              ("grad", ["k_grad", "k_long_", "k_band_finalize", "k_dense_grad", "k_dense_combine"]),
              ("update", ["k_dense_l2", "k_scatter", "k_merge_update", "k_sparse_merge"])]
-    steps = len([x for k in ["k_margin", "k_pm_margin", "k_dense_fused", "k_dense_margin"] for x in pick(bf, k)]) or 1
+    steps = args.steps or len([x for k in ["k_margin", "k_pm_margin", "k_dense_fused", "k_dense_margin"]
+                               for x in pick(bf, k)]) or 1
     total = 0.0
     for short, keys in roles:
         f = [x for k in keys for x in pick(bf, k)]
