@@ -844,8 +844,12 @@ namespace {
 #endif
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kGradWaves = 16;  // waves per workgroup
-constexpr int kGradNG = 4;      // 64-column groups per wave
+#ifndef DLR_GRAD_WAVES  // A/B builds only (make variant VDEFS=...): 16 x 4 in the product
+#define DLR_GRAD_WAVES 16
+#define DLR_GRAD_NG 4
+#endif
+constexpr int kGradWaves = DLR_GRAD_WAVES;  // waves per workgroup
+constexpr int kGradNG = DLR_GRAD_NG;        // 64-column groups per wave
 constexpr int kBlk = 256;       // window = one phase block (<= 255 entries)
 constexpr int kBlkPad = kBlk + 8;  // product slab per wave: lane reads at o + [0, 8) never leave it
 
@@ -1115,7 +1119,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     // 1 KiB -- lane l's 16 bytes land at the wave-uniform base + 16*l.
     auto fill = [&](int64_t lo) {
 #pragma unroll
-        for (int f = 0; f < FILL; ++f) {
+        for (int f = 0; f < R / (kGradWaves * kWave * 4); ++f) {  // FILL with 16 waves
             const int o = (f * kGradWaves + wv) * kWave * 4;  // floats; this wave's 1 KiB slot
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)(resid + lo + o + lane * 4),
