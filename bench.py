@@ -434,6 +434,7 @@ def run_rank(args):
                  "tree (deterministic, within tolerance; DESIGN.md 3.1)")
     else:
         order = "reference: one chain per row (margin) and per column (gradient), lr.cc:35-40/108-112 -- bitwise"
+    row_rounds = eng.train_row_rounds() if args.kind != "dense" else 0
     margin_kind = "dense rows" if args.kind == "dense" else \
         ["gathers", "product margin (pass 1 separate)",
          "product margin (pass 1 fused into the previous step's gradient)"][eng.train_product_margin()]
@@ -607,7 +608,8 @@ def run_rank(args):
                     f"{'pinned host memory, staged per batch' if streamed else 'resident in HBM'})",
             "config": {"workload": f"{args.label}: {args.rows} rows/GPU x {D} features, {args.nnz} nnz/row, "
                                    f"batch {B}, sync SGD lr {args.lr}, C=1",
-                       "name": args.config, "gradient_layout": layout + (f"+bands({band_rows} rows)" if band_rows else ""),
+                       "name": args.config, "gradient_layout": layout + (f"+bands({band_rows} rows)" if band_rows else "") +
+                       (f" (row-round gradient k_grad_rt, {row_rounds} rounds)" if row_rounds else ""),
                        "values": "unit (all 1.0f, not stored)" if unit else "fp32",
                        "margin": margin_kind,
                        "summation_order": order,

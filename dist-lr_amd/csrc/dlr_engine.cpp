@@ -3084,6 +3084,12 @@ int dlr_train_product_margin(dlr_ctx *c) {
     return c->train.pm ? (c->train.pm_fused ? 2 : 1) : 0;
 }
 
+int dlr_train_row_rounds(dlr_ctx *c) {
+    if (!c) return DLR_E_ARG;
+    if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_row_rounds: no training shard loaded");
+    return c->train.pcsc && c->train.rt ? c->train.rt_rounds : 0;
+}
+
 int dlr_train_band_rows(dlr_ctx *c) {
     if (!c || !c->train.loaded) return 0;
     return c->train.band_shift ? 1 << c->train.band_shift : 0;

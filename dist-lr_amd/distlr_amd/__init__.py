@@ -44,7 +44,7 @@ SYMBOLS = [
     "dlr_set_weights", "dlr_get_weights", "dlr_load_train", "dlr_load_test", "dlr_load_train_dense",
     "dlr_load_test_dense", "dlr_set_residency", "dlr_train_residency",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
-    "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_train_band_rows", "dlr_train_relabeled", "dlr_train_unit_values", "dlr_train_product_margin",
+    "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_train_band_rows", "dlr_train_relabeled", "dlr_train_unit_values", "dlr_train_product_margin", "dlr_train_row_rounds",
     "dlr_set_exchange_overlap", "dlr_exchange_overlap",
     "dlr_memory_info", "dlr_stream_bytes",
 ]
@@ -160,6 +160,7 @@ _sig("dlr_train_band_rows", C.c_int, P)
 _sig("dlr_train_relabeled", C.c_int, P)
 _sig("dlr_train_unit_values", C.c_int, P)
 _sig("dlr_train_product_margin", C.c_int, P)
+_sig("dlr_train_row_rounds", C.c_int, P)
 _sig("dlr_set_exchange_overlap", C.c_int, P, C.c_int)
 _sig("dlr_exchange_overlap", C.c_int, P)
 _sig("dlr_memory_info", C.c_int, P, C.POINTER(i64), C.POINTER(i64))
@@ -578,6 +579,13 @@ class Engine:
         product margin with pass 1 fused into the previous step's gradient
         (dlr_train_product_margin)."""
         rc = lib.dlr_train_product_margin(self._h)
+        self._c(min(rc, 0))
+        return rc
+
+    def train_row_rounds(self) -> int:
+        """Rounds of the row-round gradient (k_grad_rt), 0 for k_grad_lds or
+        another layout (dlr_train_row_rounds)."""
+        rc = lib.dlr_train_row_rounds(self._h)
         self._c(min(rc, 0))
         return rc
 

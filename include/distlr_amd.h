@@ -363,6 +363,14 @@ int dlr_train_unit_values(dlr_ctx *ctx);
  * Sigmoid_ dot product for these shards (same arithmetic). */
 int dlr_train_product_margin(dlr_ctx *ctx);
 
+/* The gradient kernel of a product-margin shard: the number of 8,192-row
+ * rounds of the ROW-ROUND gradient (k_grad_rt: the batch read in pass 1's
+ * row-major order, products transposed into column order in LDS; default
+ * for batches of <= 2 rounds, DLR_GRAD_RT), or 0 for the phase-split LDS
+ * gradient (k_grad_lds) / any other layout.  Same arithmetic either way
+ * (lr.cc:35-40, bitwise). */
+int dlr_train_row_rounds(dlr_ctx *ctx);
+
 /* World > 1 with the product margin: the exchange overlapped with the next
  * batch's margin (BASELINE north_star).  The in-place all-gather of the
  * merged weights (lr.cc:122's Pull) runs in 4 pieces on a second stream --

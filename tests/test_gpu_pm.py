@@ -233,6 +233,7 @@ def test_pm_row_round_gradient(monkeypatch, rt, B):
         eng.set_weights(w)
         nb = eng.load_train(ds, B)
         assert eng.train_product_margin() == 2
+        assert eng.train_row_rounds() == ((B + 8191) // 8192 if rt == "1" else 0)
         for b in range(nb + 1):  # an epoch (the last batch wraps) + the next epoch's first
             eng.train_step(b % nb, 0.2, 1.0)
             g = oracle.grad_csr((rp, col, val), lab, oracle.batch_rows(len(lab), B, b % nb), w)
