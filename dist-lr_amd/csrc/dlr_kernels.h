@@ -78,7 +78,10 @@ struct DevPcsc {
 // entries [ptr[s], ptr[s+1]) of row/val (batch-local rows, ascending).  Wave
 // k sums pairs [wstart[k], wstart[k+1]) (<= 64 * kBandPairsPerLane pairs,
 // ~one window of entries).  row/val are padded by >= 64 entries.
-constexpr int kBandPairsPerLane = 4;
+#ifndef DLR_BAND_K  // A/B builds only (make variant VDEFS=-DDLR_BAND_K=n)
+#define DLR_BAND_K 4
+#endif
+constexpr int kBandPairsPerLane = DLR_BAND_K;
 struct DevBand {
     const uint32_t *cols;
     const uint32_t *ptr;
