@@ -430,7 +430,7 @@ def run_rank(args):
                  "blocked gradient (deterministic, within tolerance; DESIGN.md 3.2)" if blocked else
                  "reference: one chain per row (margin) and per column (gradient), lr.cc:35-40/108-112 -- bitwise")
     elif band_rows and os.environ.get("DLR_LONG_COLUMN", "1") != "0":
-        order = ("reference, except long columns (> 4,096 entries): 16,384-row phase pieces combined by a fixed "
+        order = ("reference, except long columns (> 2,048 entries): 16,384-row phase pieces combined by a fixed "
                  "tree (deterministic, within tolerance; DESIGN.md 3.1)")
     else:
         order = "reference: one chain per row (margin) and per column (gradient), lr.cc:35-40/108-112 -- bitwise"

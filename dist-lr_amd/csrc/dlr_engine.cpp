@@ -2420,12 +2420,14 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         std::vector<float> cval(t.unit ? 0 : (size_t)total);
         // Long columns (DLR_LONG_COLUMN entries in a batch; 0 = none) are
         // summed in a fixed chunked order instead of the reference's single
-        // sequential chain.  Default: 4,096 in band mode only
-        // (C3's 2^21+-row batches, ~10^6-entry chains); otherwise 2^17, far
-        // above anything a local.sh-sized shard holds (8,140 rows), so a
-        // skewed a9a-like shard (columns in > 50% of the rows) stays bitwise.
+        // sequential chain.  Default: 2,048 in band mode only
+        // (C3's 2^21+-row batches, ~10^6-entry chains; 2,048 measured best
+        // of 512..16,384 with the rare-column order, profiles/r03t_*);
+        // otherwise 2^17, far above anything a local.sh-sized shard holds
+        // (8,140 rows), so a skewed a9a-like shard (columns in > 50% of the
+        // rows) stays bitwise.
         const char *lm = getenv("DLR_LONG_COLUMN");
-        const int64_t long_min = lm ? atoll(lm) : band ? 4096 : ((int64_t)1 << 17);
+        const int64_t long_min = lm ? atoll(lm) : band ? 2048 : ((int64_t)1 << 17);
         int64_t lbytes = 0;
         auto finish_long = [&](auto &lb) -> int {
             // concatenate the batches' long columns

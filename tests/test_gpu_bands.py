@@ -23,6 +23,10 @@ from engine_driver import run_engine
 from test_gpu_layouts import _c3_shards, _csr_shard
 from test_gpu_parity import assert_same_weights, compare_runs, oracle_shard
 
+# band mode's default long-column threshold (dlr_engine.cpp, DLR_LONG_COLUMN):
+# columns with more entries than this are summed in phases / pieces
+BAND_LONG_COLUMN = 2048
+
 pytestmark = pytest.mark.gpu
 
 
@@ -160,7 +164,7 @@ def test_c3_banded_pushed_gradient(monkeypatch):
     D = 1 << 24
     ds = _c3_shards(1, rows=60_000)[0]
     rp, col, val, lab = ds.csr()
-    hot = np.bincount(col, minlength=D) > 4096
+    hot = np.bincount(col, minlength=D) > BAND_LONG_COLUMN
     assert hot.sum() >= 30
     w0 = dlr.init_weight(D)
     out = {}
@@ -252,7 +256,7 @@ def test_long_phase_order_bitwise(monkeypatch, piece):
     rp, col, val, lab = ds.csr()
     N = len(lab)
     counts = np.bincount(col, minlength=D)
-    long_cols = np.flatnonzero(counts > 4096)
+    long_cols = np.flatnonzero(counts > BAND_LONG_COLUMN)
     assert len(long_cols) >= 30
     w0 = dlr.init_weight(D)
     eng = dlr.Engine(D)
@@ -275,6 +279,6 @@ def test_long_phase_order_bitwise(monkeypatch, piece):
     bad = [j for j in long_cols if np.float32(got[j]).tobytes() != want[j].tobytes()]
     assert not bad, f"{len(bad)} long columns off the documented order, e.g. {bad[:3]}"
     # and the short columns stay the reference's sequential sums
-    short = counts <= 4096
+    short = counts <= BAND_LONG_COLUMN
     assert_same_weights(got[short], g_orc[short], "short-column gradient")
 

@@ -1,7 +1,7 @@
 """BASELINE C3 at its real per-GPU size: a 12.5M-row
 Criteo-shaped shard (2^24 hashed features, 39 Zipf fields, unit values),
 B = -1 (the full shard per step, as local.sh), the DEFAULT engine choices:
-frequency relabeling, 2^20-row bands, long columns (> 4,096 entries) in
+frequency relabeling, 2^20-row bands, long columns (> 2,048 entries) in
 16,384-row phases combined by a fixed tree, hot weights in LDS for the
 margin.  Two steps against the oracle (lr.cc:35-40 + main.cc:70-72).
 
@@ -29,6 +29,7 @@ import pytest
 
 import distlr_amd as dlr
 import oracle
+from test_gpu_bands import BAND_LONG_COLUMN
 from test_gpu_parity import assert_same_weights
 
 pytestmark = pytest.mark.gpu
@@ -71,7 +72,7 @@ def test_c3_full_size_two_steps(c3_shard, init):
     if init == "centred":
         w0 = ((w0 - np.float32(0.5)) / np.float32(5.0)).astype(np.float32)
     counts = np.bincount(csr[1], minlength=D)
-    long_cols = counts > 4096
+    long_cols = counts > BAND_LONG_COLUMN
     assert long_cols.sum() > 100 and counts.max() > 500_000      # the ~10^6-entry chains are there
     eng = dlr.Engine(D)
     try:

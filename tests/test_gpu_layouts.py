@@ -179,8 +179,8 @@ def test_c3_hot_columns_bitwise_without_chunking(monkeypatch):
 
 @pytest.mark.parametrize("W", [1, 2])
 def test_c3_long_column_chunking_within_tolerance(W, monkeypatch):
-    # columns with > 4,096 entries summed in chunks (the band-mode default
-    # threshold, forced here without bands)
+    # columns with > 4,096 entries summed in chunks (forced here without
+    # bands; the band-mode default threshold is 2,048)
     # (deterministic); weights stay within the north-star bar of the
     # reference's single sequential sum: |a-b| <= 1e-5*|b| + 1e-7
     monkeypatch.setenv("DLR_LONG_COLUMN", "4096")
