@@ -82,14 +82,14 @@ CONFIGS = {
 # this process touches the GPU.
 CONFIGS["c1e2e"] = dict(rows=8140, features=123, nnz=14, batch=-1, value_mode=0, steps=100, warmup=1,
                         label="C1 local.sh job end to end (bin/distlr)", kind="e2e")
-# The reference summation orders at C3 / C4 scale: the
-# same workloads with every column of the gradient summed as ONE chain in
-# batch-row order and every margin as one chain in column order (lr.cc:35-40,
-# 108-112) -- bitwise the oracle -- instead of the deterministic reordered
-# sums the defaults use for ~10^5-10^6-add chains.
-CONFIGS["c3x"] = dict(CONFIGS["c3"], label="C3 Criteo-shaped hashed LR, reference summation order",
-                      env={"DLR_LONG_COLUMN": "0"})
-CONFIGS["c4x"] = dict(CONFIGS["c4"], label="C4 dense LR, reference summation order", env={"DLR_DENSE_GRAD": "seq"})
+# Every config runs in the engine's default, REFERENCE summation order
+# (dlr_set_summation_order: every margin one chain in column order, every
+# gradient column one chain in batch-row order, lr.cc:35-40/108-112 --
+# bitwise the oracle).  c3f / c4f: the same workloads in the opt-in FAST
+# order (deterministic reordered sums for the ~10^5-10^6-add chains,
+# DESIGN.md 3), for the price of the reference order.
+CONFIGS["c3f"] = dict(CONFIGS["c3"], label="C3 Criteo-shaped hashed LR, FAST summation order", order="fast")
+CONFIGS["c4f"] = dict(CONFIGS["c4"], label="C4 dense LR, FAST summation order (fused blocked pass)", order="fast")
 PCIE_PEAK_GBS = 63.0  # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s (spec)
 
 
@@ -138,6 +138,7 @@ def parse_args():
     args.kind = cfg.get("kind", "uniform")
     args.residency = cfg.get("residency", "auto")
     args.env = cfg.get("env", {})
+    args.order = cfg.get("order", "reference")
     return args
 
 
@@ -389,7 +390,7 @@ def run_rank(args):
         if distributed:
             dist.destroy_process_group()
         return
-    os.environ.update(args.env)  # the engine reads its order switches at load
+    os.environ.update(args.env)
     D, B = args.features, args.batch
     mode = {"mean": dlr.MODE_SYNC_MEAN, "last": dlr.MODE_SYNC_LAST, "async": dlr.MODE_ASYNC}[args.mode]
 
@@ -407,6 +408,7 @@ def run_rank(args):
         nnz_avg = ds.info()[1] / max(1, args.rows)    # hashed rows lose a few duplicate fields
     t_gen = time.perf_counter() - t_setup
     eng = dlr.Engine(D, device=local, rank=rank, world=world, unique_id=uid)
+    eng.set_summation_order(dlr.ORDER_FAST if args.order == "fast" else dlr.ORDER_REFERENCE)
     eng.set_weights(dlr.init_weight(D))
     if args.residency != "auto":
         eng.set_residency({"device": dlr.RESIDENCY_DEVICE, "stream": dlr.RESIDENCY_STREAM}[args.residency])
@@ -419,21 +421,16 @@ def run_rank(args):
     layout = "dense" if args.kind == "dense" else \
         {dlr.LAYOUT_CLASSIC: "classic", dlr.LAYOUT_LDS: "lds", dlr.LAYOUT_TOUCHED: "touched"}[eng.train_layout()]
     band_rows = eng.train_band_rows() if args.kind != "dense" else 0
-    # which summation order the numbers below are for
-    if args.kind == "dense":
-        dg = os.environ.get("DLR_DENSE_GRAD", "")
-        big = B * D > (1 << 24)
-        fused = dg == "fused" or (not dg and big and D in (512, 1024, 2048, 4096))
-        blocked = fused or dg == "blocked" or (not dg and big)
-        order = ("blocked (deterministic, within tolerance): margins as 64 lane partials + butterfly, gradient per "
-                 "256-row chunk + chunk order (DESIGN.md 3.3)" if fused else
-                 "blocked gradient (deterministic, within tolerance; DESIGN.md 3.2)" if blocked else
-                 "reference: one chain per row (margin) and per column (gradient), lr.cc:35-40/108-112 -- bitwise")
-    elif band_rows and os.environ.get("DLR_LONG_COLUMN", "1") != "0":
-        order = ("reference, except long columns (> 2,048 entries): 16,384-row phase pieces combined by a fixed "
-                 "tree (deterministic, within tolerance; DESIGN.md 3.1)")
-    else:
+    # which summation order the numbers below are for: what
+    # the loaded shard's kernels actually use (dlr_summation_order)
+    if eng.summation_order() == dlr.ORDER_REFERENCE:
         order = "reference: one chain per row (margin) and per column (gradient), lr.cc:35-40/108-112 -- bitwise"
+    elif args.kind == "dense":
+        order = ("FAST (opt-in): margins as 64 lane partials + butterfly, gradient per 256-row chunk + chunk "
+                 "order (deterministic; DESIGN.md 3.3)")
+    else:
+        order = ("FAST (opt-in): reference except long columns (> 2,048 entries): 16,384-row phase pieces "
+                 "combined by a fixed tree (deterministic; DESIGN.md 3.1)")
     row_rounds = eng.train_row_rounds() if args.kind != "dense" else 0
     margin_kind = "dense rows" if args.kind == "dense" else \
         ["gathers", "product margin (pass 1 separate)",

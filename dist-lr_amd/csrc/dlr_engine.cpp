@@ -191,6 +191,14 @@ struct TrainShard {
     uint32_t *lpptr = nullptr, *lpslot = nullptr, *lpws = nullptr;
     uint16_t *lprow = nullptr;
     float *lpval = nullptr;
+    // some sum of this shard is reordered (DLR_ORDER_FAST actually applied:
+    // long columns, blocked / fused dense gradients); dlr_summation_order
+    bool fast = false;
+    // world > 1: the pieced all-gather overlapped with the next batch's pass 1
+    // (exchange_overlapped), AGREED over the ranks at load / by the
+    // collective dlr_set_exchange_overlap -- the two forms are different
+    // collective sequences
+    bool xpieced = false;
     int64_t bytes = 0;
 };
 
@@ -235,9 +243,12 @@ struct dlr_ctx {
     double *h_ll = nullptr;                   // pinned
     TrainShard train;
     TestShard test;
-    // exchange / next-margin overlap (TrainShard::xslices): on unless
-    // dlr_set_exchange_overlap(0); its stream and events
+    // exchange / next-margin overlap (TrainShard::xslices): asked for unless
+    // dlr_set_exchange_overlap(0) (the loaded shard's agreed form:
+    // TrainShard::xpieced); its stream and events
     bool xoverlap = true;
+    // summation order of the next loaded training shard (DLR_ORDER_*)
+    int order = DLR_ORDER_REFERENCE;
     hipStream_t xstream = nullptr;
     hipEvent_t ev_xmerged = nullptr;
     hipEvent_t ev_xpiece[kXPieces] = {};
@@ -534,6 +545,31 @@ int coll_agree_load(dlr_ctx *c, const char *who, int local_rc, const std::string
     return DLR_OK;
 }
 
+// Every rank must load with the same summation order (dlr_set_summation_order):
+// a rank summing differently would hold different weights after the merge.
+int coll_agree_order(dlr_ctx *c, const char *who) {
+    int64_t v[2] = {c->order, -(int64_t)c->order};
+    int rc = coll_reduce_i64(c, v, 2, true);
+    if (rc) return rc;
+    if (v[0] != -v[1])
+        return fail(c, DLR_E_ARG, std::string(who) + ": the ranks asked for different summation orders");
+    return DLR_OK;
+}
+
+// The pieced all-gather (exchange_overlapped) only where EVERY rank can and
+// wants to run it: its RCCL send/recv groups and the plain all-gather's
+// ncclAllGather would not pair up.  Collective.
+int coll_agree_pieced(dlr_ctx *c) {
+    TrainShard &t = c->train;
+    t.xpieced = false;
+    if (!c->comm) return DLR_OK;
+    int64_t v = (t.pm && c->xoverlap && !t.sparse_stream) ? -1 : 0;  // max(-x) = -min(x)
+    int rc = coll_max_i64(c, &v);
+    if (rc) return rc;
+    t.xpieced = v == -1;
+    return DLR_OK;
+}
+
 inline int64_t pid(const std::vector<int32_t> &p, int64_t j) { return p.empty() ? j : (int64_t)p[(size_t)j]; }
 
 // Frequency order of the columns of a sparse training shard, summed over
@@ -601,6 +637,10 @@ int column_order(dlr_ctx *c, const dlr_dataset &ds, std::vector<int32_t> &np) {
         for (auto &f : first) f = -f;
         int64_t k0 = 0;
         while (k0 < D && cnt[(size_t)(key[(size_t)k0] & (((uint64_t)1 << 25) - 1))] > kRare) ++k0;
+        // the hot-weight margin stages ids [0, kMarginHot) in LDS as the
+        // hottest: keep them in count order even on a shard with few
+        // columns above kRare
+        k0 = std::max<int64_t>(k0, std::min<int64_t>(D, dlr::kMarginHot));
         // [k0, D): counts <= kRare, descending; within each count, by first occurrence
         auto cid = [&](uint64_t kk) { return (int64_t)(kk & (((uint64_t)1 << 25) - 1)); };
         std::stable_sort(key.begin() + k0, key.end(), [&](uint64_t a, uint64_t b) {
@@ -2007,7 +2047,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             msg = "dlr_load_train: empty shard (reference never terminates)";
         const int64_t nb = msg.empty() ? dlr_num_batches(ds->n_rows, batch_size) : 0;
         int rc = coll_agree_load(c, "dlr_load_train", msg.empty() ? DLR_OK : DLR_E_ARG, msg, nb);
-        if (rc) return rc;
+        if (rc || (rc = coll_agree_order(c, "dlr_load_train"))) return rc;
     }
     HIPC(c, hipStreamSynchronize(c->stream));
     free_train(c);
@@ -2252,22 +2292,35 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             for_batches(nb, nthreads, [&](int64_t b) {
                 if (ok && !pm_batch(src, t.plan[(size_t)b], D, t.unit, want_rt, pm[(size_t)b])) ok = false;
             });
+            bool rt_fits = want_rt;
             if (ok) {
                 // only where it leaves the headroom the residency choice keeps
-                // (8 GiB): else the gather margin, which needs no extra arrays
-                int64_t need = 0;
-                for (const PmBatch &q : pm)
+                // (8 GiB): else the gather margin, which needs no extra arrays.
+                // The row-round arrays are optional (k_grad_lds needs none of
+                // them): they are counted separately and dropped if only they
+                // do not fit.
+                int64_t need = 0, need_rt = 0;
+                for (const PmBatch &q : pm) {
                     need += (int64_t)(q.list.size() * 4 + q.val.size() * 4 + q.pofs.size() * 4 + q.rg.size() * 8 +
-                                      q.qs.size() * 2 + q.lbeg.size() * 4 + q.gq.size() * 4 + q.rval.size() * 4 +
-                                      q.cend.size() * 2);
+                                      q.qs.size() * 2 + q.lbeg.size() * 4);
+                    need_rt += (int64_t)(q.gq.size() * 4 + q.rval.size() * 4 + q.cend.size() * 2);
+                }
                 size_t fr = 0, tot = 0;
                 HIPC(c, hipMemGetInfo(&fr, &tot));
-                if ((double)need + (double)((size_t)8 << 30) > (double)fr) {
+                const double head = (double)((size_t)8 << 30);
+                if ((double)need + head > (double)fr) {
                     ok = false;
                     if (pme && strcmp(pme, "1") == 0)
                         return fail(c, DLR_E_NOMEM, "dlr_load_train: DLR_PM=1 but the product margin's arrays (" +
                                                         std::to_string((long long)(need >> 20)) + " MiB) do not fit");
                 }
+                rt_fits = rt_fits && (double)(need + need_rt) + head <= (double)fr;
+                if (!rt_fits)
+                    for (PmBatch &q : pm) {
+                        std::vector<uint32_t>().swap(q.gq);
+                        std::vector<float>().swap(q.rval);
+                        std::vector<uint16_t>().swap(q.cend);
+                    }
             }
             if (ok) {
                 t.pmS = S;
@@ -2313,7 +2366,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 if ((rc = cat_upload(&PmBatch::rg, &t.pm_rg, t.pmo_rg, 1, 0))) return rc;
                 if ((rc = cat_upload(&PmBatch::qoff, &t.pm_qoff, t.pmo_rg, 1, 0))) return rc;
                 if ((rc = cat_upload(&PmBatch::qs, &t.pm_qs, t.pmo_qs, 1, 8))) return rc;
-                bool rt_all = want_rt;
+                bool rt_all = rt_fits;
                 for (const PmBatch &q : pm) rt_all = rt_all && !q.gq.empty();
                 if (rt_all) {
                     std::vector<int64_t> ceoff((size_t)nb + 1);
@@ -2331,6 +2384,12 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                     t.rt_rounds = (int)((t.B + dlr::kRtRows - 1) / dlr::kRtRows);
                     resid_need = std::max(resid_need, (int64_t)t.rt_rounds * dlr::kRtRows);
                     csc_bytes += (int64_t)(t.rtoff.back() * (t.unit ? 4 : 8) + ceoff.back() * 2);
+                } else {
+                    for (PmBatch &q : pm) {  // release the unused row-round host arrays now
+                        std::vector<uint32_t>().swap(q.gq);
+                        std::vector<float>().swap(q.rval);
+                        std::vector<uint16_t>().swap(q.cend);
+                    }
                 }
                 if ((rc = dev_alloc(c, (void **)&t.pm_p, (size_t)(pcap + 64) * 4))) return rc;
                 HIPC(c, hipMemsetAsync(t.pm_p, 0, (size_t)(pcap + 64) * 4, c->stream));
@@ -2418,16 +2477,16 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         if (total >= (int64_t)1 << 31) return fail(c, DLR_E_ARG, "dlr_load_train: a batch has >= 2^31 entries");
         std::vector<uint32_t> cptr((size_t)nb * (size_t)(D + 1));
         std::vector<float> cval(t.unit ? 0 : (size_t)total);
-        // Long columns (DLR_LONG_COLUMN entries in a batch; 0 = none) are
-        // summed in a fixed chunked order instead of the reference's single
-        // sequential chain.  Default: 2,048 in band mode only
-        // (C3's 2^21+-row batches, ~10^6-entry chains; 2,048 measured best
-        // of 512..16,384 with the rare-column order, profiles/r03t_*);
-        // otherwise 2^17, far above anything a local.sh-sized shard holds
-        // (8,140 rows), so a skewed a9a-like shard (columns in > 50% of the
-        // rows) stays bitwise.
+        // Long columns (more than long_min entries in a batch; 0 = none):
+        // only under DLR_ORDER_FAST are they summed in a fixed chunked /
+        // phase order instead of the reference's single sequential chain
+        // (DESIGN.md 3).  FAST's threshold: 2,048 in band mode (C3's
+        // 2^21+-row batches, ~10^6-entry chains; 2,048 measured best of
+        // 512..16,384, profiles/r03t_*), otherwise 2^17; DLR_LONG_COLUMN
+        // overrides the FAST threshold (A/B) and never changes the
+        // reference order.
         const char *lm = getenv("DLR_LONG_COLUMN");
-        const int64_t long_min = lm ? atoll(lm) : band ? 2048 : ((int64_t)1 << 17);
+        const int64_t long_min = c->order != DLR_ORDER_FAST ? 0 : lm ? atoll(lm) : band ? 2048 : ((int64_t)1 << 17);
         int64_t lbytes = 0;
         auto finish_long = [&](auto &lb) -> int {
             // concatenate the batches' long columns
@@ -2611,6 +2670,8 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
     // streamed: the slots (counted by place()); resident: the shard arrays
     if (!t.sparse_stream)
         t.bytes = (int64_t)((t.n_rows + 1) * 8 + (t.nnz + kPad) * (t.unit ? 4 : 8) + t.n_rows * 4) + csc_bytes;
+    t.fast = t.any_long;  // only long columns reorder a sparse sum (DLR_ORDER_FAST)
+    if ((rc = coll_agree_pieced(c))) return rc;
     t.loaded = true;
     if (n_batches) *n_batches = nb;
     return DLR_OK;
@@ -2663,7 +2724,7 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
             msg = "dlr_load_train_dense: empty shard (reference never terminates)";
         const int64_t nb = msg.empty() ? dlr_num_batches(ds->n_rows, batch_size) : 0;
         int rc = coll_agree_load(c, "dlr_load_train_dense", msg.empty() ? DLR_OK : DLR_E_ARG, msg, nb);
-        if (rc) return rc;
+        if (rc || (rc = coll_agree_order(c, "dlr_load_train_dense"))) return rc;
     }
     HIPC(c, hipStreamSynchronize(c->stream));
     free_train(c);
@@ -2676,16 +2737,20 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
     t.B = batch_size < 0 ? ds->n_rows : batch_size;
     t.plan = dlr::plan_batches(ds->n_rows, batch_size);
     const int64_t D = c->D;
-    // Gradient order: the reference's per-column sequential
-    // sums (seq) for small batches; for batch rows x D > 2^24 the fused
-    // one-pass kernel where D allows (C4), else the two-pass blocked sums.
-    // DLR_DENSE_GRAD=seq|blocked|fused forces one.
-    const char *dg = getenv("DLR_DENSE_GRAD");
+    // Summation order (dlr_set_summation_order): REFERENCE --
+    // the row chains and column chains of lr.cc:108-112 / 35-39 (banded for
+    // large batches, launch_dense_step); FAST -- for batch rows x D > 2^24
+    // the fused one-pass kernel where D allows (C4), else the two-pass
+    // blocked sums (DLR_DENSE_GRAD=blocked|fused picks a FAST variant).
+    const char *dg = c->order == DLR_ORDER_FAST ? getenv("DLR_DENSE_GRAD") : nullptr;
     const bool big = t.B * D > ((int64_t)1 << 24);
-    t.dfused = dg ? strcmp(dg, "fused") == 0 : (big && dlr::dense_fused_ok(D));
-    if (t.dfused && !dlr::dense_fused_ok(D))
-        return fail(c, DLR_E_ARG, "dlr_load_train_dense: DLR_DENSE_GRAD=fused needs D in {512, 1024, 2048, 4096}");
-    t.dblocked = t.dfused || (dg ? strcmp(dg, "blocked") == 0 : big);
+    if (c->order == DLR_ORDER_FAST) {
+        t.dfused = dg ? strcmp(dg, "fused") == 0 : (big && dlr::dense_fused_ok(D));
+        if (t.dfused && !dlr::dense_fused_ok(D))
+            return fail(c, DLR_E_ARG, "dlr_load_train_dense: DLR_DENSE_GRAD=fused needs D in {512, 1024, 2048, 4096}");
+        t.dblocked = t.dfused || (dg ? strcmp(dg, "blocked") == 0 : big);
+    }
+    t.fast = t.dblocked;
     // Residency: device-resident unless asked to stream, or (auto) the rows
     // would not leave room in HBM (20M x 4096 fp32 = 328 GB
     // on one 288 GB GPU).  Streamed rows are staged per batch over PCIe.
@@ -2861,7 +2926,7 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
         HIPC(c, dlr::launch_merge_update(c->recv, c->world, c->chunk, ke - kb, c->w + kb, lr, mode, c->stream));
         time_end(c, 2, t0);
         time_begin(c, &t0);
-        if (c->train.pm && c->xoverlap && !c->train.sparse_stream) {
+        if (c->train.xpieced) {
             // (the exchange interval then includes the next batch's pass 1)
             int rc = exchange_overlapped(c, b);
             if (rc) return rc;
@@ -3109,12 +3174,28 @@ int dlr_set_exchange_overlap(dlr_ctx *c, int on) {
     HIPC(c, hipStreamSynchronize(c->stream));
     c->xoverlap = on != 0;
     c->pm_ready = -1;  // products formed under the other setting are not assumed
+    // with a shard loaded the ranks re-agree now (collective): every rank's
+    // next step must issue the same collectives
+    if (c->train.loaded) return coll_agree_pieced(c);
     return DLR_OK;
 }
 
 int dlr_exchange_overlap(dlr_ctx *c) {
     if (!c) return DLR_E_ARG;
-    return c->comm && c->train.loaded && c->train.pm && c->xoverlap && !c->train.sparse_stream ? 1 : 0;
+    return c->comm && c->train.loaded && c->train.xpieced ? 1 : 0;
+}
+
+int dlr_set_summation_order(dlr_ctx *c, int order) {
+    if (!c || (order != DLR_ORDER_REFERENCE && order != DLR_ORDER_FAST))
+        return fail(c, DLR_E_ARG, "dlr_set_summation_order: bad order");
+    c->order = order;
+    return DLR_OK;
+}
+
+int dlr_summation_order(dlr_ctx *c) {
+    if (!c) return DLR_E_ARG;
+    if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_summation_order: no training shard loaded");
+    return c->train.fast ? DLR_ORDER_FAST : DLR_ORDER_REFERENCE;
 }
 
 int dlr_memory_info(dlr_ctx *c, int64_t *train_bytes, int64_t *test_bytes) {

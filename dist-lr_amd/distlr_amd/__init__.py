@@ -28,6 +28,7 @@ LAYOUT_CLASSIC, LAYOUT_LDS, LAYOUT_TOUCHED = 0, 1, 2
 RESIDENCY_AUTO, RESIDENCY_DEVICE, RESIDENCY_STREAM = 0, 1, 2
 STAGE_MARGIN, STAGE_GRADIENT, STAGE_UPDATE = 0, 1, 2
 TRANSPORT_NONE, TRANSPORT_RCCL, TRANSPORT_LOOPBACK = 0, 1, 2
+ORDER_REFERENCE, ORDER_FAST = 0, 1
 
 # Exported symbols, in include/distlr_amd.h order (tests check the .so
 # exports every one of them).
@@ -42,7 +43,8 @@ SYMBOLS = [
     "dlr_init_weight", "dlr_format_model", "dlr_key_range",
     "dlr_get_unique_id", "dlr_create", "dlr_create_group", "dlr_comm_abort", "dlr_comm_info", "dlr_destroy", "dlr_last_error",
     "dlr_set_weights", "dlr_get_weights", "dlr_load_train", "dlr_load_test", "dlr_load_train_dense",
-    "dlr_load_test_dense", "dlr_set_residency", "dlr_train_residency",
+    "dlr_load_test_dense", "dlr_set_residency", "dlr_train_residency", "dlr_set_summation_order",
+    "dlr_summation_order",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
     "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_train_band_rows", "dlr_train_relabeled", "dlr_train_unit_values", "dlr_train_product_margin", "dlr_train_row_rounds",
     "dlr_set_exchange_overlap", "dlr_exchange_overlap",
@@ -124,6 +126,8 @@ _sig("dlr_load_train_dense", C.c_int, P, P, i64, C.POINTER(i64))
 _sig("dlr_load_test_dense", C.c_int, P, P)
 _sig("dlr_set_residency", C.c_int, P, C.c_int)
 _sig("dlr_train_residency", C.c_int, P)
+_sig("dlr_set_summation_order", C.c_int, P, C.c_int)
+_sig("dlr_summation_order", C.c_int, P)
 _sig("dlr_dataset_write_libsvm", C.c_int, P, C.c_char_p, C.c_int)
 _sig("dlr_dataset_save_binary", C.c_int, P, C.c_char_p)
 _sig("dlr_dataset_load_binary", C.c_int, C.c_char_p, C.POINTER(P))
@@ -501,6 +505,20 @@ class Engine:
 
     def train_residency(self) -> int:
         rc = lib.dlr_train_residency(self._h)
+        self._c(min(rc, 0))
+        return rc
+
+    def set_summation_order(self, order: int) -> None:
+        """ORDER_REFERENCE (default: every sum in lr.cc's order, bitwise the
+        reference's arithmetic) or ORDER_FAST (deterministic reordered long
+        sums, within tolerance) for the next loaded training shard
+        (dlr_set_summation_order)."""
+        self._c(lib.dlr_set_summation_order(self._h, order))
+
+    def summation_order(self) -> int:
+        """The loaded training shard's order: ORDER_FAST only if some sum of
+        it is actually reordered (dlr_summation_order)."""
+        rc = lib.dlr_summation_order(self._h)
         self._c(min(rc, 0))
         return rc
 

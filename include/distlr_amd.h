@@ -232,14 +232,15 @@ int dlr_load_train(dlr_ctx *ctx, const dlr_dataset *ds, int64_t batch_size, int6
 /* Test shard (LR::Test's NextBatch(-1), lr.cc:49). */
 int dlr_load_test(dlr_ctx *ctx, const dlr_dataset *ds);
 /* The dense counterparts (K6: GEMV-shaped margin and gradient kernels,
- * HBM-bound, off MFMA).  The gradient is the reference's per-column
- * sequential sum when batch rows x D <= 2^24; above that, for D in {512,
- * 1024, 2048, 4096} (C4), one FUSED pass over X (margin + per-256-row-chunk
- * gradient partials from LDS, X read from HBM once; the margin summed in a
- * fixed blocked order), else two passes with the blocked gradient
- * (per-column sequential over 256-row chunks, chunk partials added in
- * order).  Deterministic, within the north-star tolerance;
- * DLR_DENSE_GRAD=seq|blocked|fused forces one. */
+ * HBM-bound, off MFMA).  Summation order (dlr_set_summation_order): under
+ * DLR_ORDER_REFERENCE (default) every margin is lr.cc:108-112's row chain
+ * and every gradient lr.cc:35-39's column chain -- for large batches (C4) as
+ * one banded launch that runs the row chains of one band of rows beside the
+ * column chains of the bands before it; under DLR_ORDER_FAST, for batch
+ * rows x D > 2^24, one FUSED pass over X (D in {512, 1024, 2048, 4096}: the
+ * margin in a fixed blocked order, per-256-row-chunk gradient partials) or
+ * two passes with the blocked gradient (DLR_DENSE_GRAD=blocked|fused picks
+ * among these FAST variants only). */
 int dlr_load_train_dense(dlr_ctx *ctx, const dlr_dense *ds, int64_t batch_size, int64_t *n_batches);
 int dlr_load_test_dense(dlr_ctx *ctx, const dlr_dense *ds);
 
@@ -261,6 +262,29 @@ int dlr_load_test_dense(dlr_ctx *ctx, const dlr_dense *ds);
 #define DLR_RESIDENCY_STREAM 2
 int dlr_set_residency(dlr_ctx *ctx, int mode);
 int dlr_train_residency(dlr_ctx *ctx);
+
+/* Summation order of the next training shard's sums (applies at the next
+ * dlr_load_train / dlr_load_train_dense; every rank must ask for the same
+ * order, else the load fails on every rank).
+ *   DLR_ORDER_REFERENCE (default): every margin is summed in column order
+ *     (lr.cc:108-112) and every gradient column in batch-row order
+ *     (lr.cc:35-39) -- results bitwise those of the reference's arithmetic
+ *     (the oracle), on every layout and at every size.
+ *   DLR_ORDER_FAST: where the reference order is a serial chain of 10^5 -
+ *     10^6 dependent adds (C3's Zipf-hot columns in full-shard batches, C4's
+ *     65,536-row column sums), a fixed reordering: long sparse columns
+ *     summed in row-phase pieces combined by a fixed tree (DLR_LONG_COLUMN
+ *     sets the entry threshold), dense gradients by 256-row chunks (and, in
+ *     the fused dense pass, each margin by 64 lane partials combined by a
+ *     butterfly).  Deterministic; within the north-star tolerance (DESIGN.md
+ *     §3 states what each option measured).
+ * dlr_summation_order reports what the LOADED shard's kernels use:
+ * DLR_ORDER_FAST only if some sum of it is actually reordered (e.g. a FAST
+ * request on a shard with no long column is still the reference order). */
+#define DLR_ORDER_REFERENCE 0
+#define DLR_ORDER_FAST 1
+int dlr_set_summation_order(dlr_ctx *ctx, int order);
+int dlr_summation_order(dlr_ctx *ctx);
 
 /* One step of LR::Train's loop body (lr.cc:30-43) plus the server update
  * (main.cc:57-84) for batch `batch` of the loaded shard: margin + sigmoid +
@@ -329,9 +353,10 @@ int dlr_train_layout(dlr_ctx *ctx);
  * same sums as without bands (each column's running sum continues from band
  * to band in batch-row order).  DLR_BAND_ROWS=<rows> (a power of two; 0 =
  * off) overrides the default of 2^20 rows for batches of >= 2^21 rows.
- * In band mode the long columns (DLR_LONG_COLUMN) are summed per row phase
- * of 16,384 rows and the phase partials combined by a fixed tree
- * (deterministic; within 1e-5 of the single sequential sum). */
+ * Under DLR_ORDER_FAST the long columns of a band-mode batch are summed per
+ * row phase of 16,384 rows and the phase partials combined by a fixed tree
+ * (deterministic; within 1e-5 of the single sequential sum); under
+ * DLR_ORDER_REFERENCE every column is one chain in batch-row order. */
 int dlr_train_band_rows(dlr_ctx *ctx);
 
 /* 1 when the loaded sparse training shard's columns are relabeled in
@@ -380,7 +405,11 @@ int dlr_train_row_rounds(dlr_ctx *ctx);
  * own key range right after the merge).  The step's results are unchanged
  * (the same products; tests/test_gpu_pm.py).  On by default;
  * dlr_set_exchange_overlap(ctx, 0) uses the plain all-gather and forms the
- * products at the next margin.  dlr_exchange_overlap reports 1 when the
+ * products at the next margin.  The ranks AGREE on it (the two forms are
+ * different collective sequences): at load, the pieced form is used only if
+ * every rank has the product margin and asks for it; called with a shard
+ * loaded, dlr_set_exchange_overlap is collective (every rank calls it at the
+ * same point of its step sequence).  dlr_exchange_overlap reports 1 when the
  * loaded shard's steps use it. */
 int dlr_set_exchange_overlap(dlr_ctx *ctx, int on);
 int dlr_exchange_overlap(dlr_ctx *ctx);

@@ -27,9 +27,11 @@ class EngineRun:
 
 def run_engine(shards: Sequence[dlr.Dataset], D: int, num_iteration: int, batch_size: int, learning_rate: float,
                test: Optional[dlr.Dataset] = None, test_interval: int = 10, mode: int = dlr.MODE_SYNC_MEAN,
-               C_: float = 1.0, random_state: int = 0, dense: bool = False) -> EngineRun:
+               C_: float = 1.0, random_state: int = 0, dense: bool = False,
+               order: int = dlr.ORDER_REFERENCE) -> EngineRun:
     """dense=True: the shards go through the dense path (K6, DataIter's own
-    N x D layout) instead of the sparse one."""
+    N x D layout) instead of the sparse one.  order: the engines' summation
+    order (dlr_set_summation_order; the product default is the reference's)."""
     W = len(shards)
     w0 = dlr.init_weight(D, random_state)
     if dense:
@@ -46,6 +48,7 @@ def run_engine(shards: Sequence[dlr.Dataset], D: int, num_iteration: int, batch_
     if W == 1:
         eng = dlr.Engine(D)
         try:
+            eng.set_summation_order(order)
             eng.set_weights(w0)
             nb = load_train(eng, shards[0])
             if test is not None:
@@ -70,6 +73,8 @@ def run_engine(shards: Sequence[dlr.Dataset], D: int, num_iteration: int, batch_
     workers = [dlr.Engine(D) for _ in range(W)]
     server = dlr.Engine(D)
     try:
+        for wk in workers:
+            wk.set_summation_order(order)
         server.set_weights(w0)
         nbs = [load_train(wk, s) for wk, s in zip(workers, shards)]
         assert len(set(nbs)) == 1
@@ -100,7 +105,8 @@ def run_engine(shards: Sequence[dlr.Dataset], D: int, num_iteration: int, batch_
 
 def run_group(shards: Sequence, D: int, num_iteration: int, batch_size: int, learning_rate: float,
               test=None, test_interval: int = 10, mode: int = dlr.MODE_SYNC_MEAN, C_: float = 1.0,
-              random_state: int = 0, dense: bool = False, device: int = 0, setup=None) -> EngineRun:
+              random_state: int = 0, dense: bool = False, device: int = 0, setup=None,
+              order: int = dlr.ORDER_REFERENCE) -> EngineRun:
     """RunWorker (main.cc:124-170) with W = len(shards) ranks of ONE device
     linked by the loopback transport (dlr_create_group): the product's
     world > 1 step -- key-range all-to-all, rank-ordered merge, in-place
@@ -123,6 +129,7 @@ def run_group(shards: Sequence, D: int, num_iteration: int, batch_size: int, lea
     def rank_main(r: int):
         eng = engines[r]
         try:
+            eng.set_summation_order(order)
             eng.set_weights(w0)                      # every rank holds InitWeight_'s result (main.cc:141-148)
             nb = eng.load_train_dense(shards[r], batch_size) if dense else eng.load_train(shards[r], batch_size)
             if r == 0 and test is not None:

@@ -7,8 +7,10 @@ and of the oracle.  DLR_BAND_ROWS forces small bands so the golden C1
 trajectories and reduced C3-shaped shards exercise many bands, ragged last
 bands, empty bands, both row widths (uint16 for <= 65,536-row batches, else
 uint32), unit and fp32 values, the pushed gradient (N > 1 path) and the
-key-range exchange.  Long columns in band mode are summed per row phase
-(deterministic, within the 1e-5 tolerance, as the chunked long path)."""
+key-range exchange.  Under the FAST summation order (opt-in,
+dlr_set_summation_order) long columns in band mode are summed per row phase
+(deterministic, within the 1e-5*|b| + 1e-7 bar); in the reference order
+(default) every column is one chain across the bands."""
 from __future__ import annotations
 
 import os
@@ -23,8 +25,9 @@ from engine_driver import run_engine
 from test_gpu_layouts import _c3_shards, _csr_shard
 from test_gpu_parity import assert_same_weights, compare_runs, oracle_shard
 
-# band mode's default long-column threshold (dlr_engine.cpp, DLR_LONG_COLUMN):
-# columns with more entries than this are summed in phases / pieces
+# band mode's FAST long-column threshold (dlr_engine.cpp, DLR_LONG_COLUMN):
+# under ORDER_FAST columns with more entries than this are summed in phases /
+# pieces
 BAND_LONG_COLUMN = 2048
 
 pytestmark = pytest.mark.gpu
@@ -35,9 +38,10 @@ def classic(monkeypatch):
     monkeypatch.setenv("DLR_GRAD_KERNEL", "classic")
 
 
-def _band_rows(ds, D, B):
+def _band_rows(ds, D, B, order=dlr.ORDER_REFERENCE):
     eng = dlr.Engine(D)
     try:
+        eng.set_summation_order(order)
         eng.set_weights(dlr.init_weight(D))
         eng.load_train(ds, B)
         assert eng.train_layout() == dlr.LAYOUT_CLASSIC
@@ -108,16 +112,30 @@ def test_ragged_and_empty_bands(classic, monkeypatch):
 
 @pytest.mark.parametrize("rows", [4096, 32768])
 def test_c3_bands_bitwise_without_chunking(monkeypatch, rows):
-    # every column one sequential sum, carried across bands: bitwise the
-    # oracle (uint32 rows: the full-shard batch has > 65,536 rows)
-    monkeypatch.setenv("DLR_LONG_COLUMN", "0")
+    # the reference order (default): every column one sequential sum,
+    # carried across bands -- bitwise the oracle (uint32 rows: the
+    # full-shard batch has > 65,536 rows); a stray DLR_LONG_COLUMN does not
+    # change the order
+    monkeypatch.setenv("DLR_LONG_COLUMN", "50")
     monkeypatch.setenv("DLR_BAND_ROWS", str(rows))
     D = 1 << 24
     shards = _c3_shards(1, rows=80_000)
     assert _band_rows(shards[0], D, -1) == rows
     eng = run_engine(shards, D, 2, -1, 0.2)
+    assert not eng_fast(shards[0], D)
     orc = oracle.run_worker([_csr_shard(s) for s in shards], D, 2, -1, 0.2)
     compare_runs(eng, orc)
+
+
+def eng_fast(ds, D):
+    """The loaded shard's reported order is FAST (dlr_summation_order)."""
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(dlr.init_weight(D))
+        eng.load_train(ds, -1)
+        return eng.summation_order() == dlr.ORDER_FAST
+    finally:
+        eng.close()
 
 
 def _within(a, b, rel=1e-5, floor=1e-7):
@@ -134,33 +152,34 @@ def test_c3_bands_long_phases_within_tolerance(monkeypatch, W):
     D = 1 << 24
     shards = _c3_shards(W, rows=80_000)
     monkeypatch.setenv("DLR_BAND_ROWS", "8192")
-    assert _band_rows(shards[0], D, -1) == 8192
-    got = run_engine(shards, D, 3, -1, 0.2)
+    assert _band_rows(shards[0], D, -1, dlr.ORDER_FAST) == 8192
+    got = run_engine(shards, D, 3, -1, 0.2, order=dlr.ORDER_FAST)
     orc = oracle.run_worker([_csr_shard(s) for s in shards], D, 3, -1, 0.2)
     _within(got.w, orc.w)
-    again = run_engine(shards, D, 3, -1, 0.2)
+    again = run_engine(shards, D, 3, -1, 0.2, order=dlr.ORDER_FAST)
     assert_same_weights(again.w, got.w)
 
 
+@pytest.mark.parametrize("order", [dlr.ORDER_REFERENCE, dlr.ORDER_FAST])
 @pytest.mark.parametrize("W", [1, 2])
-def test_band_pipeline_bitwise_vs_sequential(monkeypatch, W):
+def test_band_pipeline_bitwise_vs_sequential(monkeypatch, W, order):
     # band mode runs the margin band by band with each band's gradient on a
     # second stream beside the next band's margin, the long-column phases
-    # after the last margin (DLR_BAND_PIPE=0: margin, then gradient): the
-    # same kernels on the same data -- bitwise the same weights
+    # (FAST) after the last margin (DLR_BAND_PIPE=0: margin, then gradient):
+    # the same kernels on the same data -- bitwise the same weights
     D = 1 << 24
     shards = _c3_shards(W, rows=80_000)
     monkeypatch.setenv("DLR_BAND_ROWS", "8192")
-    got = run_engine(shards, D, 3, -1, 0.2)
+    got = run_engine(shards, D, 3, -1, 0.2, order=order)
     monkeypatch.setenv("DLR_BAND_PIPE", "0")
-    ref = run_engine(shards, D, 3, -1, 0.2)
+    ref = run_engine(shards, D, 3, -1, 0.2, order=order)
     assert_same_weights(got.w, ref.w)
 
 
 def test_c3_banded_pushed_gradient(monkeypatch):
-    # the N > 1 path's pushed gradient (non-fused finalize): short columns
-    # bitwise the unbanded classic kernel's, long columns within 1e-5 of the
-    # oracle's sequential sums
+    # the N > 1 path's pushed gradient (non-fused finalize), FAST order:
+    # short columns bitwise the unbanded classic kernel's, long columns
+    # within 1e-5 of the oracle's sequential sums
     D = 1 << 24
     ds = _c3_shards(1, rows=60_000)[0]
     rp, col, val, lab = ds.csr()
@@ -172,6 +191,7 @@ def test_c3_banded_pushed_gradient(monkeypatch):
         monkeypatch.setenv("DLR_BAND_ROWS", rows)
         eng = dlr.Engine(D)
         try:
+            eng.set_summation_order(dlr.ORDER_FAST)
             eng.set_weights(w0)
             eng.load_train(ds, -1)
             assert eng.train_band_rows() == int(rows)
@@ -194,10 +214,10 @@ def test_long_phases_small_threshold(classic, monkeypatch, B, value_mode):
     monkeypatch.setenv("DLR_LONG_COLUMN", "50")
     D = 2000
     ds = dlr.Dataset.generate(20_000, D, 12, value_mode=value_mode, seed=9, stream=1)
-    got = run_engine([ds], D, 2, B, 0.1)
+    got = run_engine([ds], D, 2, B, 0.1, order=dlr.ORDER_FAST)
     orc = oracle.run_worker([_csr_shard(ds)], D, 2, B, 0.1)
     _within(got.w, orc.w)
-    again = run_engine([ds], D, 2, B, 0.1)
+    again = run_engine([ds], D, 2, B, 0.1, order=dlr.ORDER_FAST)
     assert_same_weights(again.w, got.w)
 
 
@@ -261,9 +281,10 @@ def test_long_phase_order_bitwise(monkeypatch, piece):
     w0 = dlr.init_weight(D)
     eng = dlr.Engine(D)
     try:
+        eng.set_summation_order(dlr.ORDER_FAST)
         eng.set_weights(w0)
         eng.load_train(ds, -1)
-        assert eng.train_band_rows() == 8192
+        assert eng.train_band_rows() == 8192 and eng.summation_order() == dlr.ORDER_FAST
         got = eng.worker_gradient(0, 1.0)
     finally:
         eng.close()

@@ -1,19 +1,23 @@
 """BASELINE C3 at its real per-GPU size: a 12.5M-row
 Criteo-shaped shard (2^24 hashed features, 39 Zipf fields, unit values),
-B = -1 (the full shard per step, as local.sh), the DEFAULT engine choices:
-frequency relabeling, 2^20-row bands, long columns (> 2,048 entries) in
-16,384-row phases combined by a fixed tree, hot weights in LDS for the
-margin.  Two steps against the oracle (lr.cc:35-40 + main.cc:70-72).
+B = -1 (the full shard per step, as local.sh), under the opt-in FAST
+summation order (dlr_set_summation_order): frequency relabeling, 2^20-row
+bands, long columns (> 2,048 entries) in 16,384-row phases combined by a
+fixed tree, hot weights in LDS for the margin.  Two steps against the
+oracle (lr.cc:35-40 + main.cc:70-72).  (The default, reference order at
+this size is bitwise: test_gpu_fullsize.py.)
 
-Bars (north_star: weights within 1e-5 relative): the pushed gradient of
+What FAST guarantees, pinned here (it is NOT the north-star parity bar:
+with the centred init it leaves 1e-5*|b| + 1e-7): the pushed gradient of
 the short columns (<= 4,096 entries: one sequential sum each, carried
 across bands) bitwise; the long columns (~10^5-10^6-entry chains) at least
 as close to the exact (fp64) column sums of the reference's own fp32
 residuals as the reference's single fp32 chain is -- that chain is itself
 off by up to ~1e-4 relative at this length, so no reordered sum can match
 it to 1e-5 (the same argument as C4's blocked gradient,
-test_gpu_dense.py); weights within 1e-5*|b| + 1e-6 after each step; a rerun
-bitwise identical.
+test_gpu_dense.py); the weights' drift from the oracle after each step
+printed against the north-star bar and bounded by FAST_DRIFT; a rerun bitwise
+identical.
 
 Two initial weight vectors: the reference's own InitWeight_ (lr.cc:92-98,
 w in [0,1]: with 39 such weights per row every margin is ~20, sigma rounds
@@ -35,6 +39,7 @@ from test_gpu_parity import assert_same_weights
 pytestmark = pytest.mark.gpu
 
 D, ROWS, LR = 1 << 24, 12_500_000, 0.2
+FAST_DRIFT = (5e-5, 1e-6)  # |a - b| <= rel * |b| + abs: FAST's documented drift, not a parity bar
 
 
 def _exact_gradient(csr, lab, w):
@@ -76,9 +81,11 @@ def test_c3_full_size_two_steps(c3_shard, init):
     assert long_cols.sum() > 100 and counts.max() > 500_000      # the ~10^6-entry chains are there
     eng = dlr.Engine(D)
     try:
+        eng.set_summation_order(dlr.ORDER_FAST)
         eng.set_weights(w0)
         assert eng.load_train(ds, -1) == 1
         assert eng.train_band_rows() == 1 << 20 and eng.train_relabeled() and eng.train_unit_values()
+        assert eng.summation_order() == dlr.ORDER_FAST
         # the pushed gradient of step 0 (the N > 1 path's finalize)
         g_eng = eng.worker_gradient(0, 1.0)
         g_orc = oracle.grad_csr(csr, lab, rows, w0)
@@ -104,8 +111,9 @@ def test_c3_full_size_two_steps(c3_shard, init):
             x, y = got.astype(np.float64), w.astype(np.float64)
             big = np.abs(y) >= 1e-2
             print(f"\nC3 full size ({init} init) step {step}: weights vs oracle max rel "
-                  f"{np.max(np.abs(x - y)[big] / np.abs(y)[big]):.3g} (|w| >= 1e-2), max abs {np.max(np.abs(x - y)):.3g}")
-            assert np.all(np.abs(x - y) <= 1e-5 * np.abs(y) + 1e-6), f"step {step}"
+                  f"{np.max(np.abs(x - y)[big] / np.abs(y)[big]):.3g} (|w| >= 1e-2), max abs {np.max(np.abs(x - y)):.3g}, "
+                  f"outside 1e-5*|b| + 1e-7: {int((np.abs(x - y) > 1e-5 * np.abs(y) + 1e-7).sum())}")
+            assert np.all(np.abs(x - y) <= FAST_DRIFT[0] * np.abs(y) + FAST_DRIFT[1]), f"step {step}"
         # deterministic: the same two steps again
         eng.set_weights(w0)
         for step in range(2):

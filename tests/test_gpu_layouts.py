@@ -167,8 +167,9 @@ def _hot_count(ds):
 
 
 def test_c3_hot_columns_bitwise_without_chunking(monkeypatch):
-    # DLR_LONG_COLUMN=0: every column is one sequential sum -> bitwise
-    monkeypatch.setenv("DLR_LONG_COLUMN", "0")
+    # the reference order (default): every column is one sequential sum ->
+    # bitwise, whatever the FAST-only DLR_LONG_COLUMN threshold says
+    monkeypatch.setenv("DLR_LONG_COLUMN", "4096")
     D = 1 << 24
     shards = _c3_shards(1)
     assert _hot_count(shards[0]) > 4096
@@ -179,20 +180,20 @@ def test_c3_hot_columns_bitwise_without_chunking(monkeypatch):
 
 @pytest.mark.parametrize("W", [1, 2])
 def test_c3_long_column_chunking_within_tolerance(W, monkeypatch):
-    # columns with > 4,096 entries summed in chunks (forced here without
-    # bands; the band-mode default threshold is 2,048)
+    # FAST order: columns with > 4,096 entries summed in chunks (forced here
+    # without bands; the band-mode FAST threshold is 2,048)
     # (deterministic); weights stay within the north-star bar of the
     # reference's single sequential sum: |a-b| <= 1e-5*|b| + 1e-7
     monkeypatch.setenv("DLR_LONG_COLUMN", "4096")
     D = 1 << 24
     shards = _c3_shards(W)
-    eng = run_engine(shards, D, 3, -1, 0.2)
+    eng = run_engine(shards, D, 3, -1, 0.2, order=dlr.ORDER_FAST)
     orc = oracle.run_worker([_csr_shard(s) for s in shards], D, 3, -1, 0.2)
     a, b = eng.w.astype(np.float64), orc.w.astype(np.float64)
     err = np.abs(a - b) - (1e-5 * np.abs(b) + 1e-7)
     assert err.max() <= 0, f"max excess {err.max():.3g}"
     # run twice: deterministic
-    eng2 = run_engine(shards, D, 3, -1, 0.2)
+    eng2 = run_engine(shards, D, 3, -1, 0.2, order=dlr.ORDER_FAST)
     assert_same_weights(eng2.w, eng.w)
 
 
@@ -203,15 +204,15 @@ def test_c3_long_columns_forced_collectives(monkeypatch):
     D = 1 << 24
     shards = _c3_shards(1)
     monkeypatch.delenv("DLR_FORCE_COLLECTIVES")
-    ref = run_engine(shards, D, 2, -1, 0.2)
+    ref = run_engine(shards, D, 2, -1, 0.2, order=dlr.ORDER_FAST)
     monkeypatch.setenv("DLR_FORCE_COLLECTIVES", "1")
-    got = run_engine(shards, D, 2, -1, 0.2)
+    got = run_engine(shards, D, 2, -1, 0.2, order=dlr.ORDER_FAST)
     assert_same_weights(got.w, ref.w)
 
 
 def test_c3_long_column_gradient_tolerance(monkeypatch):
-    # the pushed gradient itself (lr.cc:40's g): hot columns summed in
-    # chunks differ from the single sequential sum by rounding only
+    # the pushed gradient itself (lr.cc:40's g), FAST order: hot columns
+    # summed in chunks differ from the single sequential sum by rounding only
     monkeypatch.setenv("DLR_LONG_COLUMN", "4096")
     D = 1 << 24
     ds = _c3_shards(1, rows=120_000)[0]
@@ -221,8 +222,10 @@ def test_c3_long_column_gradient_tolerance(monkeypatch):
     w0 = dlr.init_weight(D)
     eng = dlr.Engine(D)
     try:
+        eng.set_summation_order(dlr.ORDER_FAST)
         eng.set_weights(w0)
         eng.load_train(ds, -1)
+        assert eng.summation_order() == dlr.ORDER_FAST
         g = eng.worker_gradient(0, 1.0)
     finally:
         eng.close()

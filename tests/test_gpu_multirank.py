@@ -160,8 +160,8 @@ def _csr(ds):
 def test_c3_shaped_two_ranks_bands_relabel_bitwise(monkeypatch):
     # C3 structure on 2 ranks: frequency relabeling from the ranks' SUMMED
     # column counts, row bands, the hot-weight margin, key-range exchange of
-    # the 2^24 weights; one sequential sum per column -> bitwise
-    monkeypatch.setenv("DLR_LONG_COLUMN", "0")
+    # the 2^24 weights; one sequential sum per column (the reference order,
+    # default) -> bitwise
     monkeypatch.setenv("DLR_BAND_ROWS", "16384")
     D = 1 << 24
     shards = _c3_shards(2, 70_000)
@@ -171,14 +171,15 @@ def test_c3_shaped_two_ranks_bands_relabel_bitwise(monkeypatch):
 
 
 def test_c3_shaped_two_ranks_long_phases_within_tolerance(monkeypatch):
+    # FAST order: long columns in phases
     monkeypatch.setenv("DLR_BAND_ROWS", "16384")
     D = 1 << 24
     shards = _c3_shards(2, 70_000)
-    got = run_group(shards, D, 2, -1, 0.2)
+    got = run_group(shards, D, 2, -1, 0.2, order=dlr.ORDER_FAST)
     orc = oracle.run_worker([_csr(s) for s in shards], D, 2, -1, 0.2)
     a, b = got.w.astype(np.float64), orc.w.astype(np.float64)
     assert np.all(np.abs(a - b) <= 1e-5 * np.abs(b) + 1e-7)
-    one = run_engine(shards, D, 2, -1, 0.2)  # the single-process W = 2 parameter-server topology
+    one = run_engine(shards, D, 2, -1, 0.2, order=dlr.ORDER_FAST)  # the W = 2 parameter-server topology
     a = one.w.astype(np.float64)
     assert np.all(np.abs(a - b) <= 1e-5 * np.abs(b) + 1e-7)
 

@@ -66,15 +66,15 @@ def test_streamed_copy_paths_bitwise(monkeypatch, coalesce, device_layout):
 
 @pytest.mark.parametrize("value_mode", [0, 1])
 def test_streamed_long_columns(monkeypatch, value_mode):
-    # classic layout with chunked long columns (per-batch long arrays streamed too)
+    # FAST order, classic layout with chunked long columns (per-batch long arrays streamed too)
     monkeypatch.setenv("DLR_GRAD_KERNEL", "classic")
     monkeypatch.setenv("DLR_LONG_COLUMN", "50")
     D = 2000
     ds = dlr.Dataset.generate(20_000, D, 12, value_mode=value_mode, seed=9, stream=1)
     monkeypatch.setenv("DLR_RESIDENCY", "device")
-    ref = run_engine([ds], D, 2, 3000, 0.1)
+    ref = run_engine([ds], D, 2, 3000, 0.1, order=dlr.ORDER_FAST)
     monkeypatch.setenv("DLR_RESIDENCY", "stream")
-    got = run_engine([ds], D, 2, 3000, 0.1)
+    got = run_engine([ds], D, 2, 3000, 0.1, order=dlr.ORDER_FAST)
     assert_same_weights(got.w, ref.w)
 
 
