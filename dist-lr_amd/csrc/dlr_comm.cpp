@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 namespace dlr {
@@ -34,30 +35,52 @@ class RcclComm final : public Comm {
 public:
     RcclComm(ncclComm_t c, int world, int rank) : comm_(c), world_(world), rank_(rank) {}
     ~RcclComm() override {
-        if (!aborted_) ncclCommDestroy(comm_);
+        if (abort_req_.load())
+            abort_now();
+        else
+            ncclCommDestroy(comm_);
     }
-    void abort(const std::string &) override {
-        if (!aborted_) (void)ncclCommAbort(comm_);  // frees the communicator; peers' RCCL calls error out
-        aborted_ = true;
+    // Any thread: flags the communicator.  Its driving thread aborts it
+    // (abort_now) at the next collective or wait: ncclCommAbort on a
+    // communicator another thread is using would free it under that
+    // thread.
+    void abort(const std::string &why) override {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            if (why_.empty()) why_ = why;
+        }
+        abort_req_.store(true);
+    }
+    bool wait(hipStream_t s, std::string &err) override {
+        // poll the stream; a flagged communicator is aborted here, which
+        // makes its pending collective kernels return, then the stream drains
+        for (int spin = 0;; ++spin) {
+            const hipError_t e = hipStreamQuery(s);
+            if (e == hipSuccess) break;
+            if (e != hipErrorNotReady) return hip_ok(e, "hipStreamQuery", err);
+            if (abort_req_.load()) abort_now();
+            if (spin > 2000) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+        return !flagged(err);
     }
     int world() const override { return world_; }
     int rank() const override { return rank_; }
     const char *kind() const override { return "rccl"; }
     bool all_reduce_i64(int64_t *d, size_t n, bool max, hipStream_t s, std::string &err) override {
-        if (aborted_) return nccl_ok(ncclInvalidUsage, "aborted communicator", err);
+        if (flagged(err)) return false;
         return nccl_ok(ncclAllReduce(d, d, n, ncclInt64, max ? ncclMax : ncclSum, comm_, s), "ncclAllReduce", err);
     }
     bool all_gather(const void *send, void *recv, size_t words, hipStream_t s, std::string &err) override {
-        if (aborted_) return nccl_ok(ncclInvalidUsage, "aborted communicator", err);
+        if (flagged(err)) return false;
         return nccl_ok(ncclAllGather(send, recv, words, ncclUint32, comm_, s), "ncclAllGather", err);
     }
     bool all_to_all(const void *send, void *recv, size_t words, hipStream_t s, std::string &err) override {
-        if (aborted_) return nccl_ok(ncclInvalidUsage, "aborted communicator", err);
+        if (flagged(err)) return false;
         return nccl_ok(ncclAllToAll(send, recv, words, ncclUint32, comm_, s), "ncclAllToAll", err);
     }
     bool all_gather_part(void *buf, size_t chunk, size_t off, size_t count, hipStream_t s,
                          std::string &err) override {
-        if (aborted_) return nccl_ok(ncclInvalidUsage, "aborted communicator", err);
+        if (flagged(err)) return false;
         if (world_ == 1 || count == 0) return true;
         // point to point: the piece of every peer's block, strided by chunk
         uint32_t *b = static_cast<uint32_t *>(buf);
@@ -77,9 +100,23 @@ public:
     }
 
 private:
+    // the driving thread: a flagged communicator is aborted, the call fails
+    bool flagged(std::string &err) {
+        if (!abort_req_.load()) return false;
+        abort_now();
+        std::lock_guard<std::mutex> g(mu_);
+        err = "RCCL communicator aborted (" + why_ + ")";
+        return true;
+    }
+    void abort_now() {
+        if (!aborted_.exchange(true)) (void)ncclCommAbort(comm_);
+    }
+
     ncclComm_t comm_;
     int world_, rank_;
-    bool aborted_ = false;
+    std::atomic<bool> abort_req_{false}, aborted_{false};
+    std::mutex mu_;
+    std::string why_;
 };
 
 }  // namespace
@@ -124,8 +161,11 @@ int loop_timeout_s() {
 }
 
 struct LoopGroup {
-    explicit LoopGroup(int w) : W(w), timeout_s(loop_timeout_s()), send((size_t)w, nullptr), recv((size_t)w, nullptr) {}
+    LoopGroup(int w, bool a)
+        : W(w), async(a), timeout_s(loop_timeout_s()), send((size_t)w, nullptr), recv((size_t)w, nullptr),
+          ev_send((size_t)w, nullptr), ev_done((size_t)w, nullptr) {}
     const int W;
+    const bool async;
     const int timeout_s;
     std::mutex mu;
     std::condition_variable cv;
@@ -135,6 +175,10 @@ struct LoopGroup {
     std::string why;      // ... and why
     std::vector<const void *> send;
     std::vector<void *> recv;
+    // async: rank q's events -- its send buffer is produced (recorded on its
+    // stream before the collective's first barrier), its copies out of the
+    // peers' buffers are done (before the second)
+    std::vector<hipEvent_t> ev_send, ev_done;
     std::atomic<int> refs{0};
 
     void abort(const std::string &reason) {
@@ -175,6 +219,8 @@ class LoopbackComm final : public Comm {
 public:
     LoopbackComm(LoopGroup *g, int rank) : g_(g), rank_(rank) { g_->refs.fetch_add(1); }
     ~LoopbackComm() override {
+        for (hipEvent_t e : {g_->ev_send[(size_t)rank_], g_->ev_done[(size_t)rank_]})
+            if (e) (void)hipEventDestroy(e);
         if (g_->refs.fetch_sub(1) == 1) delete g_;
     }
     int world() const override { return g_->W; }
@@ -183,8 +229,9 @@ public:
     void abort(const std::string &why) override { g_->abort("rank " + std::to_string(rank_) + ": " + why); }
 
     bool all_reduce_i64(int64_t *d, size_t n, bool max, hipStream_t s, std::string &err) override {
+        // load-time agreement on host values: always synchronous
         const int W = g_->W;
-        if (!publish(d, d, s, err)) return false;
+        if (!publish_sync(d, d, s, err)) return false;
         std::vector<int64_t> all((size_t)W * n);
         bool ok = true;
         for (int q = 0; q < W && ok; ++q)
@@ -210,8 +257,8 @@ public:
         for (int q = 0; q < g_->W && ok; ++q) {
             char *dst = static_cast<char *>(recv) + (size_t)q * bytes;
             if (dst == g_->send[(size_t)q] || bytes == 0) continue;  // in place
-            ok = hip_ok(hipMemcpyAsync(dst, g_->send[(size_t)q], bytes, hipMemcpyDeviceToDevice, s),
-                        "loopback all_gather", err);
+            ok = after(q, s, err) && hip_ok(hipMemcpyAsync(dst, g_->send[(size_t)q], bytes, hipMemcpyDeviceToDevice, s),
+                                             "loopback all_gather", err);
         }
         return finish(ok, s, err);
     }
@@ -223,7 +270,8 @@ public:
         for (int q = 0; q < g_->W && ok && count; ++q) {
             if (q == rank_) continue;
             const size_t at = ((size_t)q * chunk + off) * 4;
-            ok = hip_ok(hipMemcpyAsync(static_cast<char *>(buf) + at, static_cast<const char *>(g_->send[(size_t)q]) + at,
+            ok = after(q, s, err) &&
+                 hip_ok(hipMemcpyAsync(static_cast<char *>(buf) + at, static_cast<const char *>(g_->send[(size_t)q]) + at,
                                        count * 4, hipMemcpyDeviceToDevice, s),
                         "loopback all_gather_part", err);
         }
@@ -235,7 +283,8 @@ public:
         if (!publish(send, recv, s, err)) return false;
         bool ok = true;
         for (int q = 0; q < g_->W && ok && bytes; ++q)
-            ok = hip_ok(hipMemcpyAsync(static_cast<char *>(recv) + (size_t)q * bytes,
+            ok = after(q, s, err) &&
+                 hip_ok(hipMemcpyAsync(static_cast<char *>(recv) + (size_t)q * bytes,
                                        static_cast<const char *>(g_->send[(size_t)q]) + (size_t)rank_ * bytes, bytes,
                                        hipMemcpyDeviceToDevice, s),
                         "loopback all_to_all", err);
@@ -243,22 +292,55 @@ public:
     }
 
 private:
-    // This rank's buffers are complete (stream drained) and visible to the
-    // peers once every rank has passed the barrier.
-    bool publish(const void *send, void *recv, hipStream_t s, std::string &err) {
+    bool events(std::string &err) {
+        for (hipEvent_t *e : {&g_->ev_send[(size_t)rank_], &g_->ev_done[(size_t)rank_]})
+            if (!*e && !hip_ok(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate", err)) return false;
+        return true;
+    }
+    // sync: this rank's buffers are complete (stream drained) and visible
+    // to the peers once every rank has passed the barrier
+    bool publish_sync(const void *send, void *recv, hipStream_t s, std::string &err) {
         if (!hip_ok(hipStreamSynchronize(s), "loopback collective", err)) return false;
         g_->send[(size_t)rank_] = send;
         g_->recv[(size_t)rank_] = recv;
         return g_->barrier(err);
     }
+    // async: the buffers are published with the event that marks them
+    // produced on this rank's stream; nothing waits for the GPU here
+    bool publish(const void *send, void *recv, hipStream_t s, std::string &err) {
+        if (!g_->async) return publish_sync(send, recv, s, err);
+        if (!events(err) ||
+            !hip_ok(hipEventRecord(g_->ev_send[(size_t)rank_], s), "loopback collective (record)", err))
+            return false;
+        g_->send[(size_t)rank_] = send;
+        g_->recv[(size_t)rank_] = recv;
+        return g_->barrier(err);
+    }
+    // async: this stream's copies out of rank q's buffer start after q produced it
+    bool after(int q, hipStream_t s, std::string &err) {
+        if (!g_->async || q == rank_) return true;
+        return hip_ok(hipStreamWaitEvent(s, g_->ev_send[(size_t)q], 0), "loopback collective (wait)", err);
+    }
     // The copies out of the peers' buffers are done before any rank reuses
-    // its send buffer.
+    // its send buffer: sync -- both streams drained behind a barrier; async
+    // -- every rank's stream waits on every copier's event
     bool finish(bool ok, hipStream_t s, std::string &err) {
-        ok = ok && hip_ok(hipStreamSynchronize(s), "loopback collective", err);
+        if (!g_->async) {
+            ok = ok && hip_ok(hipStreamSynchronize(s), "loopback collective", err);
+            std::string berr;
+            const bool b = g_->barrier(berr);
+            if (ok && !b) err = berr;
+            return ok && b;
+        }
+        ok = ok && hip_ok(hipEventRecord(g_->ev_done[(size_t)rank_], s), "loopback collective (record)", err);
         std::string berr;
         const bool b = g_->barrier(berr);
         if (ok && !b) err = berr;
-        return ok && b;
+        ok = ok && b;
+        for (int q = 0; q < g_->W && ok; ++q)
+            if (q != rank_)
+                ok = hip_ok(hipStreamWaitEvent(s, g_->ev_done[(size_t)q], 0), "loopback collective (wait)", err);
+        return ok;
     }
 
     LoopGroup *g_;
@@ -267,7 +349,7 @@ private:
 
 }  // namespace
 
-LoopGroup *make_loop_group(int world) { return new LoopGroup(world); }
+LoopGroup *make_loop_group(int world, bool async) { return new LoopGroup(world, async); }
 
 Comm *make_loopback_comm(LoopGroup *g, int rank) { return new LoopbackComm(g, rank); }
 

@@ -49,8 +49,23 @@ public:
                                  std::string &err) = 0;
     // A rank that will not reach its next collective (it failed) releases
     // its peers: their pending and later collectives fail with `why`
-    // instead of waiting (loopback), or the communicator is aborted (RCCL).
+    // instead of waiting (loopback).  RCCL: callable from any thread (the
+    // in-process topology of bin/distlr aborts every rank's communicator
+    // from the failing rank's thread): it only flags the communicator; the
+    // thread that drives it aborts it (ncclCommAbort) at its next
+    // collective or stream wait (wait below), which also makes its
+    // stuck collective kernels exit.
     virtual void abort(const std::string &why) = 0;
+    // Waits for stream s (the engine's waits on streams that carry this
+    // transport's collectives).  RCCL: polls, and aborts the communicator
+    // when abort() was called -- a plain hipStreamSynchronize would never
+    // return behind a collective whose peer died.
+    virtual bool wait(hipStream_t s, std::string &err) {
+        const hipError_t e = hipStreamSynchronize(s);
+        if (e == hipSuccess) return true;
+        err = std::string("hipStreamSynchronize: ") + hipGetErrorString(e);
+        return false;
+    }
 };
 
 // RCCL communicator for rank `rank` of `world` (unique_id: the 128-byte
@@ -62,8 +77,16 @@ bool rccl_unique_id(void *out, std::string &err);
 
 // In-process group of `world` loopback ranks; make_loopback_comm(g, r) is
 // rank r's endpoint.  The group is reference-counted by its endpoints.
+// async (default; DLR_LOOPBACK_SYNC=1 turns it off): the data collectives
+// are STREAM-ORDERED like RCCL's -- a rank's copies out of a peer's buffer
+// wait on the event the peer recorded after producing it, and the peer's
+// stream waits on the copiers' events before it may overwrite it; the host
+// threads meet only to exchange buffers and events (they never wait for
+// GPU work), so a rank's next kernels queue up behind the collective as
+// they would over RCCL.  sync: every collective drains both streams behind
+// host barriers.
 struct LoopGroup;
-LoopGroup *make_loop_group(int world);
+LoopGroup *make_loop_group(int world, bool async);
 Comm *make_loopback_comm(LoopGroup *g, int rank);
 
 }  // namespace dlr

@@ -141,6 +141,12 @@ struct TrainShard {
     // dense shard (dlr_load_train_dense): X row-major n_rows x D
     bool dense = false, dblocked = false, dfused = false;
     float *dX = nullptr, *dpart = nullptr;
+    // reference order, large batches: the banded one-launch step (K6r,
+    // k_dense_ref) and its hand-off words (dlr_kernels.h DevRefSync)
+    bool dref = false;
+    uint32_t *dref_sync = nullptr;
+    uint32_t dref_seq = 0;
+    int dref_lead = 0;
     // streamed dense shard (DLR_RESIDENCY_STREAM): X stays in the caller's
     // host memory (registered, pinned in place); each batch's rows and labels
     // are staged into one of two device slots on the copy stream
@@ -312,6 +318,19 @@ int fail(dlr_ctx *c, int code, const std::string &msg) {
         if (!(c)->comm->expr) return fail((c), DLR_E_RCCL, std::string((c)->comm->kind()) + " " + e_);  \
     } while (0)
 
+// Waits for a stream that may carry this rank's collectives: through the
+// transport (an aborted RCCL communicator makes its stuck kernels return
+// instead of blocking here forever, dlr_comm.h), else hipStreamSynchronize.
+int wait_stream(dlr_ctx *c, hipStream_t s, const char *who) {
+    if (!c->comm) {
+        HIPC(c, hipStreamSynchronize(s));
+        return DLR_OK;
+    }
+    std::string err;
+    if (!c->comm->wait(s, err)) return fail(c, DLR_E_RCCL, std::string(who) + ": " + err);
+    return DLR_OK;
+}
+
 int dev_alloc(dlr_ctx *c, void **p, size_t bytes) {
     *p = nullptr;
     if (bytes == 0) bytes = 16;
@@ -386,7 +405,7 @@ void free_train(dlr_ctx *c) {
                     (void *)t.lpslot, (void *)t.lpws, (void *)t.lprow, (void *)t.lpval, (void *)t.pm_lbeg,
                     (void *)t.pm_list, (void *)t.pm_pofs, (void *)t.pm_rg, (void *)t.pm_qoff, (void *)t.pm_val,
                     (void *)t.pm_p, (void *)t.pm_qs, (void *)t.xslices, (void *)t.rt_gq, (void *)t.rt_val,
-                    (void *)t.rt_cend})
+                    (void *)t.rt_cend, (void *)t.dref_sync})
         dev_free(c, p);
     t = TrainShard();
     c->pm_ready = -1;
@@ -1616,6 +1635,7 @@ hipError_t launch_margin(dlr_ctx *c, int64_t b, bool rowsum_only = false) {
         int64_t first;
         hipError_t e = dense_batch(c, b, &dd, &first);
         if (e != hipSuccess) return e;
+        if (t.dref) return hipSuccess;  // one launch with the gradient (launch_gradient)
         if (t.dfused) return dlr::launch_dense_fused(dd, first, t.plan[(size_t)b].rows, c->w, t.dpart, c->stream);
         return dlr::launch_dense_margin(dd, first, t.plan[(size_t)b].rows, c->w, c->resid, c->stream);
     }
@@ -1677,12 +1697,17 @@ hipError_t launch_long_columns(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
 }
 
 hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float lr, float C, bool fused) {
-    const TrainShard &t = c->train;
+    TrainShard &t = c->train;
     if (t.dense) {
         dlr::DevDense dd;
         int64_t first;
         hipError_t e = dense_batch(c, b, &dd, &first);
-        if (e == hipSuccess)
+        if (e == hipSuccess && t.dref) {
+            const dlr::DevRefSync sy{t.dref_sync, t.dref_sync + dlr::dense_ref_sync_words(B) - 64,
+                                     t.dref_sync + dlr::dense_ref_sync_words(B) - 32, t.dref_seq, t.dref_lead};
+            e = dlr::launch_dense_ref(dd, first, B, c->w, gout, c->resid, sy, lr, C, fused, c->stream);
+            if (e == hipSuccess) ++c->train.dref_seq;
+        } else if (e == hipSuccess)
             e = t.dfused ? dlr::launch_dense_combine(t.dpart, c->D, B, c->w, gout, lr, C, fused, c->stream)
                          : dlr::launch_dense_grad(dd, first, B, c->resid, c->w, gout, t.dpart, t.dblocked, lr, C, fused,
                                                   c->stream);
@@ -1877,7 +1902,8 @@ int dlr_create_group(int device, int world, int64_t D, dlr_ctx **out) {
     if (!out || D <= 0 || world <= 0 || world > dlr::kMaxRanks)
         return fail(nullptr, DLR_E_ARG, "dlr_create_group: bad argument");
     for (int r = 0; r < world; ++r) out[r] = nullptr;
-    dlr::LoopGroup *g = dlr::make_loop_group(world);
+    const char *ls = getenv("DLR_LOOPBACK_SYNC");  // "1": host-synchronous collectives (A/B)
+    dlr::LoopGroup *g = dlr::make_loop_group(world, !(ls && strcmp(ls, "1") == 0));
     std::vector<dlr::Comm *> comms((size_t)world);
     for (int r = 0; r < world; ++r) comms[(size_t)r] = dlr::make_loopback_comm(g, r);  // endpoints own g
     for (int r = 0; r < world; ++r) {
@@ -1962,12 +1988,11 @@ int dlr_get_weights(dlr_ctx *c, float *w, int64_t D) {
     HIPC(c, hipSetDevice(c->device));
     if (c->perm.empty()) {
         HIPC(c, hipMemcpyAsync(w, c->w, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
-        HIPC(c, hipStreamSynchronize(c->stream));
-        return DLR_OK;
+        return wait_stream(c, c->stream, "dlr_get_weights");
     }
     std::vector<float> tmp((size_t)D);
     HIPC(c, hipMemcpyAsync(tmp.data(), c->w, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipStreamSynchronize(c->stream));
+    if (int rc = wait_stream(c, c->stream, "dlr_get_weights")) return rc;
     for (int64_t j = 0; j < D; ++j) w[j] = tmp[(size_t)c->perm[(size_t)j]];
     return DLR_OK;
 }
@@ -2749,6 +2774,14 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
         if (t.dfused && !dlr::dense_fused_ok(D))
             return fail(c, DLR_E_ARG, "dlr_load_train_dense: DLR_DENSE_GRAD=fused needs D in {512, 1024, 2048, 4096}");
         t.dblocked = t.dfused || (dg ? strcmp(dg, "blocked") == 0 : big);
+    } else {
+        // the banded reference-order launch (k_dense_ref) for large batches;
+        // DLR_DENSE_REF=1|0 forces it on (where D allows) / off (A/B: the
+        // margin kernel, then the column-chain kernel -- the same order)
+        const char *dr = getenv("DLR_DENSE_REF");
+        t.dref = dlr::dense_ref_ok(D, ds->n_rows, t.B) && (dr ? strcmp(dr, "0") != 0 : big);
+        const char *dl = getenv("DLR_DENSE_REF_LEAD");  // A/B: margin throttle in 256-row slots (0 = off)
+        t.dref_lead = dl ? atoi(dl) : 0;
     }
     t.fast = t.dblocked;
     // Residency: device-resident unless asked to stream, or (auto) the rows
@@ -2791,8 +2824,15 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
     if (t.dblocked &&
         (rc = dev_alloc(c, (void **)&t.dpart, (size_t)dlr::dense_chunks(t.B) * (size_t)((D + 3) & ~int64_t(3)) * 4)))
         return rc;
-    // residuals: whole 4-row quads + 4 (the reference-order gradient reads them 16 bytes at a time)
-    const int64_t rneed = ((t.B + 3) & ~int64_t(3)) + 4;
+    // residuals: whole 4-row quads + 4 (the reference-order gradient reads
+    // them 16 bytes at a time); the banded launch reads whole 256-row slots
+    const int64_t rneed = t.dref ? dlr::dense_ref_resid(t.B) : ((t.B + 3) & ~int64_t(3)) + 4;
+    if (t.dref) {
+        const int64_t nw = dlr::dense_ref_sync_words(t.B);
+        if ((rc = dev_alloc(c, (void **)&t.dref_sync, (size_t)nw * 4))) return rc;
+        HIPC(c, hipMemsetAsync(t.dref_sync, 0, (size_t)nw * 4, c->stream));
+        t.dref_seq = 0;
+    }
     if (c->resid_cap < rneed) {
         dev_free(c, c->resid);
         c->resid = nullptr;
@@ -3028,7 +3068,7 @@ int dlr_predict(dlr_ctx *c, int64_t *correct, int64_t *n_rows, double *logloss) 
     }
     HIPC(c, hipMemcpyAsync(c->h_correct, c->correct, 8, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipMemcpyAsync(c->h_ll, c->ll, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipStreamSynchronize(c->stream));
+    if (int rc = wait_stream(c, c->stream, "dlr_predict")) return rc;
     if (correct) *correct = (int64_t)*c->h_correct;
     if (n_rows) *n_rows = t.n_rows;
     if (logloss) *logloss = *c->h_ll;
@@ -3038,7 +3078,7 @@ int dlr_predict(dlr_ctx *c, int64_t *correct, int64_t *n_rows, double *logloss) 
 int dlr_sync(dlr_ctx *c) {
     if (!c) return DLR_E_ARG;
     HIPC(c, hipSetDevice(c->device));
-    HIPC(c, hipStreamSynchronize(c->stream));
+    if (int rc = wait_stream(c, c->stream, "dlr_sync")) return rc;
     if (c->cstream) HIPC(c, hipStreamSynchronize(c->cstream));  // a streamed shard's batch copies
     return DLR_OK;
 }

@@ -180,6 +180,18 @@ struct DevDense {
     int64_t N, D;
 };
 
+// K6r (k_dense_ref) hand-off state, device words of the loaded shard
+// (zeroed at load): per chain slot of 256 rows the count of its 32-row
+// margin units published, the margin unit queue head, the chains' progress
+// (for the throttle); all monotonic over the launches of the shard (seq).
+struct DevRefSync {
+    uint32_t *slot_cnt;
+    uint32_t *head;
+    uint32_t *prog;
+    uint32_t seq;
+    int lead;  // margin throttle: units claimed at most `lead` slots ahead of the chains (0: off)
+};
+
 // Batch size of every rank (the L2 term of rank r's push is
 // fl32(C*w)/(float)B_r); at most kMaxRanks ranks.
 constexpr int kMaxRanks = 16;
@@ -262,6 +274,15 @@ hipError_t launch_dense_fused(const DevDense &dd, int64_t first, int64_t B, cons
                               hipStream_t s);
 hipError_t launch_dense_combine(const float *part, int64_t D, int64_t B, float *w, float *gout, float lr, float C,
                                 bool fused, hipStream_t s);
+// K6r: the reference-order dense step as one banded launch (margins +
+// column chains + update).  D % 128 == 0, 512 <= D <= 4096, B <= N (the
+// shard, or the streamed slot).  resid: whole 256-row slots (+4).  sync
+// words: dense_ref_sync_words(B) (zeroed).
+bool dense_ref_ok(int64_t D, int64_t N, int64_t B);
+int64_t dense_ref_sync_words(int64_t B);
+int64_t dense_ref_resid(int64_t B);
+hipError_t launch_dense_ref(const DevDense &dd, int64_t first, int64_t B, float *w, float *gout, float *resid,
+                            const DevRefSync &sy, float lr, float C, bool fused, hipStream_t s);
 int predict_dense_grid(int64_t rows);
 hipError_t launch_dense_predict(const DevDense &dd, const float *w, unsigned long long *correct, double *ll_part,
                                 double *ll_out, hipStream_t s);

@@ -69,10 +69,12 @@ struct Config {
 };
 
 // main.cc:124-170 for one rank.
-void run_worker(const Config &cfg, int rank, distlr::KVWorker *kv, std::vector<int> *failed) {
-    // The LR (which owns kv) outlives the try block, so a failing rank can
-    // still release its peers through kv in the handler.
-    std::unique_ptr<distlr::LR> owner;
+// The LR (which owns kv, lr.h:13-15) lives in `owner`, a slot of main's:
+// every rank's KVWorker stays alive until all threads have joined, so a
+// failing rank can release every peer through `all` whatever state they are in.
+void run_worker(const Config &cfg, int rank, distlr::KVWorker *kv, std::vector<distlr::KVWorker *> *all,
+                std::unique_ptr<distlr::LR> *owner_slot, std::vector<int> *failed) {
+    std::unique_ptr<distlr::LR> &owner = *owner_slot;
     try {
         {
             std::lock_guard<std::mutex> g(g_out);
@@ -109,7 +111,13 @@ void run_worker(const Config &cfg, int rank, distlr::KVWorker *kv, std::vector<i
         std::string modelfile = cfg.root + "/models/part-00" + std::to_string(rank + 1);
         lr.SaveModel(modelfile);
     } catch (const std::exception &e) {
-        kv->Abort(std::string("worker ") + std::to_string(rank) + " failed: " + e.what());  // release its peers
+        // release its peers: every rank's transport (the ranks are threads
+        // of this process, so the failing thread can flag their RCCL
+        // communicators too -- each rank's own thread then aborts its
+        // communicator at its next wait, which returns its stuck collectives)
+        const std::string why = std::string("worker ") + std::to_string(rank) + " failed: " + e.what();
+        for (distlr::KVWorker *p : *all)
+            if (p) p->Abort(why);
         std::lock_guard<std::mutex> g(g_out);
         std::cerr << "distlr: worker " << rank << ": " << e.what() << std::endl;
         (*failed)[(size_t)rank] = 1;
@@ -173,6 +181,7 @@ int main(int argc, char **argv) {
     }
 
     std::vector<int> failed((size_t)cfg.workers, 0);
+    std::vector<std::unique_ptr<distlr::LR>> models((size_t)cfg.workers);  // destroyed after every thread joined
     std::vector<std::thread> th;
     std::unique_ptr<distlr::ParamServer> ps;
     std::vector<distlr::KVWorker *> kvs((size_t)cfg.workers, nullptr);
@@ -215,7 +224,7 @@ int main(int argc, char **argv) {
         return 4;
     }
     for (int r = 0; r < cfg.workers; ++r)
-        th.emplace_back(run_worker, std::cref(cfg), r, kvs[(size_t)r], &failed);
+        th.emplace_back(run_worker, std::cref(cfg), r, kvs[(size_t)r], &kvs, &models[(size_t)r], &failed);
     for (auto &t : th) t.join();
     for (int f : failed)
         if (f) return 1;

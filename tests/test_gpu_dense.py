@@ -14,7 +14,7 @@ import pytest
 import distlr_amd as dlr
 import oracle
 from conftest import GOLDEN, read_golden_json
-from engine_driver import run_engine
+from engine_driver import run_engine, run_group
 from test_gpu_parity import assert_same_weights, compare_runs
 
 pytestmark = pytest.mark.gpu
@@ -354,3 +354,62 @@ def test_fused_dense_order_bitwise(monkeypatch, D, B, N):
         eng.close()
     want = _fused_order_gradient(X, y, oracle.batch_rows(N, B, 1), w0)
     assert_same_weights(got, want, "fused pushed gradient")
+
+
+# The banded reference-order launch (k_dense_ref, K6r: margin units and column
+# chains in one launch; C4's default).  DLR_DENSE_REF=1 forces it at small
+# sizes: slots of 256 rows with a ragged last slot, 32-row margin units,
+# wrapping batches, batches longer than the shard, a shard shorter than a slot,
+# the pushed gradient (world > 1 / parameter-server path) and streamed rows --
+# all bitwise the oracle (lr.cc:35-40, 108-113).
+@pytest.mark.parametrize("D,B,N", [(512, 300, 1000), (512, 1000, 700), (1024, 5000, 3000), (4096, 600, 1500),
+                                   (4096, 1500, 1500), (2048, 100, 100), (512, 33, 40), (640, 4096, 9000)])
+def test_dense_ref_banded_bitwise(monkeypatch, D, B, N):
+    monkeypatch.setenv("DLR_DENSE_REF", "1")
+    dd = dlr.DenseDataset.generate(N, D, seed=41, stream=1)
+    eng = run_engine([dd], D, 2, B, 0.2, dense=True)
+    orc = oracle.run_worker([dense_shard(dd)], D, 2, B, 0.2, sparse=False)
+    compare_runs(eng, orc)
+
+
+@pytest.mark.parametrize("W", [2, 3])
+def test_dense_ref_banded_ranks(monkeypatch, W):
+    # the pushed gradient (non-fused epilogue): the parameter-server topology
+    # and the loopback group's key-range exchange
+    monkeypatch.setenv("DLR_DENSE_REF", "1")
+    D = 1024
+    shards = [dlr.DenseDataset.generate(1200, D, seed=43, stream=r + 1) for r in range(W)]
+    orc = oracle.run_worker([dense_shard(s) for s in shards], D, 2, 700, 0.2, sparse=False)
+    got = run_engine(shards, D, 2, 700, 0.2, dense=True)
+    assert_same_weights(got.w, orc.w, "parameter-server topology")
+    grp = run_group(shards, D, 2, 700, 0.2, dense=True)
+    assert_same_weights(grp.w, orc.w, "loopback group")
+
+
+def test_dense_ref_banded_streamed(monkeypatch):
+    monkeypatch.setenv("DLR_DENSE_REF", "1")
+    D = 2048
+    dd = dlr.DenseDataset.generate(3000, D, seed=47, stream=1)
+    monkeypatch.setenv("DLR_RESIDENCY", "stream")
+    got = run_engine([dd], D, 3, 1300, 0.2, dense=True)
+    orc = oracle.run_worker([dense_shard(dd)], D, 3, 1300, 0.2, sparse=False)
+    assert_same_weights(got.w, orc.w)
+
+
+def test_dense_ref_default_for_c4_shape():
+    # the reference order picks the banded launch for C4-sized batches
+    D, B = 4096, 65536
+    dd = dlr.DenseDataset.generate(B + 1000, D, seed=10, stream=4)
+    X, y = dd.arrays()
+    w0 = dlr.init_weight(D)
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(w0)
+        assert eng.load_train_dense(dd, B) == 2 and eng.summation_order() == dlr.ORDER_REFERENCE
+        w = w0.copy()
+        for b in (0, 1, 1, 0):  # the second batch wraps to row 0
+            eng.train_step(b, 0.2, 1.0)
+            oracle.server_update(w, [oracle.grad_dense(X, y, oracle.batch_rows(len(y), B, b), w)], 0.2)
+            assert_same_weights(eng.get_weights(), w, f"C4 shape, batch {b}")
+    finally:
+        eng.close()
