@@ -1703,9 +1703,24 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
         int64_t first;
         hipError_t e = dense_batch(c, b, &dd, &first);
         if (e == hipSuccess && t.dref) {
-            const dlr::DevRefSync sy{t.dref_sync, t.dref_sync + dlr::dense_ref_sync_words(B) - 64,
-                                     t.dref_sync + dlr::dense_ref_sync_words(B) - 32, t.dref_seq, t.dref_lead};
-            e = dlr::launch_dense_ref(dd, first, B, c->w, gout, c->resid, sy, lr, C, fused, c->stream);
+            // the chains on the engine stream, the margins on the second
+            // stream: both after everything queued so far (the previous
+            // step's update of w), and the engine stream past the margins
+            // before its next work
+            if (!c->gstream) {
+                e = hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking);
+                if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_bstart, hipEventDisableTiming);
+                if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_bdone, hipEventDisableTiming);
+            }
+            const int64_t nw = dlr::dense_ref_sync_words(B);
+            const dlr::DevRefSync sy{t.dref_sync, t.dref_sync + nw - 64, t.dref_sync + nw - 32, t.dref_seq,
+                                     t.dref_lead, 0};
+            if (e == hipSuccess) e = hipEventRecord(c->ev_bstart, c->stream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(c->gstream, c->ev_bstart, 0);
+            if (e == hipSuccess)
+                e = dlr::launch_dense_ref(dd, first, B, c->w, gout, c->resid, sy, lr, C, fused, c->stream, c->gstream);
+            if (e == hipSuccess) e = hipEventRecord(c->ev_bdone, c->gstream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_bdone, 0);
             if (e == hipSuccess) ++c->train.dref_seq;
         } else if (e == hipSuccess)
             e = t.dfused ? dlr::launch_dense_combine(t.dpart, c->D, B, c->w, gout, lr, C, fused, c->stream)
@@ -2780,8 +2795,11 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
         // margin kernel, then the column-chain kernel -- the same order)
         const char *dr = getenv("DLR_DENSE_REF");
         t.dref = dlr::dense_ref_ok(D, ds->n_rows, t.B) && (dr ? strcmp(dr, "0") != 0 : big);
-        const char *dl = getenv("DLR_DENSE_REF_LEAD");  // A/B: margin throttle in 256-row slots (0 = off)
-        t.dref_lead = dl ? atoi(dl) : 0;
+        // how far (in 256-row slots) the margins may run ahead of the column
+        // chains: the rows the chains re-read stay in the Infinity Cache
+        // (DLR_DENSE_REF_LEAD: A/B; 0 = no limit)
+        const char *dl = getenv("DLR_DENSE_REF_LEAD");
+        t.dref_lead = dl ? atoi(dl) : 32;
     }
     t.fast = t.dblocked;
     // Residency: device-resident unless asked to stream, or (auto) the rows

@@ -182,14 +182,15 @@ struct DevDense {
 
 // K6r (k_dense_ref) hand-off state, device words of the loaded shard
 // (zeroed at load): per chain slot of 256 rows the count of its 32-row
-// margin units published, the margin unit queue head, the chains' progress
-// (for the throttle); all monotonic over the launches of the shard (seq).
+// margin units published, and the margin unit queue head; both monotonic
+// over the launches of the shard (seq = launches so far).
 struct DevRefSync {
     uint32_t *slot_cnt;
     uint32_t *head;
-    uint32_t *prog;
+    uint32_t *limit;  // the margins' limit in queue positions, published by chain workgroup 0
     uint32_t seq;
-    int lead;  // margin throttle: units claimed at most `lead` slots ahead of the chains (0: off)
+    int lead;         // slots the margins may run ahead of the chains (0: no limit)
+    int mgrid;        // margin workgroups (set by launch_dense_ref)
 };
 
 // Batch size of every rank (the L2 term of rank r's push is
@@ -281,8 +282,13 @@ hipError_t launch_dense_combine(const float *part, int64_t D, int64_t B, float *
 bool dense_ref_ok(int64_t D, int64_t N, int64_t B);
 int64_t dense_ref_sync_words(int64_t B);
 int64_t dense_ref_resid(int64_t B);
+int dense_ref_grid(int64_t D, int64_t B);  // chain + margin workgroups (the stamps tool's buffer)
+// The chains go on chain_s, the margins on margin_s (the caller orders the
+// two streams: both start after the previous step, and chain_s waits for
+// the margins before its next work).
 hipError_t launch_dense_ref(const DevDense &dd, int64_t first, int64_t B, float *w, float *gout, float *resid,
-                            const DevRefSync &sy, float lr, float C, bool fused, hipStream_t s);
+                            const DevRefSync &sy, float lr, float C, bool fused, hipStream_t chain_s,
+                            hipStream_t margin_s);
 int predict_dense_grid(int64_t rows);
 hipError_t launch_dense_predict(const DevDense &dd, const float *w, unsigned long long *correct, double *ll_part,
                                 double *ll_out, hipStream_t s);

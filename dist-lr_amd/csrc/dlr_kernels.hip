@@ -826,9 +826,39 @@ namespace {
     do {                                                                                     \
         if (threadIdx.x == 0) g_stamp[blockIdx.x * 16 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+// k_dense_ref: 64 slots per workgroup, written by one chosen lane
+#define DLR_STAMP64(slot, cond)                                                                      \
+    do {                                                                                             \
+        if (cond) g_stamp[blockIdx.x * 64 + (slot)] = __builtin_amdgcn_s_memrealtime();               \
+    } while (0)
+#define DLR_STAMP64V(slot, cond, v)                                                                  \
+    do {                                                                                             \
+        if (cond) g_stamp[blockIdx.x * 64 + (slot)] = (v);                                           \
+    } while (0)
+// (the margin launch's workgroups: rows 256 + blockIdx.x)
+#define DLR_STAMP64M(slot, cond)                                                                     \
+    do {                                                                                             \
+        if (cond) g_stamp[(256 + blockIdx.x) * 64 + (slot)] = __builtin_amdgcn_s_memrealtime();      \
+    } while (0)
+#define DLR_STAMP64MV(slot, cond, v)                                                                 \
+    do {                                                                                             \
+        if (cond) g_stamp[(256 + blockIdx.x) * 64 + (slot)] = (v);                                   \
+    } while (0)
 #else
 #define DLR_STAMP(slot) \
     do {                \
+    } while (0)
+#define DLR_STAMP64(slot, cond) \
+    do {                        \
+    } while (0)
+#define DLR_STAMP64V(slot, cond, v) \
+    do {                            \
+    } while (0)
+#define DLR_STAMP64M(slot, cond) \
+    do {                         \
+    } while (0)
+#define DLR_STAMP64MV(slot, cond, v) \
+    do {                             \
     } while (0)
 #endif
 // Timing-only ablations of the stamps build (tools/c2_stamps.py; WRONG
@@ -2517,55 +2547,56 @@ __global__ __launch_bounds__(256) void k_dense_combine(const float *__restrict__
 }
 
 // ---------------------------------------------------------------------------
-// K6r: the dense step in the REFERENCE order as ONE banded launch (C4's
+// K6r: the dense step in the REFERENCE order as two concurrent launches (C4's
 // default).  lr.cc's arithmetic is two families of serial fp32 chains: every
 // margin z_i is a chain over the columns in order (lr.cc:108-112), every
 // gradient G_j a chain over the batch rows in order (lr.cc:35-39), and a row
 // can enter the column chains only once its own chain is done.  A column
 // chain of B = 65,536 dependent adds is the floor (8.3 cycles each on
-// gfx950, profiles/r04_kbench_chain2.txt: ~0.23 ms), so the launch is built
+// gfx950, profiles/r04_kbench_chain2.txt: ~0.23 ms), so the step is built
 // around keeping every column chain busy from its first row to its last:
 //
-//   chain workgroups (blockIdx < nstripes; one 16-column stripe each):
+//   k_dense_ref_chain (one workgroup per 16-column stripe, 35 KB of LDS):
 //     wave 0    lane c runs column c's chain over slot t-1's products (LDS,
 //               16-byte reads, 256 rows per slot) -- its only work;
 //     waves 1-2 load slot t's 256 rows x 16 columns into registers (three
 //               slots in flight: the rows were read from HBM moments ago by
 //               the margin workgroups and come back from the Infinity
 //               Cache), form fl32(r_i * x_ij) and store them transposed;
-//     wave 3    waits until the margins of slot t+2 are published, then
-//               loads those residuals (sc1: written by other CUs).
-//   margin workgroups (the rest; one per CU): claim units of 32 batch rows
-//     in row order from a queue (so rows finish in order and any resident
-//     subset of workgroups drains it), stream the unit's rows through an
-//     LDS ring by LDS-DMA (waves 1-3) while lane i of wave 0 runs row i's
-//     chain in column order; publish sigma - y with sc1 stores and one
-//     agent-scope add to the slot's counter (MI355X_MICROARCH.md,
-//     inter-workgroup hand-off, the sc1 row).
+//     wave 3    loads the residuals of slot t+3 once its margins are
+//               published (sc1: written by other CUs); workgroup 0's also
+//               publishes the margins' LIMIT: `lead` slots past its own
+//               progress, so the rows the chains re-read are still in the
+//               Infinity Cache;
+//   k_dense_ref_margin (one workgroup per CU, a 112 KB LDS ring), on a second
+//     stream: claims units of 32 batch rows in row order from a queue (rows
+//     finish in order, and any resident subset of workgroups drains it),
+//     waits for the limit before it starts a unit (holding only later
+//     units: no chain waits on it), streams the unit's rows through the
+//     ring by LDS-DMA (waves 1-3, six stages in flight) while lane i of
+//     wave 0 runs row i's chain in column order; publishes sigma - y with
+//     sc1 stores and one agent-scope add to the slot's counter
+//     (MI355X_MICROARCH.md, inter-workgroup hand-off, the sc1 row).
 //
 // The weights are written only by the chain epilogue, after its last slot:
-// by then every unit -- every read of w -- is done.  Counters are monotonic
-// over launches (sy.seq), so nothing is reset between steps.  Every wait is
-// bounded (kRefSpin polls): a launch whose producers never come runs to the
-// end with wrong sums instead of hanging the GPU.  X is read once from HBM
-// (the margins) and once from the Infinity Cache (the chains).
+// by then every unit -- every read of w -- is done.  Counters and the queue
+// are monotonic over launches (sy.seq), so nothing is reset between steps.
+// Every wait is bounded (kRefSpin polls): a launch whose producers never
+// come runs to the end with wrong sums instead of hanging the GPU.  X is
+// read once from HBM (the margins) and once from the Infinity Cache (the
+// chains).
 constexpr int kRefCols = 16;     // columns per chain workgroup
 constexpr int kRefSlot = 256;    // batch rows per chain slot
 constexpr int kRefUnit = 32;     // batch rows per margin unit (one lane each)
 constexpr int kRefStage = 128;   // columns per margin stage
-constexpr int kRefRing = 4;      // margin stages in the LDS ring (3 in flight)
+constexpr int kRefRing = 7;      // margin stages in the LDS ring (up to 6 in flight)
 constexpr int kRefPad = kRefSlot + 4;
 constexpr int kRefThreads = 256;
 constexpr uint32_t kRefNone = 0xFFFFFFFFu;
 constexpr int kRefSpin = 1 << 22;
-constexpr size_t kRefLds = (size_t)kRefRing * kRefUnit * kRefStage * 4 + 64;  // the margin ring (> chain's 35 KB)
-static_assert((size_t)(2 * kRefCols * kRefPad + 2 * kRefSlot) * 4 <= kRefLds, "chain LDS within the launch's");
-
-__device__ __forceinline__ uint32_t ld_sc1_u32(const uint32_t *p) {
-    uint32_t v;
-    asm volatile("global_load_dword %0, %1, off sc1\n s_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
+constexpr size_t kRefChainLds = (size_t)(2 * kRefCols * kRefPad + 2 * kRefSlot) * 4;
+constexpr size_t kRefMarginLds = (size_t)kRefRing * kRefUnit * kRefStage * 4 + 64;
+static_assert(kRefChainLds + kRefMarginLds <= 160 * 1024, "one chain and one margin workgroup per CU");
 
 // Shard row (first + i) mod N of batch row i: the launch needs B <= N
 // (dense_ref_ok), so first + i < 2N and one subtraction wraps it
@@ -2592,177 +2623,215 @@ __device__ __forceinline__ void ref_rd8(v4f (&d)[8], uint32_t a) {
     asm volatile("s_waitcnt lgkmcnt(" #N ")"                                                                 \
                  : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]), "+v"(d[6]), "+v"(d[7]))
 
-// w: read by the margin role (through wr, a read-only view: scalar loads)
-// and written only by the chain epilogue after every margin is done.
+// The queue position (claims so far) at the start of launch seq: every
+// launch makes nunits successful claims and one failed claim per margin
+// workgroup.
+__device__ __forceinline__ uint32_t ref_base(const DevRefSync &sy, int64_t nunits) {
+    return sy.seq * (uint32_t)(nunits + sy.mgrid);
+}
+
 template <bool FUSED>
-__global__ __launch_bounds__(kRefThreads) void k_dense_ref(DevDense dd, int64_t first, int64_t B,
-                                                           const float *__restrict__ wr, float *w,
-                                                           float *__restrict__ gout, float *resid, DevRefSync sy,
-                                                           int nstripes, float Bf, double Bd, float lr, float C) {
+__global__ __launch_bounds__(kRefThreads) void k_dense_ref_chain(DevDense dd, int64_t first, int64_t B, float *w,
+                                                                 float *__restrict__ gout, float *resid, DevRefSync sy,
+                                                                 float Bf, double Bd, float lr, float C) {
     extern __shared__ __attribute__((aligned(16))) float rsm[];
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int64_t D = dd.D, N = dd.N;
     const int64_t nslot = (B + kRefSlot - 1) / kRefSlot;
     const int64_t nunits = (B + kRefUnit - 1) / kRefUnit;
-    if ((int)blockIdx.x < nstripes) {
-        // ------------------------------------------------------ chain role
-        float *s_p = rsm;                              // [2][kRefCols][kRefPad]
-        float *s_r = rsm + 2 * kRefCols * kRefPad;     // [2][kRefSlot]
-        unsigned cg = blockIdx.x;
-        if ((nstripes & 15) == 0) {  // stripes 2m, 2m+1 (one 128-byte line of a row) on one XCD
-            const unsigned k = blockIdx.x >> 3;
-            cg = ((k >> 1) << 4) | ((blockIdx.x & 7) << 1) | (k & 1);
+    const int nstripes = (int)gridDim.x;
+    float *s_p = rsm;                              // [2][kRefCols][kRefPad]
+    float *s_r = rsm + 2 * kRefCols * kRefPad;     // [2][kRefSlot]
+    unsigned cg = blockIdx.x;
+    if ((nstripes & 15) == 0) {  // stripes 2m, 2m+1 (one 128-byte line of a row) on one XCD
+        const unsigned k = blockIdx.x >> 3;
+        cg = ((k >> 1) << 4) | ((blockIdx.x & 7) << 1) | (k & 1);
+    }
+    const int64_t c0 = (int64_t)cg * kRefCols;
+    // helpers: lane hl in [0, 128) owns 4x4 blocks b = hl, hl + 128 of the
+    // slot (row quad b >> 2, column quad b & 3)
+    const int hl = (wv - 1) * kWave + lane;
+    auto load = [&](int64_t t, v4f (&x)[8]) {
+        const int64_t tc = t < nslot ? t : nslot - 1;  // past the end: the last slot again (never used)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int b = hl + 128 * h;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t i = min<int64_t>(tc * kRefSlot + 4 * (b >> 2) + u, B - 1);
+                x[4 * h + u] = __builtin_nontemporal_load(
+                    reinterpret_cast<const v4f *>(dd.X + ref_row(first, i, N) * D + c0 + 4 * (b & 3)));
+            }
         }
-        const int64_t c0 = (int64_t)cg * kRefCols;
-        // helpers: lane hl in [0, 128) owns 4x4 blocks b = hl, hl + 128 of the
-        // slot (row quad b >> 2, column quad b & 3)
-        const int hl = (wv - 1) * kWave + lane;
-        auto load = [&](int64_t t, v4f (&x)[8]) {
-            const int64_t tc = t < nslot ? t : nslot - 1;  // past the end: the last slot again (never used)
+    };
+    auto transform = [&](int64_t t, const v4f (&x)[8]) {
+        const float *sr = s_r + (t & 1) * kRefSlot;
+        float *sp = s_p + (t & 1) * kRefCols * kRefPad;
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int b = hl + 128 * h;
+        for (int h = 0; h < 2; ++h) {
+            const int b = hl + 128 * h, rq = b >> 2, cq = b & 3;
+            const v4f r4 = *reinterpret_cast<const v4f *>(sr + 4 * rq);
+            const float rr[4] = {r4.x, r4.y, r4.z, r4.w};
+            float p[4][4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int64_t i = min<int64_t>(tc * kRefSlot + 4 * (b >> 2) + u, B - 1);
-                    x[4 * h + u] = __builtin_nontemporal_load(
-                        reinterpret_cast<const v4f *>(dd.X + ref_row(first, i, N) * D + c0 + 4 * (b & 3)));
-                }
+            for (int u = 0; u < 4; ++u) {
+                const bool ok = t * kRefSlot + 4 * rq + u < B;  // rows past B: +0 (never -0 in a sum from +0)
+                const v4f xv = x[4 * h + u];
+                p[u][0] = ok ? rr[u] * xv.x : 0.0f;
+                p[u][1] = ok ? rr[u] * xv.y : 0.0f;
+                p[u][2] = ok ? rr[u] * xv.z : 0.0f;
+                p[u][3] = ok ? rr[u] * xv.w : 0.0f;
             }
-        };
-        auto transform = [&](int64_t t, const v4f (&x)[8]) {
-            const float *sr = s_r + (t & 1) * kRefSlot;
-            float *sp = s_p + (t & 1) * kRefCols * kRefPad;
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int b = hl + 128 * h, rq = b >> 2, cq = b & 3;
-                const v4f r4 = *reinterpret_cast<const v4f *>(sr + 4 * rq);
-                const float rr[4] = {r4.x, r4.y, r4.z, r4.w};
-                float p[4][4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const bool ok = t * kRefSlot + 4 * rq + u < B;  // rows past B: +0 (never -0 in a sum from +0)
-                    const v4f xv = x[4 * h + u];
-                    p[u][0] = ok ? rr[u] * xv.x : 0.0f;
-                    p[u][1] = ok ? rr[u] * xv.y : 0.0f;
-                    p[u][2] = ok ? rr[u] * xv.z : 0.0f;
-                    p[u][3] = ok ? rr[u] * xv.w : 0.0f;
-                }
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    *reinterpret_cast<v4f *>(sp + (4 * cq + q) * kRefPad + 4 * rq) =
-                        v4f{p[0][q], p[1][q], p[2][q], p[3][q]};
-            }
-        };
-        // wave 3: the residuals of slot t, once every unit of it is published
-        auto slot_target = [&](int64_t t) -> uint32_t {
-            const int64_t rows = min<int64_t>(kRefSlot, B - t * kRefSlot);
-            const uint32_t units = (uint32_t)((rows + kRefUnit - 1) / kRefUnit);
-            return units * (sy.seq + 1);
-        };
-        auto r_issue = [&](int64_t t, v4f &rv) {
-            const uint32_t want = slot_target(t);
-            for (int k = 0; k < kRefSpin && ld_sc1_u32(sy.slot_cnt + t) < want; ++k) __builtin_amdgcn_s_sleep(1);
-            const float *src = resid + t * kRefSlot + 4 * lane;  // resid holds whole slots (+4)
-            asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(rv) : "v"(src) : "memory");
-        };
-        auto r_store = [&](int64_t t, v4f &rv) {
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(rv)::"memory");
-            *reinterpret_cast<v4f *>(s_r + (t & 1) * kRefSlot + 4 * lane) = rv;
-        };
-        float acc = 0.0f;
-        auto chain = [&](int64_t t) {
-            const float *sp = s_p + (t & 1) * kRefCols * kRefPad + (lane & (kRefCols - 1)) * kRefPad;
+            for (int q = 0; q < 4; ++q)
+                *reinterpret_cast<v4f *>(sp + (4 * cq + q) * kRefPad + 4 * rq) = v4f{p[0][q], p[1][q], p[2][q], p[3][q]};
+        }
+    };
+    // wave 3: the residuals of slot t, once every unit of it is published
+    auto slot_target = [&](int64_t t) -> uint32_t {
+        const int64_t rows = min<int64_t>(kRefSlot, B - t * kRefSlot);
+        const uint32_t units = (uint32_t)((rows + kRefUnit - 1) / kRefUnit);
+        return units * (sy.seq + 1);
+    };
+    // wave 3's view of the margins: every slot <= ready is published.
+    // Waiting for a slot polls its counter from ONE lane, a microsecond
+    // apart (hundreds of CUs polling flat out take HBM bandwidth from the
+    // margins they wait for); once it is published, one 64-lane poll of the
+    // next 64 counters extends `ready`, so while the margins run ahead a
+    // round trip is paid once per 64 slots.  Loads and stores go through the
+    // buffer path with sc1 (aux 16): L2-coherent, and tracked by the
+    // compiler's waits.
+    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(sy.slot_cnt, 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(resid, 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc(sy.limit, 0, 0x7FFFFFFF, 0x00020000);
+    const bool leader = blockIdx.x == 0 && sy.lead > 0;
+    const uint32_t qbase = ref_base(sy, nunits);
+    auto publish_limit = [&](int64_t t) {  // workgroup 0, wave 3, lane 0
+        const int64_t lim = min<int64_t>(nunits, (t + sy.lead) * (kRefSlot / kRefUnit));
+        if (lane == 0) __builtin_amdgcn_raw_buffer_store_b32(qbase + (uint32_t)lim, lrs, 0, 0, 16);
+    };
+    int64_t ready = -1;
+    auto poll_from = [&](int64_t t0) {
+        const uint32_t want0 = slot_target(t0);
+        for (int k = 0; k < kRefSpin; ++k) {
+            const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(crs, (int)(t0 * 4), 0, 16);
+            if (v >= want0) break;
+            __builtin_amdgcn_s_sleep(32);
+        }
+        const int64_t sl = min<int64_t>(t0 + lane, nslot - 1);
+        const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(crs, (int)(sl * 4), 0, 16);
+        const bool ok = t0 + lane >= nslot || v >= slot_target(sl);
+        const unsigned long long bad = ~__ballot(ok) | 1ull << 63;  // (lane 63: not counted past it)
+        const int first_bad = __ffsll((long long)bad) - 1;
+        ready = t0 + max(first_bad, 1) - 1;  // t0 itself is published (or the bounded wait ran out)
+    };
+    // residuals of slot t, once published
+    auto r_issue = [&](int64_t t, v4f &rv) {
+        const int64_t tc = t < nslot ? t : nslot - 1;  // past the end: a load of a published slot, unused
+        if (tc > ready) poll_from(tc);
+        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rrs, (int)((tc * kRefSlot + 4 * lane) * 4), 0, 16);
+        __builtin_memcpy(&rv, &q, 16);
+    };
+    auto r_store = [&](int64_t t, const v4f &rv) { *reinterpret_cast<v4f *>(s_r + (t & 1) * kRefSlot + 4 * lane) = rv; };
+    float acc = 0.0f;
+    auto chain = [&](int64_t t) {
+        const float *sp = s_p + (t & 1) * kRefCols * kRefPad + (lane & (kRefCols - 1)) * kRefPad;
 #pragma unroll 2
-            for (int k = 0; k < kRefSlot; k += 32) {
-                v4f d[8];
+        for (int k = 0; k < kRefSlot; k += 32) {
+            v4f d[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) d[u] = *reinterpret_cast<const v4f *>(sp + k + 4 * u);
+            for (int u = 0; u < 8; ++u) d[u] = *reinterpret_cast<const v4f *>(sp + k + 4 * u);
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    acc = acc + d[u].x;
-                    acc = acc + d[u].y;
-                    acc = acc + d[u].z;
-                    acc = acc + d[u].w;
-                }
+            for (int u = 0; u < 8; ++u) {
+                acc = acc + d[u].x;
+                acc = acc + d[u].y;
+                acc = acc + d[u].z;
+                acc = acc + d[u].w;
             }
-        };
-        v4f xa[8], xb[8], xc[8], rv;
-        if (wv == 3) {
-            r_issue(0, rv);
-            r_store(0, rv);
-            if (nslot > 1) r_issue(1, rv);
-        } else if (wv >= 1) {
-            load(0, xa);
-            load(1, xb);
-            load(2, xc);
+        }
+    };
+    v4f xa[8], xb[8], xc[8], ra, rb, rc;
+    DLR_STAMP64(0, threadIdx.x == 0);
+    if (wv == 3) {
+        if (leader) publish_limit(0);
+        r_issue(0, ra);
+        r_issue(1, rb);
+        r_issue(2, rc);
+        r_store(0, ra);
+    } else if (wv >= 1) {
+        load(0, xa);
+        load(1, xb);
+        load(2, xc);
+    }
+    lds_barrier();
+    DLR_STAMP64(1, threadIdx.x == 0);
+    // iteration t: wave 0 adds slot t-1; waves 1-2 transform slot t and
+    // reload its registers with slot t+3; wave 3 stores slot t+1's residuals
+    // (loaded two iterations ago) and issues slot t+3's
+    auto step = [&](int64_t t, v4f (&x)[8], v4f &rnext, v4f &rfree) {
+        if (wv == 0) {
+            if (t >= 1) chain(t - 1);
+        } else if (wv <= 2) {
+            if (t < nslot) {
+                transform(t, x);
+                load(t + 3, x);
+            }
+        } else {
+            r_store(t + 1, rnext);  // (past the last slot: an unused write of a free buffer)
+            r_issue(t + 3, rfree);
+            if (leader) publish_limit(t);
         }
         lds_barrier();
-        // iteration t: wave 0 adds slot t-1; waves 1-2 transform slot t and
-        // reload its registers with slot t+3; wave 3 stores slot t+1's
-        // residuals and fetches slot t+2's
-        auto step = [&](int64_t t, v4f (&x)[8]) {
-            if (wv == 0) {
-                if (t >= 1) chain(t - 1);
-            } else if (wv <= 2) {
-                if (t < nslot) {
-                    transform(t, x);
-                    load(t + 3, x);
-                }
-            } else if (t + 1 < nslot) {
-                r_store(t + 1, rv);
-                if (t + 2 < nslot) r_issue(t + 2, rv);
-                if (blockIdx.x == 0 && lane == 0 && sy.lead > 0) {
-                    uint32_t *pg = sy.prog;
-                    const uint32_t pv = (uint32_t)t + sy.seq * 65536u;
-                    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(pg), "v"(pv) : "memory");
-                }
-            }
-            lds_barrier();
-        };
-        for (int64_t t = 0; t <= nslot; t += 3) {
-            step(t, xa);
-            if (t + 1 <= nslot) step(t + 1, xb);
-            if (t + 2 <= nslot) step(t + 2, xc);
-        }
-        if (wv != 0) return;
-        const int64_t j = c0 + lane;
-        if (lane >= kRefCols || j >= D) return;
-        const float wj = w[j];
-        const float cw = C * wj;
-        const float l2 = cw / Bf;
-        const float g = (float)((double)acc / Bd + (double)l2);
-        if (FUSED) {
-            const float stepv = lr * g;
-            w[j] = wj - stepv;
-        } else {
-            gout[j] = g;
-        }
-        return;
+        DLR_STAMP64(2 + (int)(t >> 4), threadIdx.x == 0 && (t & 15) == 0 && t < 16 * 40);
+    };
+    for (int64_t t = 0; t <= nslot; t += 3) {
+        step(t, xa, rb, ra);
+        if (t + 1 <= nslot) step(t + 1, xb, rc, rb);
+        if (t + 2 <= nslot) step(t + 2, xc, ra, rc);
     }
-    // ---------------------------------------------------------- margin role
-    float *ring = rsm;                                                   // [kRefRing][16 x 2 x 32][16 B]
+    DLR_STAMP64(50, threadIdx.x == 0);
+    if (wv != 0) return;
+    const int64_t j = c0 + lane;
+    if (lane >= kRefCols || j >= D) return;
+    const float wj = w[j];
+    const float cw = C * wj;
+    const float l2 = cw / Bf;
+    const float g = (float)((double)acc / Bd + (double)l2);
+    if (FUSED) {
+        const float stepv = lr * g;
+        w[j] = wj - stepv;
+    } else {
+        gout[j] = g;
+    }
+}
+
+// LA: stages a loader keeps in flight ahead of the one computed (6; 3 when
+// a unit has fewer than 7 stages, D < 896, so that the loaders never need a
+// unit two ahead).  w: read-only here (the chains update it after every
+// margin is published).
+template <int LA>
+__global__ __launch_bounds__(kRefThreads) void k_dense_ref_margin(DevDense dd, int64_t first, int64_t B,
+                                                                  const float *__restrict__ wr, float *resid,
+                                                                  DevRefSync sy) {
+    extern __shared__ __attribute__((aligned(16))) float rsm[];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t D = dd.D, N = dd.N;
+    const int64_t nunits = (B + kRefUnit - 1) / kRefUnit;
+    float *ring = rsm;  // [kRefRing][16 x 2 x 32][16 B]
     uint32_t *s_unit = reinterpret_cast<uint32_t *>(rsm + kRefRing * kRefUnit * kRefStage);  // [4]
-    const int M = (int)gridDim.x - nstripes;
     const int spu = (int)(D / kRefStage);  // stages per unit (>= 4)
-    const uint32_t base = sy.seq * (uint32_t)(nunits + M);
+    const uint32_t base = ref_base(sy, nunits);
+    const __amdgpu_buffer_rsrc_t rres = __builtin_amdgcn_make_buffer_rsrc(resid, 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc(sy.limit, 0, 0x7FFFFFFF, 0x00020000);
     // claims: unit ids in row order; after the first failed claim none more
     // (so every workgroup fails exactly once and the head advances by
-    // nunits + M per launch)
+    // nunits + mgrid per launch)
     bool claiming = true;
-    // lane 0 of wave 0: the throttle, then the claim's atomic (its result is
-    // used only at the end of the unit, when the wave drains anyway)
+    // lane 0 of wave 0: the claim's atomic (its result is used only at the
+    // end of the unit, when the wave drains anyway)
     auto claim_issue = [&]() -> uint32_t {
-        if (sy.lead > 0) {  // stay within `lead` slots of the chains' progress
-            for (int k = 0; k < kRefSpin / 64; ++k) {
-                const uint32_t nu = ld_sc1_u32(sy.head) - base;
-                const uint32_t pg = ld_sc1_u32(sy.prog);
-                const uint32_t done = pg >= sy.seq * 65536u ? pg - sy.seq * 65536u : 0u;
-                if (nu / (kRefSlot / kRefUnit) <= done + (uint32_t)sy.lead) break;
-                __builtin_amdgcn_s_sleep(8);
-            }
-        }
         return __hip_atomic_fetch_add(sy.head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     auto claim_finish = [&](uint32_t raw) -> uint32_t {
@@ -2773,6 +2842,7 @@ __global__ __launch_bounds__(kRefThreads) void k_dense_ref(DevDense dd, int64_t 
         }
         return u;
     };
+    DLR_STAMP64M(0, threadIdx.x == 0);
     if (wv == 0 && lane == 0) {
         const uint32_t u0 = claim_finish(claim_issue());
         const uint32_t u1 = claiming ? claim_finish(claim_issue()) : kRefNone;
@@ -2782,45 +2852,61 @@ __global__ __launch_bounds__(kRefThreads) void k_dense_ref(DevDense dd, int64_t 
         s_unit[3] = kRefNone;
     }
     __syncthreads();
-    // loaders: stage g of this workgroup's unit sequence into ring[g % 4]:
-    // 16 LDS-DMA pieces of 1 KiB, piece k = columns [8k, 8k + 8) of the
-    // stage for the unit's 32 rows (lane l: row l & 31, 16-byte half l >> 5)
-    const int lw = wv - 1;                         // loader 0..2: pieces lw, lw + 3, ...
-    const int npieces = lw == 0 ? 6 : 5;           // of the 16 (6 + 5 + 5)
+    // loaders: stage g of this workgroup's unit sequence into ring[g % 7]:
+    // 16 LDS-DMA pieces of 1 KiB, piece p = columns [8p, 8p + 8) of the stage
+    // for the unit's 32 rows (lane l: row l & 31, 16-byte half l >> 5)
+    const int lw = wv - 1;                // loader 0..2: pieces lw, lw + 3, ...
+    const int npieces = lw == 0 ? 6 : 5;  // of the 16 (6 + 5 + 5)
     // stage (k, sg): unit slot k of this workgroup's sequence, stage sg of it
-    auto issue = [&](int k, int sg, int g) {
+    auto issue = [&](int k, int sg, int ri) {
         const uint32_t u = s_unit[k & 3];
         const int64_t col0 = (int64_t)sg * kRefStage;
         int64_t i = (int64_t)(u == kRefNone ? 0 : u) * kRefUnit + (lane & 31);
         i = min(i, B - 1);
         const int64_t row = ref_row(first, i, N);
         const float *src = dd.X + row * D + col0 + 4 * (lane >> 5);
-        float *dst = ring + (size_t)(g & (kRefRing - 1)) * kRefUnit * kRefStage;
+        float *dst = ring + (size_t)ri * kRefUnit * kRefStage;
         for (int p = lw; p < 16; p += 3)
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + 8 * p),
                                              (__attribute__((address_space(3))) void *)(dst + p * 256), 16, 0, 0);
     };
     if (wv >= 1) {
-        issue(0, 0, 0);
-        issue(0, 1, 1);
-        issue(0, 2, 2);
+#pragma unroll
+        for (int s0 = 0; s0 < LA; ++s0) issue(0, s0, s0);
     }
     float z = 0.0f, y = 0.0f;
-    int64_t urow = -1;    // batch row of this lane in the current unit (-1: none)
-    uint32_t pend = 0;    // lane 0: the raw claim issued at the start of the unit
+    int64_t urow = -1;  // batch row of this lane in the current unit (-1: none)
+    uint32_t pend = 0;  // lane 0: the raw claim issued at the start of the unit
     bool have_pend = false;
-    for (int g = 0, k = 0, sg = 0;; ++g) {
+    DLR_STAMP64M(1, threadIdx.x == 0);
+    for (int k = 0, sg = 0, ri = 0;;) {
         const uint32_t u = s_unit[k & 3];
         if (u == kRefNone) break;  // uniform: every wave read the same LDS word after the last barrier
-        if (wv >= 1) {  // stage g landed (stages g + 1, g + 2 still in flight)
-            if (npieces == 6)
-                asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+        if (wv >= 1) {  // stage g landed (the LA - 1 later stages still in flight)
+            if (LA == 6) {
+                if (npieces == 6)
+                    asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(25)" ::: "memory");
+            } else {
+                if (npieces == 6)
+                    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+            }
         }
         lds_barrier();
         if (wv == 0) {
             if (sg == 0) {
+                // the margins' limit: start unit u only once the chains are
+                // within `lead` slots of it (every unit this workgroup still
+                // holds is later: nothing a chain waits for is held here)
+                if (sy.lead > 0 && lane == 0)
+                    for (int s = 0; s < kRefSpin; ++s) {
+                        const uint32_t lim = __builtin_amdgcn_raw_buffer_load_b32(lrs, 0, 0, 16);
+                        if ((int32_t)(lim - (base + u)) > 0) break;
+                        __builtin_amdgcn_s_sleep(16);
+                    }
                 urow = lane < kRefUnit && (int64_t)u * kRefUnit + lane < B ? (int64_t)u * kRefUnit + lane : -1;
                 if (urow >= 0) y = dd.label[ref_row(first, urow, N)];
                 z = 0.0f;
@@ -2828,10 +2914,10 @@ __global__ __launch_bounds__(kRefThreads) void k_dense_ref(DevDense dd, int64_t 
                 if (have_pend) pend = claim_issue();  // the unit after the next one
             }
             if (lane < kRefUnit) {
-                // row chain over the stage's 128 columns in order: 4 groups
-                // of 8 reads (piece p, half h -> columns 8p + 4h .. + 3),
-                // the next group in flight while this one is added
-                const uint32_t a0 = lds_addr(ring + (size_t)(g & (kRefRing - 1)) * kRefUnit * kRefStage) + 16 * lane;
+                // row chain over the stage's 128 columns in order: 4 groups of
+                // 8 reads (piece p, half h -> columns 8p + 4h .. + 3), the next
+                // group in flight while this one is added
+                const uint32_t a0 = lds_addr(ring + (size_t)ri * kRefUnit * kRefStage) + 16 * lane;
                 const float *__restrict__ wp = wr + sg * kRefStage;
                 v4f xa[8], xb[8];
                 auto grp = [&](const v4f(&x)[8], int gi) {
@@ -2860,8 +2946,7 @@ __global__ __launch_bounds__(kRefThreads) void k_dense_ref(DevDense dd, int64_t 
             if (sg == spu - 1) {
                 if (urow >= 0) {
                     const float r = sigmoid_ref(z) - y;
-                    float *dst = resid + urow;
-                    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(dst), "v"(r) : "memory");
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), rres, (int)(urow * 4), 0, 16);  // sc1
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every residual of the unit stored
                 if (lane == 0) {
@@ -2869,19 +2954,24 @@ __global__ __launch_bounds__(kRefThreads) void k_dense_ref(DevDense dd, int64_t 
                                            __HIP_MEMORY_SCOPE_AGENT);
                     s_unit[(k + 2) & 3] = have_pend ? claim_finish(pend) : kRefNone;
                 }
+                DLR_STAMP64M(2 + k, lane == 0 && k < 40);
+                DLR_STAMP64MV(44 + k, lane == 0 && k < 16, (unsigned long long)u);
             }
         } else {
-            const int s3 = sg + 3;
-            if (s3 < spu)
-                issue(k, s3, g + 3);
-            else
-                issue(k + 1, s3 - spu, g + 3);
+            int sa = sg + LA, ka = k;  // the stage LA ahead (its ring slot was computed 7 - LA stages ago)
+            if (sa >= spu) {
+                sa -= spu;
+                ++ka;
+            }
+            issue(ka, sa, ri + LA < kRefRing ? ri + LA : ri + LA - kRefRing);
         }
         if (++sg == spu) {
             sg = 0;
             ++k;
         }
+        if (++ri == kRefRing) ri = 0;
     }
+    DLR_STAMP64M(63, threadIdx.x == 0);
     if (wv >= 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives its wave
 }
 #undef DLR_REF_WAIT
@@ -3460,22 +3550,36 @@ bool dense_ref_ok(int64_t D, int64_t N, int64_t B) {
 }
 int64_t dense_ref_resid(int64_t B) { return (B + kRefSlot - 1) / kRefSlot * kRefSlot + 4; }
 int64_t dense_ref_sync_words(int64_t B) { return (B + kRefSlot - 1) / kRefSlot + 96; }
+int dense_ref_grid(int64_t D, int64_t B) {
+    return (int)(D / kRefCols + std::min<int64_t>(256, (B + kRefUnit - 1) / kRefUnit));
+}
 
 hipError_t launch_dense_ref(const DevDense &dd, int64_t first, int64_t B, float *w, float *gout, float *resid,
-                            const DevRefSync &sy, float lr, float C, bool fused, hipStream_t s) {
+                            const DevRefSync &sy_in, float lr, float C, bool fused, hipStream_t chain_s,
+                            hipStream_t margin_s) {
     if (B <= 0) return hipSuccess;
     if (!dense_ref_ok(dd.D, dd.N, B) || first < 0 || first >= dd.N) return hipErrorInvalidValue;
     const int nstripes = (int)(dd.D / kRefCols);
     const int64_t nunits = (B + kRefUnit - 1) / kRefUnit;
-    const int M = (int)std::min<int64_t>(256, nunits);
+    DevRefSync sy = sy_in;
+    sy.mgrid = (int)std::min<int64_t>(256, nunits);
     const float Bf = (float)B;
     const double Bd = (double)B;
+    // the chains first: their workgroups are resident when the margins start
     if (fused)
-        hipLaunchKernelGGL(k_dense_ref<true>, dim3(nstripes + M), dim3(kRefThreads), kRefLds, s, dd, first, B, w, w,
-                           gout, resid, sy, nstripes, Bf, Bd, lr, C);
+        hipLaunchKernelGGL(k_dense_ref_chain<true>, dim3(nstripes), dim3(kRefThreads), kRefChainLds, chain_s, dd,
+                           first, B, w, gout, resid, sy, Bf, Bd, lr, C);
     else
-        hipLaunchKernelGGL(k_dense_ref<false>, dim3(nstripes + M), dim3(kRefThreads), kRefLds, s, dd, first, B, w, w,
-                           gout, resid, sy, nstripes, Bf, Bd, lr, C);
+        hipLaunchKernelGGL(k_dense_ref_chain<false>, dim3(nstripes), dim3(kRefThreads), kRefChainLds, chain_s, dd,
+                           first, B, w, gout, resid, sy, Bf, Bd, lr, C);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (dd.D / kRefStage >= 7)
+        hipLaunchKernelGGL(k_dense_ref_margin<6>, dim3(sy.mgrid), dim3(kRefThreads), kRefMarginLds, margin_s, dd,
+                           first, B, w, resid, sy);
+    else
+        hipLaunchKernelGGL(k_dense_ref_margin<3>, dim3(sy.mgrid), dim3(kRefThreads), kRefMarginLds, margin_s, dd,
+                           first, B, w, resid, sy);
     return hipGetLastError();
 }
 

@@ -8,6 +8,9 @@
 //   distlr_tool debuginfo <libsvm-file> <D>   (Sample::DebugInfo per sample)
 //   distlr_tool lrdebug <D> [random_state]      (LR::DebugInfo of a new LR: its
 //                                               initial weights, lr.cc:84-90)
+//   distlr_tool partial <libsvm-file> <D> <B> <k> <lr>   (GPU: NextBatch(k), then
+//       LR::Train on what is left of the round, lr.cc:29-30; prints the
+//       iterator's state and the last pulled weights as hex bits)
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -88,6 +91,18 @@ int main(int argc, char **argv) {
                 for (auto &s : batch)
                     std::printf("%d %016llx\n", s.GetLabel(), (unsigned long long)fnv(s.GetFeature()));
             }
+            return 0;
+        }
+        if (mode == "partial" && argc >= 7) {  // GPU: one rank, KVWorker on device 0
+            const int B = std::atoi(argv[4]), k = std::atoi(argv[5]);
+            const float lr = (float)std::atof(argv[6]);
+            if (k > 0) (void)it.NextBatch(k);
+            std::printf("before %d %d\n", it.offset(), it.HasNext() ? 1 : 0);
+            distlr::LR model(D);
+            model.SetKVWorker(new distlr::KVWorker(0, 0, 1, nullptr, lr, true, D));
+            model.Train(it, 0, B);
+            std::printf("after %d %d\n", it.offset(), it.HasNext() ? 1 : 0);
+            for (float v : model.GetWeight()) std::printf("%08x\n", bits(v));
             return 0;
         }
         if (mode == "debuginfo") {

@@ -177,14 +177,55 @@ void LR::PullWeight_() {
     check(dlr_get_weights(kv_->ctx(), weight_.data(), num_feature_dim_), kv_->ctx(), "dlr_get_weights");
 }
 
+namespace {
+// The shard's rows starting at row k, wrapping (row i of the result is row
+// (k + i) mod N): batch m of it is NextBatch's m-th batch after k rows were
+// consumed (data_iter.h:40-55), so a partially consumed DataIter trains the
+// same rows in the same order as lr.cc:29-30's loop.
+std::shared_ptr<Shard> rotated_shard(const Shard &sh, int64_t k) {
+    const int64_t n = sh.rows();
+    const int64_t *rp;
+    const int32_t *col;
+    const float *val;
+    const int32_t *lab;
+    dlr_dataset_view(sh.get(), &rp, &col, &val, &lab);
+    std::vector<int64_t> rp2((size_t)n + 1, 0);
+    std::vector<int32_t> col2, lab2((size_t)n);
+    std::vector<float> val2;
+    col2.reserve((size_t)rp[n]);
+    val2.reserve((size_t)rp[n]);
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t r = (k + i) % n;
+        col2.insert(col2.end(), col + rp[r], col + rp[r + 1]);
+        val2.insert(val2.end(), val + rp[r], val + rp[r + 1]);
+        rp2[(size_t)i + 1] = (int64_t)col2.size();
+        lab2[(size_t)i] = lab[r];
+    }
+    dlr_dataset *ds = nullptr;
+    check(dlr_dataset_from_csr(n, sh.feature_dim(), rp2.data(), col2.data(), val2.data(), lab2.data(), &ds), nullptr,
+          "LR::Train: dlr_dataset_from_csr");
+    return std::make_shared<Shard>(ds);
+}
+}  // namespace
+
 void LR::Train(DataIter &iter, int /*num_iter*/, int batch_size) {
     if (!kv_) throw std::logic_error("LR::Train: SetKVWorker first");
     if (!iter.HasNext()) return;  // lr.cc:29: nothing left in this round
-    const std::shared_ptr<Shard> &sh = iter.shard();
-    if (sh->rows() == 0) throw std::runtime_error("LR::Train: empty shard (the reference never terminates)");
+    std::shared_ptr<Shard> sh = iter.shard();
+    const int64_t n = sh->rows();
+    if (n == 0) throw std::runtime_error("LR::Train: empty shard (the reference never terminates)");
     if (batch_size == 0) throw std::runtime_error("LR::Train: batch_size 0 (the reference never terminates)");
-    if (iter.offset() != 0)
-        throw std::logic_error("LR::Train: the DataIter was partially consumed by NextBatch; pass a fresh one");
+    const int64_t bs = batch_size < 0 ? n : batch_size;
+    // A DataIter that NextBatch already advanced k rows (lr.cc:29-30 trains
+    // what is left of the round): batches of bs rows from row k on, wrapping
+    // to row 0, ceil((n - k) / bs) of them, as NextBatch would hand them out;
+    // trained from the shard rotated by k rows.
+    const int64_t k = iter.offset();
+    int64_t nb_run = -1;  // -1: every batch of the loaded plan
+    if (k != 0) {
+        sh = rotated_shard(*sh, k);
+        nb_run = (n - k + bs - 1) / bs;
+    }
     dlr_ctx *ctx = kv_->ctx();
     if (kv_->train_shard != sh.get() || kv_->train_batch != batch_size) {
         int64_t nb = 0;
@@ -194,7 +235,7 @@ void LR::Train(DataIter &iter, int /*num_iter*/, int batch_size) {
         kv_->train_batch = batch_size;
         kv_->train_batches = nb;
     }
-    const int64_t nb = kv_->train_batches;
+    const int64_t nb = nb_run < 0 ? kv_->train_batches : nb_run;
     const float lr = kv_->learning_rate();
     const int mode = kv_->mode();
     if (kv_->ps()) {  // worker half on this GPU, server half in ParamServer
@@ -204,18 +245,20 @@ void LR::Train(DataIter &iter, int /*num_iter*/, int batch_size) {
             check(dlr_worker_gradient(ctx, b, C_, grad.data(), num_feature_dim_), ctx, "dlr_worker_gradient");
             kv_->ps()->Push(rank_, grad);
         }
+    } else {
+        for (int64_t b = 0; b < nb; ++b) {
+            // Every batch pulls before it computes (lr.cc:32); only the last
+            // pull of the epoch is observable (GetWeight/SaveModel), so only
+            // it is copied to the host.
+            if (b == nb - 1) PullWeight_();
+            check(dlr_train_step(ctx, b, lr, C_, mode), ctx, "dlr_train_step");
+        }
+        check(dlr_sync(ctx), ctx, "dlr_sync");
+    }
+    if (k == 0)
         iter.ConsumeEpoch();
-        return;
-    }
-    for (int64_t b = 0; b < nb; ++b) {
-        // Every batch pulls before it computes (lr.cc:32); only the last pull
-        // of the epoch is observable (GetWeight/SaveModel), so only it is
-        // copied to the host.
-        if (b == nb - 1) PullWeight_();
-        check(dlr_train_step(ctx, b, lr, C_, mode), ctx, "dlr_train_step");
-    }
-    check(dlr_sync(ctx), ctx, "dlr_sync");
-    iter.ConsumeEpoch();
+    else
+        iter.ConsumeRows(nb * bs);
 }
 
 void LR::Test(DataIter &iter, int num_iter) {

@@ -170,6 +170,17 @@ void DataIter::ClearCache() {
     g_cache.clear();
 }
 
+void DataIter::ConsumeRows(int64_t rows) {
+    const int64_t n = shard_->rows();
+    if (n == 0 || rows <= 0) {
+        if (n == 0) round_end_ = true;
+        return;
+    }
+    const int64_t end = (int64_t)offset_ + rows;
+    if (end >= n) round_end_ = true;
+    offset_ = (int)(end % n);
+}
+
 std::vector<Sample> DataIter::NextBatch(int batch_size) {
     const int64_t n = shard_->rows();
     if (batch_size < 0) batch_size = (int)n;

@@ -60,6 +60,9 @@ class DataIter {
         offset_ = 0;
         round_end_ = true;
     }
+    // What NextBatch would do to the position for `rows` more rows
+    // (data_iter.h:49-52: offset wraps to 0 and ends the round at the end).
+    void ConsumeRows(int64_t rows);
     // Drops every cached shard (frees host memory).
     static void ClearCache();
 

@@ -132,3 +132,34 @@ def test_unknown_role_is_reported(tmp_path):
            "DMLC_ROLE": "bogus"}
     r = subprocess.run([BIN], env=env, capture_output=True, timeout=60)
     assert r.returncode == 2 and b"DMLC_ROLE" in r.stderr
+
+
+@pytest.mark.parametrize("B,k", [(7, 3), (64, 100), (-1, 5), (3000, 1)])
+def test_train_on_partially_consumed_dataiter(B, k):
+    # lr.cc:29-30 trains what is left of the round: after NextBatch(k) the
+    # batches start at row k and wrap to row 0 (data_iter.h:49-52), and
+    # Train stops after the batch that ends the round.  Against the oracle's
+    # sequential sums for exactly those rows; the iterator ends where
+    # NextBatch would leave it; GetWeight is the last PULLED weights (the
+    # ones before the last batch's update, lr.cc:32).
+    tool = os.path.join(ROOT, "dist-lr_amd", "bin", "distlr_tool")
+    path = os.path.join(GOLDEN, "c1_tiny", "train", "part-001")
+    D, lr = 123, 0.2
+    r = subprocess.run([tool, "partial", path, str(D), str(B), str(k), repr(lr)], capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr.decode()
+    out = r.stdout.decode().split()
+    n_rows = dlr.Dataset.load_libsvm(path, D).n_rows
+    assert out[0:3] == ["before", str(k % n_rows), "1" if k < n_rows else "0"]
+    got = np.array([int(x, 16) for x in out[6:]], dtype=np.uint32).view(np.float32)
+    bs = n_rows if B < 0 else B
+    nb = -(-(n_rows - k) // bs)
+    assert out[3:6] == ["after", str((k + nb * bs) % n_rows), "0"]
+    ds = dlr.Dataset.load_libsvm(path, D)
+    rp, col, val, lab = ds.csr()
+    w = dlr.init_weight(D)
+    pulled = w.copy()
+    for m in range(nb):
+        rows = (k + m * bs + np.arange(bs)) % n_rows
+        pulled = w.copy()
+        oracle.server_update(w, [oracle.grad_csr((rp, col, val), lab, rows, w)], lr)
+    assert np.array_equal(got.view(np.uint32), pulled.view(np.uint32))

@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""Per-workgroup timeline of the banded reference-order dense launch
+(k_dense_ref, C4) from s_memrealtime stamps (100 MHz).  Loads the DLR_STAMPS
+build of the library (make -C dist-lr_amd stamps) through DLR_LIB.
+Development tool, never part of the product.
+
+Chain workgroups: slot 0 start, 1 prologue done, 2 + t/16 the end of slot
+iteration t (t = 0, 16, ...), 50 end.  Margin workgroups: 0 start, 1 prologue done,
+2 + k the publish time of its k-th unit, 44 + k that unit's id, 63 end.
+
+  python tools/c4_stamps.py [--rows N] [--steps K] [--reps R]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("DLR_LIB", os.path.join(ROOT, "dist-lr_amd", "lib", "libdistlr_amd_stamps.so"))
+sys.path.insert(0, os.path.join(ROOT, "dist-lr_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (one HIP runtime: torch's)
+
+import distlr_amd as dlr  # noqa: E402
+
+
+def pct(v):
+    v = np.asarray(v, dtype=np.float64)
+    if v.size == 0:
+        return "(none)"
+    return "min %7.1f p10 %7.1f med %7.1f p90 %7.1f max %7.1f" % tuple(np.percentile(v, [0, 10, 50, 90, 100]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=300_000)
+    ap.add_argument("--features", type=int, default=4096)
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    assert "stamps" in dlr.LIB_PATH, dlr.LIB_PATH
+    f = dlr.lib.dlr_debug_stamp_buffer
+    f.argtypes, f.restype = [C.c_void_p], C.c_int
+    D, B = a.features, a.batch
+    S = D // 16
+    M = min(256, (B + 31) // 32)
+    G = 512  # chain workgroups write rows [0, S), margin workgroups rows [256, 256 + M)
+    buf = torch.zeros(G * 64, dtype=torch.int64, device="cuda")
+    assert f(buf.data_ptr()) == 0
+    dd = dlr.DenseDataset.generate(a.rows, D, seed=10, stream=1)
+    eng = dlr.Engine(D)
+    eng.set_weights(dlr.init_weight(D))
+    nb = eng.load_train_dense(dd, B)
+    nslot = (B + 255) // 256
+    k = 0
+    for rep in range(a.reps + 1):
+        buf.zero_()
+        torch.cuda.synchronize()
+        for _ in range(a.steps):
+            eng.train_step(k % nb, 0.2, 1.0)
+            k += 1
+        eng.sync()
+        torch.cuda.synchronize()
+        st = buf.cpu().numpy().reshape(G, 64).astype(np.float64)
+        if rep == 0:
+            continue  # warm-up
+        ch, mg = st[:S], st[256:256 + M]
+        t0 = min(ch[:, 0].min(), mg[:, 0].min())
+        us = lambda x: (x - t0) * 0.01  # noqa: E731
+        print(f"--- last launch of rep {rep}: {S} chain + {M} margin workgroups, {nslot} slots")
+        print("chain start      ", pct(us(ch[:, 0])))
+        print("chain prologue   ", pct(us(ch[:, 1])))
+        for t in range(0, nslot + 1, 32):
+            print(f"chain slot {t:4d}  ", pct(us(ch[:, 2 + t // 16])))
+        print("chain end        ", pct(us(ch[:, 50])))
+        print("margin start     ", pct(us(mg[:, 0])))
+        print("margin prologue  ", pct(us(mg[:, 1])))
+        units = [[] for _ in range(40)]
+        ids = []
+        for r in range(M):
+            for kk in range(40):
+                if mg[r, 2 + kk] > 0:
+                    units[kk].append(us(mg[r, 2 + kk]))
+            for kk in range(16):
+                if mg[r, 2 + kk] > 0:
+                    ids.append((mg[r, 44 + kk], us(mg[r, 2 + kk])))
+        for kk in range(0, 40, 2):
+            if units[kk]:
+                print(f"margin unit #{kk:2d}   ", pct(units[kk]), f"({len(units[kk])} WGs)")
+        print("margin end       ", pct(us(mg[:, 63])))
+        ids.sort()
+        if ids:
+            u = np.array([x for x, _ in ids])
+            t = np.array([y for _, y in ids])
+            slots = u // 8
+            print("slot publish time (last unit of slot):")
+            for s_ in range(0, nslot, 32):
+                m = slots == s_
+                if m.any():
+                    print(f"   slot {s_:4d}: {t[m].max():8.1f} us")
+        print(f"wall per step (bench-style) n/a; chain span {np.median(us(ch[:, 50])):.1f} us")
+
+
+if __name__ == "__main__":
+    main()
