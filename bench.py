@@ -113,6 +113,8 @@ def parse_args():
     ap.add_argument("--nnz", type=int, default=None)
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--lr", type=float, default=0.2)
+    ap.add_argument("--xpieces", type=int, default=4,
+                    help="N > 1: pieces of the overlapped all-gather (dlr_set_exchange_pieces)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=["mean", "last", "async"], default="mean",
@@ -409,6 +411,7 @@ def run_rank(args):
     t_gen = time.perf_counter() - t_setup
     eng = dlr.Engine(D, device=local, rank=rank, world=world, unique_id=uid)
     eng.set_summation_order(dlr.ORDER_FAST if args.order == "fast" else dlr.ORDER_REFERENCE)
+    eng.set_exchange_pieces(args.xpieces)
     eng.set_weights(dlr.init_weight(D))
     if args.residency != "auto":
         eng.set_residency({"device": dlr.RESIDENCY_DEVICE, "stream": dlr.RESIDENCY_STREAM}[args.residency])
@@ -496,6 +499,7 @@ def run_rank(args):
     # exchange NOT overlapped with the next batch's pass 1 (plain all-gather,
     # pass 1 in the next margin), so the line shows what the overlap buys
     overlap = eng.exchange_overlap() if world > 1 else False
+    xpieces = eng.exchange_pieces()
     no_overlap = None
     if overlap:
         eng.set_exchange_overlap(False)
@@ -621,9 +625,10 @@ def run_rank(args):
                             ("torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else
                              ("external" if distributed else "single process")),
                 "us_per_step": round(avg_us["exchange"], 3),
-                "overlap": ("the all-gather in 4 pieces, the next batch's pass 1 formed slice group by slice group "
+                "overlap": ("the all-gather in pieces, the next batch's pass 1 formed slice group by slice group "
                             "as its weights land (us_per_step includes that pass 1; the margin then runs pass 2 only)"
                             if overlap else None),
+                "pieces": xpieces,
                 "without_overlap": no_overlap,
                 "merge_us_per_step": round(avg_us["merge"], 3) if world > 1 else 0.0,
                 "protocol": ("touched-list all-gather + rank-ordered merge" if layout == "touched" else

@@ -28,7 +28,7 @@
 namespace {
 
 constexpr int kTimers = 5;  // 0 margin, 1 gradient, 2 update, 3 exchange, 4 step
-constexpr int kXPieces = 4;  // pieces of the overlapped all-gather (exchange_overlapped)
+constexpr int kXPiecesMax = 16;  // pieces of the overlapped all-gather (exchange_overlapped), at most
 constexpr int64_t kPad = 64;  // padding entries after col/val (16-B tail loads)
 
 struct DeviceBuf {
@@ -114,7 +114,7 @@ struct TrainShard {
     std::vector<int64_t> rtoff;
     std::vector<uint32_t> rt_cap;
     // world > 1: the exchange / next-margin overlap (dlr_train_step).  The
-    // in-place all-gather of the updated weights runs in kXPieces pieces on
+    // in-place all-gather of the updated weights runs in xpieces pieces on
     // the exchange stream; after piece k the next batch's pass 1 forms the
     // slices whose weights have all landed.  xslices: slice ids grouped by
     // the piece that completes them (group 0: inside this rank's own key
@@ -123,6 +123,7 @@ struct TrainShard {
     uint32_t *xslices = nullptr;
     std::vector<int64_t> xgofs;
     int64_t xsub = 0;  // words per piece of a rank's key range
+    int xpieces = 4;   // pieces (dlr_set_exchange_pieces at load, agreed over the ranks)
     // touched-column layout (huge D, small batches): per batch the touched
     // columns tcols[tcoff[b] .. +tncols[b]), segment pointers in cptr at
     // tpoff[b] (tncols[b]+1 entries), entries at coff[b] in crow/cval
@@ -257,7 +258,9 @@ struct dlr_ctx {
     int order = DLR_ORDER_REFERENCE;
     hipStream_t xstream = nullptr;
     hipEvent_t ev_xmerged = nullptr;
-    hipEvent_t ev_xpiece[kXPieces] = {};
+    hipEvent_t ev_xpiece[kXPiecesMax] = {};
+    // pieces of the next loaded shard's overlapped all-gather
+    int xpieces = 4;
     // product margin: the batch whose products pm_p holds, formed from the
     // CURRENT weights by the last step's fused gradient (-1: none; every
     // entry point that changes w or the shard resets it)
@@ -565,13 +568,17 @@ int coll_agree_load(dlr_ctx *c, const char *who, int local_rc, const std::string
 }
 
 // Every rank must load with the same summation order (dlr_set_summation_order):
-// a rank summing differently would hold different weights after the merge.
+// a rank summing differently would hold different weights after the merge;
+// and with the same exchange piece count (dlr_set_exchange_pieces): the
+// pieces are collectives.
 int coll_agree_order(dlr_ctx *c, const char *who) {
-    int64_t v[2] = {c->order, -(int64_t)c->order};
-    int rc = coll_reduce_i64(c, v, 2, true);
+    int64_t v[4] = {c->order, -(int64_t)c->order, c->xpieces, -(int64_t)c->xpieces};
+    int rc = coll_reduce_i64(c, v, 4, true);
     if (rc) return rc;
     if (v[0] != -v[1])
         return fail(c, DLR_E_ARG, std::string(who) + ": the ranks asked for different summation orders");
+    if (v[2] != -v[3])
+        return fail(c, DLR_E_ARG, std::string(who) + ": the ranks asked for different exchange piece counts");
     return DLR_OK;
 }
 
@@ -1703,24 +1710,10 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
         int64_t first;
         hipError_t e = dense_batch(c, b, &dd, &first);
         if (e == hipSuccess && t.dref) {
-            // the chains on the engine stream, the margins on the second
-            // stream: both after everything queued so far (the previous
-            // step's update of w), and the engine stream past the margins
-            // before its next work
-            if (!c->gstream) {
-                e = hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking);
-                if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_bstart, hipEventDisableTiming);
-                if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_bdone, hipEventDisableTiming);
-            }
             const int64_t nw = dlr::dense_ref_sync_words(B);
             const dlr::DevRefSync sy{t.dref_sync, t.dref_sync + nw - 64, t.dref_sync + nw - 32, t.dref_seq,
                                      t.dref_lead, 0};
-            if (e == hipSuccess) e = hipEventRecord(c->ev_bstart, c->stream);
-            if (e == hipSuccess) e = hipStreamWaitEvent(c->gstream, c->ev_bstart, 0);
-            if (e == hipSuccess)
-                e = dlr::launch_dense_ref(dd, first, B, c->w, gout, c->resid, sy, lr, C, fused, c->stream, c->gstream);
-            if (e == hipSuccess) e = hipEventRecord(c->ev_bdone, c->gstream);
-            if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_bdone, 0);
+            e = dlr::launch_dense_ref(dd, first, B, c->w, gout, c->resid, sy, lr, C, fused, c->stream);
             if (e == hipSuccess) ++c->train.dref_seq;
         } else if (e == hipSuccess)
             e = t.dfused ? dlr::launch_dense_combine(t.dpart, c->D, B, c->w, gout, lr, C, fused, c->stream)
@@ -2019,8 +2012,8 @@ int dlr_get_weights(dlr_ctx *c, float *w, int64_t D) {
 int build_overlap_groups(dlr_ctx *c) {
     TrainShard &t = c->train;
     const int64_t S = t.pmS, chunk = c->chunk, W = c->world;
-    t.xsub = (chunk + kXPieces - 1) / kXPieces;
-    std::vector<std::vector<uint32_t>> g((size_t)kXPieces + 1);
+    t.xsub = (chunk + t.xpieces - 1) / t.xpieces;
+    std::vector<std::vector<uint32_t>> g((size_t)t.xpieces + 1);
     for (int64_t s = 0; s < S; ++s) {
         const int64_t a = s * dlr::kPmSlice, b = std::min((s + 1) * dlr::kPmSlice, c->D);
         int grp = 0;
@@ -2061,7 +2054,7 @@ int exchange_overlapped(dlr_ctx *c, int64_t b) {
         return dlr::launch_pm_products(pm, c->w, c->D, t.pm_p, c->stream, t.xslices + t.xgofs[(size_t)grp], n);
     };
     HIPC(c, pass1(0));  // inside this rank's own key range: ready now
-    for (int k = 0; k < kXPieces; ++k) {
+    for (int k = 0; k < t.xpieces; ++k) {
         const int64_t off = k * t.xsub, cnt = std::max<int64_t>(0, std::min(t.xsub, c->chunk - off));
         COMMC(c, all_gather_part(c->w, (size_t)c->chunk, (size_t)off, (size_t)cnt, c->xstream, e_));
         HIPC(c, hipEventRecord(c->ev_xpiece[k], c->xstream));
@@ -2092,6 +2085,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
     HIPC(c, hipStreamSynchronize(c->stream));
     free_train(c);
     TrainShard &t = c->train;
+    t.xpieces = c->xpieces;
     t.n_rows = ds->n_rows;
     t.nnz = (int64_t)ds->col.size();
     t.B = batch_size < 0 ? ds->n_rows : batch_size;
@@ -3241,6 +3235,18 @@ int dlr_set_exchange_overlap(dlr_ctx *c, int on) {
 int dlr_exchange_overlap(dlr_ctx *c) {
     if (!c) return DLR_E_ARG;
     return c->comm && c->train.loaded && c->train.xpieced ? 1 : 0;
+}
+
+int dlr_set_exchange_pieces(dlr_ctx *c, int pieces) {
+    if (!c || pieces < 1 || pieces > kXPiecesMax)
+        return fail(c, DLR_E_ARG, "dlr_set_exchange_pieces: pieces must be in [1, 16]");
+    c->xpieces = pieces;  // the next load's (the ranks agree there)
+    return DLR_OK;
+}
+
+int dlr_exchange_pieces(dlr_ctx *c) {
+    if (!c) return DLR_E_ARG;
+    return c->comm && c->train.loaded && c->train.xpieced ? c->train.xpieces : 0;
 }
 
 int dlr_set_summation_order(dlr_ctx *c, int order) {

@@ -282,13 +282,9 @@ hipError_t launch_dense_combine(const float *part, int64_t D, int64_t B, float *
 bool dense_ref_ok(int64_t D, int64_t N, int64_t B);
 int64_t dense_ref_sync_words(int64_t B);
 int64_t dense_ref_resid(int64_t B);
-int dense_ref_grid(int64_t D, int64_t B);  // chain + margin workgroups (the stamps tool's buffer)
-// The chains go on chain_s, the margins on margin_s (the caller orders the
-// two streams: both start after the previous step, and chain_s waits for
-// the margins before its next work).
+int dense_ref_grid(int64_t D, int64_t B);  // workgroups of the launch
 hipError_t launch_dense_ref(const DevDense &dd, int64_t first, int64_t B, float *w, float *gout, float *resid,
-                            const DevRefSync &sy, float lr, float C, bool fused, hipStream_t chain_s,
-                            hipStream_t margin_s);
+                            const DevRefSync &sy, float lr, float C, bool fused, hipStream_t s);
 int predict_dense_grid(int64_t rows);
 hipError_t launch_dense_predict(const DevDense &dd, const float *w, unsigned long long *correct, double *ll_part,
                                 double *ll_out, hipStream_t s);

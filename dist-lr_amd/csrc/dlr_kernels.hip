@@ -866,6 +866,8 @@ namespace {
 // bit 2 no pass 1, bit 3 no weight loads.  Always 0 in the product library.
 // Bit 4 (a variant, same results): pass 1's product stores write-through
 // (sc1), so they leave L2 as they issue instead of in the kernel-end flush.
+// k_dense_ref (tools/c4_stamps.py --abl): bit 5 no chain halves (run with
+// --lead 0), bit 6 no margin row chains (the stages stream, nothing adds).
 #ifndef DLR_ABL
 #define DLR_ABL 0
 #endif
@@ -2547,35 +2549,36 @@ __global__ __launch_bounds__(256) void k_dense_combine(const float *__restrict__
 }
 
 // ---------------------------------------------------------------------------
-// K6r: the dense step in the REFERENCE order as two concurrent launches (C4's
-// default).  lr.cc's arithmetic is two families of serial fp32 chains: every
-// margin z_i is a chain over the columns in order (lr.cc:108-112), every
-// gradient G_j a chain over the batch rows in order (lr.cc:35-39), and a row
-// can enter the column chains only once its own chain is done.  A column
-// chain of B = 65,536 dependent adds is the floor (8.3 cycles each on
-// gfx950, profiles/r04_kbench_chain2.txt: ~0.23 ms), so the step is built
-// around keeping every column chain busy from its first row to its last:
+// K6r: the dense step in the REFERENCE order as one launch (C4's default).
+// lr.cc's arithmetic is two families of serial fp32 chains: every margin z_i
+// is a chain over the columns in order (lr.cc:108-112), every gradient G_j a
+// chain over the batch rows in order (lr.cc:35-39), and a row can enter the
+// column chains only once its own chain is done.  A column chain of
+// B = 65,536 dependent adds is the floor (8.3 cycles each on gfx950,
+// profiles/r04_kbench_chain2.txt: ~0.23 ms), so the step keeps every column
+// chain busy from its first row to its last.  One 512-thread workgroup per
+// CU, two independent halves (no workgroup barrier after the start: each
+// half hands off through LDS counters):
 //
-//   k_dense_ref_chain (one workgroup per 16-column stripe, 35 KB of LDS):
-//     wave 0    lane c runs column c's chain over slot t-1's products (LDS,
+//   chain half (waves 0-3; workgroup b < D/16 owns columns [16b, 16b + 16)):
+//     wave 0    lane c runs column c's chain over each slot's products (LDS,
 //               16-byte reads, 256 rows per slot) -- its only work;
 //     waves 1-2 load slot t's 256 rows x 16 columns into registers (three
 //               slots in flight: the rows were read from HBM moments ago by
-//               the margin workgroups and come back from the Infinity
-//               Cache), form fl32(r_i * x_ij) and store them transposed;
+//               the margin halves and come back from the Infinity Cache),
+//               form fl32(r_i * x_ij) and store them transposed;
 //     wave 3    loads the residuals of slot t+3 once its margins are
 //               published (sc1: written by other CUs); workgroup 0's also
-//               publishes the margins' LIMIT: `lead` slots past its own
+//               publishes the margins' LIMIT, `lead` slots past its own
 //               progress, so the rows the chains re-read are still in the
 //               Infinity Cache;
-//   k_dense_ref_margin (one workgroup per CU, a 112 KB LDS ring), on a second
-//     stream: claims units of 32 batch rows in row order from a queue (rows
-//     finish in order, and any resident subset of workgroups drains it),
-//     waits for the limit before it starts a unit (holding only later
-//     units: no chain waits on it), streams the unit's rows through the
-//     ring by LDS-DMA (waves 1-3, six stages in flight) while lane i of
-//     wave 0 runs row i's chain in column order; publishes sigma - y with
-//     sc1 stores and one agent-scope add to the slot's counter
+//   margin half (waves 4-7): claims units of 32 batch rows in row order from
+//     a queue (rows finish in order, and any resident subset of workgroups
+//     drains it), waits for the limit before it starts a unit (holding only
+//     later units: no chain waits on it), streams the unit's rows through a
+//     7-stage LDS ring by LDS-DMA (waves 5-7, six stages in flight) while
+//     lane i of wave 4 runs row i's chain in column order; publishes
+//     sigma - y with sc1 stores and one agent-scope add to the slot's counter
 //     (MI355X_MICROARCH.md, inter-workgroup hand-off, the sc1 row).
 //
 // The weights are written only by the chain epilogue, after its last slot:
@@ -2585,18 +2588,34 @@ __global__ __launch_bounds__(256) void k_dense_combine(const float *__restrict__
 // come runs to the end with wrong sums instead of hanging the GPU.  X is
 // read once from HBM (the margins) and once from the Infinity Cache (the
 // chains).
-constexpr int kRefCols = 16;     // columns per chain workgroup
+#ifndef DLR_REF_SWZ  // A/B (stamps variants): the chunk swizzle of the margin ring
+#define DLR_REF_SWZ 1
+#endif
+#ifndef DLR_REF_WDMA  // A/B: the stage's weights by LDS-DMA (0: timing only, wrong sums)
+#define DLR_REF_WDMA 1
+#endif
+constexpr int kRefCols = 16;     // columns per chain half
 constexpr int kRefSlot = 256;    // batch rows per chain slot
 constexpr int kRefUnit = 32;     // batch rows per margin unit (one lane each)
 constexpr int kRefStage = 128;   // columns per margin stage
 constexpr int kRefRing = 7;      // margin stages in the LDS ring (up to 6 in flight)
 constexpr int kRefPad = kRefSlot + 4;
-constexpr int kRefThreads = 256;
+constexpr int kRefThreads = 512;
 constexpr uint32_t kRefNone = 0xFFFFFFFFu;
 constexpr int kRefSpin = 1 << 22;
-constexpr size_t kRefChainLds = (size_t)(2 * kRefCols * kRefPad + 2 * kRefSlot) * 4;
-constexpr size_t kRefMarginLds = (size_t)kRefRing * kRefUnit * kRefStage * 4 + 64;
-static_assert(kRefChainLds + kRefMarginLds <= 160 * 1024, "one chain and one margin workgroup per CU");
+// LDS (floats): chain products [2][16][kRefPad], residuals [2][256], the
+// margin ring [7][32 x 128 + 256], then 16 words of hand-off counters / unit ids
+constexpr int kRefOffR = 2 * kRefCols * kRefPad;
+constexpr int kRefOffRing = kRefOffR + 2 * kRefSlot;
+constexpr int kRefSlotF = kRefUnit * kRefStage + 256;  // a ring slot: the stage's rows + its 128 weights (1 KiB)
+constexpr int kRefOffCtl = kRefOffRing + kRefRing * kRefSlotF;
+constexpr size_t kRefLds = (size_t)(kRefOffCtl + 16) * 4;
+static_assert(kRefLds <= 160 * 1024, "one workgroup per CU");
+// control words (uint32 at kRefOffCtl): chain half -- helper 1 / 2 slots
+// done, chain slots done, residual slots staged; margin half -- loader 0..2
+// stages landed, compute stages done, unit ids published, unit ids [4]
+// (unit k's id in [k & 3], valid once ids > k)
+enum { kCtlH0 = 0, kCtlH1, kCtlChain, kCtlR, kCtlL0, kCtlL1, kCtlL2, kCtlComp, kCtlIds, kCtlUnit };
 
 // Shard row (first + i) mod N of batch row i: the launch needs B <= N
 // (dense_ref_ok), so first + i < 2N and one subtraction wraps it
@@ -2606,45 +2625,69 @@ __device__ __forceinline__ int64_t ref_row(int64_t first, int64_t i, int64_t N) 
     return r >= N ? r - N : r;
 }
 
-// 8 of a margin stage's 32 reads: piece 4G + m / 2, half m & 1 (offset
-// (2 * piece + half) * 512 bytes from the lane's 16-byte slot)
-template <int G>
-__device__ __forceinline__ void ref_rd8(v4f (&d)[8], uint32_t a) {
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[0]) : "v"(a), "n"(G * 4096 + 0 * 512));
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[1]) : "v"(a), "n"(G * 4096 + 1 * 512));
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[2]) : "v"(a), "n"(G * 4096 + 2 * 512));
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[3]) : "v"(a), "n"(G * 4096 + 3 * 512));
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[4]) : "v"(a), "n"(G * 4096 + 4 * 512));
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[5]) : "v"(a), "n"(G * 4096 + 5 * 512));
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[6]) : "v"(a), "n"(G * 4096 + 6 * 512));
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[7]) : "v"(a), "n"(G * 4096 + 7 * 512));
+// LDS hand-off words between the waves of one half (no s_barrier: the two
+// halves run at their own pace).  A producer's data writes (or, for LDS-DMA,
+// its covering vmcnt wait) complete before the word is written; a consumer
+// reads the data only after it has seen the word.
+__device__ __forceinline__ uint32_t ctl_read(const uint32_t *p) {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+    return v;
 }
-#define DLR_REF_WAIT(N, d)                                                                                    \
+__device__ __forceinline__ void ctl_write(uint32_t *p, uint32_t v) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n ds_write_b32 %0, %1\n s_waitcnt lgkmcnt(0)" ::"v"(lds_addr(p)), "v"(v)
+                 : "memory");
+}
+__device__ __forceinline__ void ctl_wait_ge(const uint32_t *p, uint32_t v) {
+    for (int k = 0; k < kRefSpin && (int32_t)(ctl_read(p) - v) < 0; ++k) __builtin_amdgcn_s_sleep(0);
+}
+
+// A margin stage in the ring: 16 blocks of 1 KiB, block q = 4L + G holds
+// line L (columns [32L, 32L + 32) of the stage, 128 bytes) of the rows
+// [8G, 8G + 8) of the unit, row r at (r & 7) * 128 and its 16-byte chunk k
+// at ((k ^ (r & 7)) * 16) -- each LDS-DMA instruction reads 8 whole lines
+// from HBM, and the compute lanes' 16-byte reads (lane = row) meet no bank
+// conflict.  After the 16 blocks: the stage's 128 weights (w[128 sg ..]).
+// ref_rd8<L, H>: row i's chunks 4H .. 4H + 3 of line L (a[k] = the
+// lane's base + ((k ^ (i & 7)) * 16)) and their 16 weights (wa: the slot,
+// uniform; every lane reads the same 16 bytes, an LDS broadcast) -- eight
+// reads, so that two sets in flight stay within lgkmcnt's 15.
+template <int L, int H>
+__device__ __forceinline__ void ref_rd8(v4f (&d)[4], v4f (&wq)[4], const uint32_t (&a)[8], uint32_t wa) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[0]) : "v"(a[4 * H + 0]), "n"(L * 4096));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[1]) : "v"(a[4 * H + 1]), "n"(L * 4096));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[2]) : "v"(a[4 * H + 2]), "n"(L * 4096));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[3]) : "v"(a[4 * H + 3]), "n"(L * 4096));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(wq[0]) : "v"(wa), "n"(16384 + L * 128 + H * 64 + 0));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(wq[1]) : "v"(wa), "n"(16384 + L * 128 + H * 64 + 16));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(wq[2]) : "v"(wa), "n"(16384 + L * 128 + H * 64 + 32));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(wq[3]) : "v"(wa), "n"(16384 + L * 128 + H * 64 + 48));
+}
+#define DLR_REF_WAIT(N, d, e)                                                                                 \
     asm volatile("s_waitcnt lgkmcnt(" #N ")"                                                                 \
-                 : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]), "+v"(d[6]), "+v"(d[7]))
+                 : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(e[0]), "+v"(e[1]), "+v"(e[2]), "+v"(e[3]))
 
 // The queue position (claims so far) at the start of launch seq: every
-// launch makes nunits successful claims and one failed claim per margin
-// workgroup.
+// launch makes nunits successful claims and one failed claim per margin half.
 __device__ __forceinline__ uint32_t ref_base(const DevRefSync &sy, int64_t nunits) {
     return sy.seq * (uint32_t)(nunits + sy.mgrid);
 }
 
+// The chain half of workgroup blockIdx.x (< D / 16).
 template <bool FUSED>
-__global__ __launch_bounds__(kRefThreads) void k_dense_ref_chain(DevDense dd, int64_t first, int64_t B, float *w,
-                                                                 float *__restrict__ gout, float *resid, DevRefSync sy,
-                                                                 float Bf, double Bd, float lr, float C) {
-    extern __shared__ __attribute__((aligned(16))) float rsm[];
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+__device__ __forceinline__ void ref_chain_half(const DevDense &dd, int64_t first, int64_t B, float *w,
+                                               float *__restrict__ gout, float *resid, const DevRefSync &sy,
+                                               float Bf, double Bd, float lr, float C, float *rsm, int wv,
+                                               int lane) {
     const int64_t D = dd.D, N = dd.N;
     const int64_t nslot = (B + kRefSlot - 1) / kRefSlot;
     const int64_t nunits = (B + kRefUnit - 1) / kRefUnit;
-    const int nstripes = (int)gridDim.x;
-    float *s_p = rsm;                              // [2][kRefCols][kRefPad]
-    float *s_r = rsm + 2 * kRefCols * kRefPad;     // [2][kRefSlot]
+    const int nstripes = (int)(D / kRefCols);
+    float *s_p = rsm;            // [2][kRefCols][kRefPad]
+    float *s_r = rsm + kRefOffR; // [2][kRefSlot]
+    uint32_t *ctl = reinterpret_cast<uint32_t *>(rsm + kRefOffCtl);
     unsigned cg = blockIdx.x;
-    if ((nstripes & 15) == 0) {  // stripes 2m, 2m+1 (one 128-byte line of a row) on one XCD
+    if ((nstripes & 15) == 0 && (int)gridDim.x == nstripes) {  // stripes 2m, 2m+1 (one 128-byte line of a row) on one XCD
         const unsigned k = blockIdx.x >> 3;
         cg = ((k >> 1) << 4) | ((blockIdx.x & 7) << 1) | (k & 1);
     }
@@ -2688,26 +2731,85 @@ __global__ __launch_bounds__(kRefThreads) void k_dense_ref_chain(DevDense dd, in
                 *reinterpret_cast<v4f *>(sp + (4 * cq + q) * kRefPad + 4 * rq) = v4f{p[0][q], p[1][q], p[2][q], p[3][q]};
         }
     };
-    // wave 3: the residuals of slot t, once every unit of it is published
+    if (wv == 0) {
+        // the chain: slot t once both helpers have stored it
+        float acc = 0.0f;
+        for (int64_t t = 0; t < nslot; ++t) {
+            ctl_wait_ge(ctl + kCtlH0, (uint32_t)t + 1);
+            ctl_wait_ge(ctl + kCtlH1, (uint32_t)t + 1);
+            const float *sp = s_p + (t & 1) * kRefCols * kRefPad + (lane & (kRefCols - 1)) * kRefPad;
+#pragma unroll 2
+            for (int k = 0; k < kRefSlot; k += 32) {
+                v4f d[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) d[u] = *reinterpret_cast<const v4f *>(sp + k + 4 * u);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    acc = acc + d[u].x;
+                    acc = acc + d[u].y;
+                    acc = acc + d[u].z;
+                    acc = acc + d[u].w;
+                }
+            }
+            if (lane == 0) ctl_write(ctl + kCtlChain, (uint32_t)t + 1);
+            DLR_STAMP64(2 + (int)(t >> 4), lane == 0 && (t & 15) == 0 && t < 16 * 40);
+        }
+        DLR_STAMP64(50, lane == 0);
+        const int64_t j = c0 + lane;
+        if (lane >= kRefCols || j >= D) return;
+        const float wj = w[j];
+        const float cw = C * wj;
+        const float l2 = cw / Bf;
+        const float g = (float)((double)acc / Bd + (double)l2);
+        if (FUSED) {
+            const float stepv = lr * g;
+            w[j] = wj - stepv;
+        } else {
+            gout[j] = g;
+        }
+        return;
+    }
+    if (wv <= 2) {
+        // helpers: slot t needs its residuals staged and the products buffer
+        // of slot t - 2 consumed by the chain
+        uint32_t *mine = ctl + (wv == 1 ? kCtlH0 : kCtlH1);
+        v4f xa[8], xb[8], xc[8];
+        load(0, xa);
+        load(1, xb);
+        load(2, xc);
+        auto step = [&](int64_t t, v4f (&x)[8]) {
+            ctl_wait_ge(ctl + kCtlR, (uint32_t)t + 1);
+            if (t >= 2) ctl_wait_ge(ctl + kCtlChain, (uint32_t)t - 1);
+            transform(t, x);
+            if (lane == 0) ctl_write(mine, (uint32_t)t + 1);
+            load(t + 3, x);
+        };
+        for (int64_t t = 0; t < nslot; t += 3) {
+            step(t, xa);
+            if (t + 1 < nslot) step(t + 1, xb);
+            if (t + 2 < nslot) step(t + 2, xc);
+        }
+        return;
+    }
+    // wave 3: the residuals.  Its view of the margins: every slot <= ready
+    // is published.  Waiting for a slot polls its counter from ONE lane, a
+    // microsecond apart (hundreds of CUs polling flat out take HBM bandwidth
+    // from the margins they wait for); once it is published, one 64-lane
+    // poll of the next 64 counters extends `ready`, so while the margins run
+    // ahead a round trip is paid once per 64 slots.  Global loads and stores
+    // go through the buffer path with sc1 (aux 16): L2-coherent, and tracked
+    // by the compiler's waits.
     auto slot_target = [&](int64_t t) -> uint32_t {
         const int64_t rows = min<int64_t>(kRefSlot, B - t * kRefSlot);
         const uint32_t units = (uint32_t)((rows + kRefUnit - 1) / kRefUnit);
         return units * (sy.seq + 1);
     };
-    // wave 3's view of the margins: every slot <= ready is published.
-    // Waiting for a slot polls its counter from ONE lane, a microsecond
-    // apart (hundreds of CUs polling flat out take HBM bandwidth from the
-    // margins they wait for); once it is published, one 64-lane poll of the
-    // next 64 counters extends `ready`, so while the margins run ahead a
-    // round trip is paid once per 64 slots.  Loads and stores go through the
-    // buffer path with sc1 (aux 16): L2-coherent, and tracked by the
-    // compiler's waits.
     const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(sy.slot_cnt, 0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(resid, 0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc(sy.limit, 0, 0x7FFFFFFF, 0x00020000);
     const bool leader = blockIdx.x == 0 && sy.lead > 0;
     const uint32_t qbase = ref_base(sy, nunits);
-    auto publish_limit = [&](int64_t t) {  // workgroup 0, wave 3, lane 0
+    auto publish_limit = [&](int64_t t) {
         const int64_t lim = min<int64_t>(nunits, (t + sy.lead) * (kRefSlot / kRefUnit));
         if (lane == 0) __builtin_amdgcn_raw_buffer_store_b32(qbase + (uint32_t)lim, lrs, 0, 0, 16);
     };
@@ -2726,113 +2828,147 @@ __global__ __launch_bounds__(kRefThreads) void k_dense_ref_chain(DevDense dd, in
         const int first_bad = __ffsll((long long)bad) - 1;
         ready = t0 + max(first_bad, 1) - 1;  // t0 itself is published (or the bounded wait ran out)
     };
-    // residuals of slot t, once published
     auto r_issue = [&](int64_t t, v4f &rv) {
         const int64_t tc = t < nslot ? t : nslot - 1;  // past the end: a load of a published slot, unused
         if (tc > ready) poll_from(tc);
         const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rrs, (int)((tc * kRefSlot + 4 * lane) * 4), 0, 16);
         __builtin_memcpy(&rv, &q, 16);
     };
-    auto r_store = [&](int64_t t, const v4f &rv) { *reinterpret_cast<v4f *>(s_r + (t & 1) * kRefSlot + 4 * lane) = rv; };
-    float acc = 0.0f;
-    auto chain = [&](int64_t t) {
-        const float *sp = s_p + (t & 1) * kRefCols * kRefPad + (lane & (kRefCols - 1)) * kRefPad;
-#pragma unroll 2
-        for (int k = 0; k < kRefSlot; k += 32) {
-            v4f d[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) d[u] = *reinterpret_cast<const v4f *>(sp + k + 4 * u);
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                acc = acc + d[u].x;
-                acc = acc + d[u].y;
-                acc = acc + d[u].z;
-                acc = acc + d[u].w;
-            }
+    // slot t's residuals into s_r[t & 1] once both helpers are done with
+    // slot t - 2 (the same buffer)
+    auto r_store = [&](int64_t t, const v4f &rv) {
+        if (t >= 2) {
+            ctl_wait_ge(ctl + kCtlH0, (uint32_t)t - 1);
+            ctl_wait_ge(ctl + kCtlH1, (uint32_t)t - 1);
         }
+        *reinterpret_cast<v4f *>(s_r + (t & 1) * kRefSlot + 4 * lane) = rv;
+        if (lane == 0) ctl_write(ctl + kCtlR, (uint32_t)t + 1);
     };
-    v4f xa[8], xb[8], xc[8], ra, rb, rc;
-    DLR_STAMP64(0, threadIdx.x == 0);
-    if (wv == 3) {
-        if (leader) publish_limit(0);
-        r_issue(0, ra);
-        r_issue(1, rb);
-        r_issue(2, rc);
-        r_store(0, ra);
-    } else if (wv >= 1) {
-        load(0, xa);
-        load(1, xb);
-        load(2, xc);
-    }
-    lds_barrier();
-    DLR_STAMP64(1, threadIdx.x == 0);
-    // iteration t: wave 0 adds slot t-1; waves 1-2 transform slot t and
-    // reload its registers with slot t+3; wave 3 stores slot t+1's residuals
-    // (loaded two iterations ago) and issues slot t+3's
-    auto step = [&](int64_t t, v4f (&x)[8], v4f &rnext, v4f &rfree) {
-        if (wv == 0) {
-            if (t >= 1) chain(t - 1);
-        } else if (wv <= 2) {
-            if (t < nslot) {
-                transform(t, x);
-                load(t + 3, x);
-            }
-        } else {
-            r_store(t + 1, rnext);  // (past the last slot: an unused write of a free buffer)
-            r_issue(t + 3, rfree);
-            if (leader) publish_limit(t);
-        }
-        lds_barrier();
-        DLR_STAMP64(2 + (int)(t >> 4), threadIdx.x == 0 && (t & 15) == 0 && t < 16 * 40);
+    v4f ra, rb, rc;
+    if (leader) publish_limit(0);
+    r_issue(0, ra);
+    r_issue(1, rb);
+    r_issue(2, rc);
+    auto step = [&](int64_t t, v4f &rv) {  // slot t staged, slot t + 3 issued into its registers
+        r_store(t, rv);
+        r_issue(t + 3, rv);
+        if (leader) publish_limit(t);
     };
-    for (int64_t t = 0; t <= nslot; t += 3) {
-        step(t, xa, rb, ra);
-        if (t + 1 <= nslot) step(t + 1, xb, rc, rb);
-        if (t + 2 <= nslot) step(t + 2, xc, ra, rc);
-    }
-    DLR_STAMP64(50, threadIdx.x == 0);
-    if (wv != 0) return;
-    const int64_t j = c0 + lane;
-    if (lane >= kRefCols || j >= D) return;
-    const float wj = w[j];
-    const float cw = C * wj;
-    const float l2 = cw / Bf;
-    const float g = (float)((double)acc / Bd + (double)l2);
-    if (FUSED) {
-        const float stepv = lr * g;
-        w[j] = wj - stepv;
-    } else {
-        gout[j] = g;
+    for (int64_t t = 0; t < nslot; t += 3) {
+        step(t, ra);
+        if (t + 1 < nslot) step(t + 1, rb);
+        if (t + 2 < nslot) step(t + 2, rc);
     }
 }
 
-// LA: stages a loader keeps in flight ahead of the one computed (6; 3 when
-// a unit has fewer than 7 stages, D < 896, so that the loaders never need a
-// unit two ahead).  w: read-only here (the chains update it after every
-// margin is published).
+// The margin half (the workgroup's waves 4-7; mw = wave - 4).  LA: stages a
+// loader keeps in flight ahead of the one computed (6; 3 when a unit has
+// fewer than 7 stages, D < 896, so that a loader never needs a unit two
+// ahead).  wr: read-only here (the chains update w after every margin is
+// published).
 template <int LA>
-__global__ __launch_bounds__(kRefThreads) void k_dense_ref_margin(DevDense dd, int64_t first, int64_t B,
-                                                                  const float *__restrict__ wr, float *resid,
-                                                                  DevRefSync sy) {
-    extern __shared__ __attribute__((aligned(16))) float rsm[];
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+__device__ __forceinline__ void ref_margin_half(const DevDense &dd, int64_t first, int64_t B,
+                                                const float *__restrict__ wr, float *resid, const DevRefSync &sy,
+                                                float *rsm, int mw, int lane) {
     const int64_t D = dd.D, N = dd.N;
     const int64_t nunits = (B + kRefUnit - 1) / kRefUnit;
-    float *ring = rsm;  // [kRefRing][16 x 2 x 32][16 B]
-    uint32_t *s_unit = reinterpret_cast<uint32_t *>(rsm + kRefRing * kRefUnit * kRefStage);  // [4]
+    float *ring = rsm + kRefOffRing;  // [kRefRing][16 x 2 x 32][16 B]
+    uint32_t *ctl = reinterpret_cast<uint32_t *>(rsm + kRefOffCtl);
+    uint32_t *s_unit = ctl + kCtlUnit;  // [4]
     const int spu = (int)(D / kRefStage);  // stages per unit (>= 4)
     const uint32_t base = ref_base(sy, nunits);
+    if (mw < 3) {
+        // loaders: stage g of this half's unit sequence into ring[g % 7]: the
+        // 16 blocks above, one LDS-DMA instruction each (lane l: row
+        // 8G + (l >> 3), chunk (l & 7) ^ (l >> 3) of line L).  Stage g + LA
+        // goes into the slot stage g + LA - 7 used, once the compute is past
+        // it; stage g is published (kCtlL0 + lw) once this loader's blocks of
+        // it have landed.
+        const int lw = mw;                   // loader 0..2: blocks lw, lw + 3, ...
+        const int npieces = lw == 2 ? 5 : 6;  // of the 16 + 1 (6 + 5 + 5, and loader 1 the weights)
+        const int lrow = lane >> 3, lchunk = DLR_REF_SWZ ? (lane & 7) ^ (lane >> 3) : (lane & 7);
+        auto issue = [&](int k, int sg, int ri, int g) {
+            if (g >= kRefRing) ctl_wait_ge(ctl + kCtlComp, (uint32_t)(g - kRefRing + 1));
+            ctl_wait_ge(ctl + kCtlIds, (uint32_t)k + 1);
+            const uint32_t u = ctl_read(s_unit + (k & 3));
+            const int64_t ubase = (int64_t)(u == kRefNone ? 0 : u) * kRefUnit;
+            const int64_t col0 = (int64_t)sg * kRefStage + 4 * lchunk;
+            float *dst = ring + (size_t)ri * kRefSlotF;
+            for (int q = lw; q < 16; q += 3) {
+                const int L = q >> 2, G = q & 3;
+                const int64_t i = min(ubase + 8 * G + lrow, B - 1);
+                const float *src = dd.X + ref_row(first, i, N) * D + col0 + 32 * L;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                                 (__attribute__((address_space(3))) void *)(dst + q * 256), 16, 0, 0);
+            }
+            if (DLR_REF_WDMA && lw == 1)  // the stage's weights (lanes 32..63 again into the slot's last 512 bytes, unused)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(wr + (int64_t)sg * kRefStage + 4 * (lane & 31)),
+                    (__attribute__((address_space(3))) void *)(dst + kRefUnit * kRefStage), 16, 0, 0);
+            return u;
+        };
+        // issue stages [0, LA) first; then per stage g: issue g + LA, wait
+        // for g, publish it
+        int ka = 0, sa = 0, ria = 0;  // the next stage to issue
+        auto issue_next = [&](int g) {
+            const uint32_t u = issue(ka, sa, ria, g);
+            if (++sa == spu) {
+                sa = 0;
+                ++ka;
+            }
+            if (++ria == kRefRing) ria = 0;
+            return u;
+        };
+        for (int g = 0; g < LA; ++g) issue_next(g);
+        uint32_t *mine = ctl + kCtlL0 + lw;
+        for (int g = 0, k = 0, sg = 0;; ++g) {
+            ctl_wait_ge(ctl + kCtlIds, (uint32_t)k + 1);
+            const uint32_t u = ctl_read(s_unit + (k & 3));
+            if (u == kRefNone) break;
+            issue_next(g + LA);
+            if (LA == 6) {  // stage g landed (the LA later stages still in flight)
+                if (npieces == 6)
+                    asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
+            } else {
+                if (npieces == 6)
+                    asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+            }
+            if (lane == 0) ctl_write(mine, (uint32_t)g + 1);
+            if (++sg == spu) {
+                sg = 0;
+                ++k;
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives its wave
+        return;
+    }
+    // compute wave (wave 7: its SIMD's other wave is the chain half's
+    // mostly idle wave 3, not the column chain): lane i < 32 runs row i's
+    // chain; the weights come with the stage (w is read-only until the chain
+    // epilogue, after every margin)
+    const uint32_t xr = (uint32_t)(lane & 7);
+    uint32_t abase[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        abase[k] = lds_addr(ring) + (uint32_t)((lane & 31) >> 3) * 1024 + xr * 128 +
+                   (((uint32_t)k ^ (DLR_REF_SWZ ? xr : 0u)) << 4);
     const __amdgpu_buffer_rsrc_t rres = __builtin_amdgcn_make_buffer_rsrc(resid, 0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc(sy.limit, 0, 0x7FFFFFFF, 0x00020000);
     // claims: unit ids in row order; after the first failed claim none more
-    // (so every workgroup fails exactly once and the head advances by
-    // nunits + mgrid per launch)
+    // (so every margin half fails exactly once and the head advances by
+    // nunits + mgrid per launch).  The atomic's address is made
+    // non-uniform-looking so the compiler's atomic optimizer (a wave scan
+    // that waits for the result at once) leaves it alone: the result is
+    // used only at the end of the unit.
     bool claiming = true;
-    // lane 0 of wave 0: the claim's atomic (its result is used only at the
-    // end of the unit, when the wave drains anyway)
+    int vz;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
     auto claim_issue = [&]() -> uint32_t {
-        return __hip_atomic_fetch_add(sy.head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return __hip_atomic_fetch_add(sy.head + vz, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     auto claim_finish = [&](uint32_t raw) -> uint32_t {
         const uint32_t u = raw - base;
@@ -2842,137 +2978,134 @@ __global__ __launch_bounds__(kRefThreads) void k_dense_ref_margin(DevDense dd, i
         }
         return u;
     };
-    DLR_STAMP64M(0, threadIdx.x == 0);
-    if (wv == 0 && lane == 0) {
+    if (lane == 0) {
         const uint32_t u0 = claim_finish(claim_issue());
         const uint32_t u1 = claiming ? claim_finish(claim_issue()) : kRefNone;
-        s_unit[0] = u0;
-        s_unit[1] = u1;
-        s_unit[2] = kRefNone;
-        s_unit[3] = kRefNone;
+        ctl_write(s_unit + 0, u0);
+        ctl_write(s_unit + 1, u1);
+        ctl_write(ctl + kCtlIds, 2u);
     }
-    __syncthreads();
-    // loaders: stage g of this workgroup's unit sequence into ring[g % 7]:
-    // 16 LDS-DMA pieces of 1 KiB, piece p = columns [8p, 8p + 8) of the stage
-    // for the unit's 32 rows (lane l: row l & 31, 16-byte half l >> 5)
-    const int lw = wv - 1;                // loader 0..2: pieces lw, lw + 3, ...
-    const int npieces = lw == 0 ? 6 : 5;  // of the 16 (6 + 5 + 5)
-    // stage (k, sg): unit slot k of this workgroup's sequence, stage sg of it
-    auto issue = [&](int k, int sg, int ri) {
-        const uint32_t u = s_unit[k & 3];
-        const int64_t col0 = (int64_t)sg * kRefStage;
-        int64_t i = (int64_t)(u == kRefNone ? 0 : u) * kRefUnit + (lane & 31);
-        i = min(i, B - 1);
-        const int64_t row = ref_row(first, i, N);
-        const float *src = dd.X + row * D + col0 + 4 * (lane >> 5);
-        float *dst = ring + (size_t)ri * kRefUnit * kRefStage;
-        for (int p = lw; p < 16; p += 3)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + 8 * p),
-                                             (__attribute__((address_space(3))) void *)(dst + p * 256), 16, 0, 0);
-    };
-    if (wv >= 1) {
-#pragma unroll
-        for (int s0 = 0; s0 < LA; ++s0) issue(0, s0, s0);
-    }
+    DLR_STAMP64M(1, lane == 0);
     float z = 0.0f, y = 0.0f;
     int64_t urow = -1;  // batch row of this lane in the current unit (-1: none)
     uint32_t pend = 0;  // lane 0: the raw claim issued at the start of the unit
     bool have_pend = false;
-    DLR_STAMP64M(1, threadIdx.x == 0);
-    for (int k = 0, sg = 0, ri = 0;;) {
-        const uint32_t u = s_unit[k & 3];
-        if (u == kRefNone) break;  // uniform: every wave read the same LDS word after the last barrier
-        if (wv >= 1) {  // stage g landed (the LA - 1 later stages still in flight)
-            if (LA == 6) {
-                if (npieces == 6)
-                    asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
-                else
-                    asm volatile("s_waitcnt vmcnt(25)" ::: "memory");
-            } else {
-                if (npieces == 6)
-                    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-                else
-                    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-            }
+    for (int g = 0, k = 0, sg = 0, ri = 0;; ++g) {
+        const uint32_t u = ctl_read(s_unit + (k & 3));
+        if (u == kRefNone) break;
+        if (sg == 0) {
+            // the margins' limit: start unit u only once the chains are
+            // within `lead` slots of it (every unit this half still holds is
+            // later: nothing a chain waits for is held here)
+            if (sy.lead > 0 && lane == 0)
+                for (int s = 0; s < kRefSpin / 64; ++s) {
+                    const uint32_t lim = __builtin_amdgcn_raw_buffer_load_b32(lrs, 0, 0, 16);
+                    if ((int32_t)(lim - (base + u)) > 0) break;
+                    __builtin_amdgcn_s_sleep(16);
+                }
+            DLR_STAMP64M(22 + k, lane == 0 && k < 20);
+            urow = lane < kRefUnit && (int64_t)u * kRefUnit + lane < B ? (int64_t)u * kRefUnit + lane : -1;
+            if (urow >= 0) y = dd.label[ref_row(first, urow, N)];
+            z = 0.0f;
+            have_pend = lane == 0 && claiming;
+            if (have_pend) pend = claim_issue();  // the unit after the next one
         }
-        lds_barrier();
-        if (wv == 0) {
-            if (sg == 0) {
-                // the margins' limit: start unit u only once the chains are
-                // within `lead` slots of it (every unit this workgroup still
-                // holds is later: nothing a chain waits for is held here)
-                if (sy.lead > 0 && lane == 0)
-                    for (int s = 0; s < kRefSpin; ++s) {
-                        const uint32_t lim = __builtin_amdgcn_raw_buffer_load_b32(lrs, 0, 0, 16);
-                        if ((int32_t)(lim - (base + u)) > 0) break;
-                        __builtin_amdgcn_s_sleep(16);
-                    }
-                urow = lane < kRefUnit && (int64_t)u * kRefUnit + lane < B ? (int64_t)u * kRefUnit + lane : -1;
-                if (urow >= 0) y = dd.label[ref_row(first, urow, N)];
-                z = 0.0f;
-                have_pend = lane == 0 && claiming;
-                if (have_pend) pend = claim_issue();  // the unit after the next one
-            }
-            if (lane < kRefUnit) {
-                // row chain over the stage's 128 columns in order: 4 groups of
-                // 8 reads (piece p, half h -> columns 8p + 4h .. + 3), the next
-                // group in flight while this one is added
-                const uint32_t a0 = lds_addr(ring + (size_t)ri * kRefUnit * kRefStage) + 16 * lane;
-                const float *__restrict__ wp = wr + sg * kRefStage;
-                v4f xa[8], xb[8];
-                auto grp = [&](const v4f(&x)[8], int gi) {
+        // stage g landed: every loader's pieces of it
+        ctl_wait_ge(ctl + kCtlL0, (uint32_t)g + 1);
+        ctl_wait_ge(ctl + kCtlL1, (uint32_t)g + 1);
+        ctl_wait_ge(ctl + kCtlL2, (uint32_t)g + 1);
+        if (!(DLR_ABL & 64) && lane < kRefUnit) {
+            // row chain over the stage's 128 columns in order: 4 groups of 8
+            // reads (piece p, half h -> columns 8p + 4h .. + 3), the next
+            // group in flight while this one is added
+            uint32_t a[8];
 #pragma unroll
-                    for (int m = 0; m < 8; ++m) {
-                        const v4f wq = *reinterpret_cast<const v4f *>(wp + 32 * gi + 4 * m);
-                        z = z + wq.x * x[m].x;
-                        z = z + wq.y * x[m].y;
-                        z = z + wq.z * x[m].z;
-                        z = z + wq.w * x[m].w;
-                    }
-                };
-                ref_rd8<0>(xa, a0);
-                ref_rd8<1>(xb, a0);
-                DLR_REF_WAIT(8, xa);
-                grp(xa, 0);
-                ref_rd8<2>(xa, a0);
-                DLR_REF_WAIT(8, xb);
-                grp(xb, 1);
-                ref_rd8<3>(xb, a0);
-                DLR_REF_WAIT(8, xa);
-                grp(xa, 2);
-                DLR_REF_WAIT(0, xb);
-                grp(xb, 3);
-            }
-            if (sg == spu - 1) {
-                if (urow >= 0) {
-                    const float r = sigmoid_ref(z) - y;
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), rres, (int)(urow * 4), 0, 16);  // sc1
+            for (int k = 0; k < 8; ++k) a[k] = abase[k] + (uint32_t)ri * (kRefSlotF * 4);
+            const uint32_t wa = lds_addr(ring) + (uint32_t)ri * (kRefSlotF * 4);
+            v4f xa[4], xb[4], wa4[4], wb4[4];
+            auto grp = [&](const v4f(&x)[4], const v4f(&wq)[4]) {
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    z = z + wq[m].x * x[m].x;
+                    z = z + wq[m].y * x[m].y;
+                    z = z + wq[m].z * x[m].z;
+                    z = z + wq[m].w * x[m].w;
                 }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every residual of the unit stored
-                if (lane == 0) {
-                    __hip_atomic_fetch_add(sy.slot_cnt + (u / (kRefSlot / kRefUnit)), 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                    s_unit[(k + 2) & 3] = have_pend ? claim_finish(pend) : kRefNone;
-                }
-                DLR_STAMP64M(2 + k, lane == 0 && k < 40);
-                DLR_STAMP64MV(44 + k, lane == 0 && k < 16, (unsigned long long)u);
-            }
-        } else {
-            int sa = sg + LA, ka = k;  // the stage LA ahead (its ring slot was computed 7 - LA stages ago)
-            if (sa >= spu) {
-                sa -= spu;
-                ++ka;
-            }
-            issue(ka, sa, ri + LA < kRefRing ? ri + LA : ri + LA - kRefRing);
+            };
+            // the stage's 128 columns in order: 8 sets of 16, the next set in
+            // flight while one is added
+            ref_rd8<0, 0>(xa, wa4, a, wa);
+            ref_rd8<0, 1>(xb, wb4, a, wa);
+            DLR_REF_WAIT(8, xa, wa4);
+            grp(xa, wa4);
+            ref_rd8<1, 0>(xa, wa4, a, wa);
+            DLR_REF_WAIT(8, xb, wb4);
+            grp(xb, wb4);
+            ref_rd8<1, 1>(xb, wb4, a, wa);
+            DLR_REF_WAIT(8, xa, wa4);
+            grp(xa, wa4);
+            ref_rd8<2, 0>(xa, wa4, a, wa);
+            DLR_REF_WAIT(8, xb, wb4);
+            grp(xb, wb4);
+            ref_rd8<2, 1>(xb, wb4, a, wa);
+            DLR_REF_WAIT(8, xa, wa4);
+            grp(xa, wa4);
+            ref_rd8<3, 0>(xa, wa4, a, wa);
+            DLR_REF_WAIT(8, xb, wb4);
+            grp(xb, wb4);
+            ref_rd8<3, 1>(xb, wb4, a, wa);
+            DLR_REF_WAIT(8, xa, wa4);
+            grp(xa, wa4);
+            DLR_REF_WAIT(0, xb, wb4);
+            grp(xb, wb4);
         }
+        if (sg == spu - 1) {
+            if (urow >= 0) {
+                const float r = sigmoid_ref(z) - y;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), rres, (int)(urow * 4), 0, 16);  // sc1
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every residual of the unit stored
+            if (lane == 0) {
+                __hip_atomic_fetch_add(sy.slot_cnt + (u / (kRefSlot / kRefUnit)), 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                // the next-but-one unit, before the stage count that lets the
+                // loaders reach it
+                ctl_write(s_unit + ((k + 2) & 3), have_pend ? claim_finish(pend) : kRefNone);
+                ctl_write(ctl + kCtlIds, (uint32_t)k + 3);
+            }
+            DLR_STAMP64M(2 + k, lane == 0 && k < 20);
+            DLR_STAMP64MV(42 + k, lane == 0 && k < 20, (unsigned long long)u);
+        }
+        if (lane == 0) ctl_write(ctl + kCtlComp, (uint32_t)g + 1);  // ring slot ri free
         if (++sg == spu) {
             sg = 0;
             ++k;
         }
         if (++ri == kRefRing) ri = 0;
     }
-    DLR_STAMP64M(63, threadIdx.x == 0);
-    if (wv >= 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives its wave
+    DLR_STAMP64M(63, lane == 0);
+}
+
+// grid: max(D / 16, margin halves) workgroups; workgroup b runs the chain
+// half of stripe b (b < D / 16) and a margin half (b < sy.mgrid)
+template <bool FUSED, int LA>
+__global__ __launch_bounds__(kRefThreads) void k_dense_ref(DevDense dd, int64_t first, int64_t B,
+                                                           const float *__restrict__ wr, float *w,
+                                                           float *__restrict__ gout, float *resid, DevRefSync sy,
+                                                           float Bf, double Bd, float lr, float C) {
+    extern __shared__ __attribute__((aligned(16))) float rsm[];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    uint32_t *ctl = reinterpret_cast<uint32_t *>(rsm + kRefOffCtl);
+    if (threadIdx.x < 16) ctl[threadIdx.x] = threadIdx.x >= kCtlUnit ? kRefNone : 0u;
+    DLR_STAMP64(0, threadIdx.x == 0);
+    __syncthreads();  // the only workgroup barrier: the halves go their own ways
+    if (wv < 4) {
+        if (!(DLR_ABL & 32) && (int)blockIdx.x < (int)(dd.D / kRefCols))
+            ref_chain_half<FUSED>(dd, first, B, w, gout, resid, sy, Bf, Bd, lr, C, rsm, wv, lane);
+    } else if ((int)blockIdx.x < sy.mgrid) {
+        ref_margin_half<LA>(dd, first, B, wr, resid, sy, rsm, wv - 4, lane);
+    }
 }
 #undef DLR_REF_WAIT
 
@@ -3551,35 +3684,31 @@ bool dense_ref_ok(int64_t D, int64_t N, int64_t B) {
 int64_t dense_ref_resid(int64_t B) { return (B + kRefSlot - 1) / kRefSlot * kRefSlot + 4; }
 int64_t dense_ref_sync_words(int64_t B) { return (B + kRefSlot - 1) / kRefSlot + 96; }
 int dense_ref_grid(int64_t D, int64_t B) {
-    return (int)(D / kRefCols + std::min<int64_t>(256, (B + kRefUnit - 1) / kRefUnit));
+    return (int)std::max<int64_t>(D / kRefCols, std::min<int64_t>(256, (B + kRefUnit - 1) / kRefUnit));
 }
 
 hipError_t launch_dense_ref(const DevDense &dd, int64_t first, int64_t B, float *w, float *gout, float *resid,
-                            const DevRefSync &sy_in, float lr, float C, bool fused, hipStream_t chain_s,
-                            hipStream_t margin_s) {
+                            const DevRefSync &sy_in, float lr, float C, bool fused, hipStream_t s) {
     if (B <= 0) return hipSuccess;
     if (!dense_ref_ok(dd.D, dd.N, B) || first < 0 || first >= dd.N) return hipErrorInvalidValue;
-    const int nstripes = (int)(dd.D / kRefCols);
-    const int64_t nunits = (B + kRefUnit - 1) / kRefUnit;
     DevRefSync sy = sy_in;
-    sy.mgrid = (int)std::min<int64_t>(256, nunits);
+    sy.mgrid = (int)std::min<int64_t>(256, (B + kRefUnit - 1) / kRefUnit);
+    const unsigned grid = (unsigned)std::max<int64_t>(dd.D / kRefCols, sy.mgrid);
     const float Bf = (float)B;
     const double Bd = (double)B;
-    // the chains first: their workgroups are resident when the margins start
-    if (fused)
-        hipLaunchKernelGGL(k_dense_ref_chain<true>, dim3(nstripes), dim3(kRefThreads), kRefChainLds, chain_s, dd,
-                           first, B, w, gout, resid, sy, Bf, Bd, lr, C);
+#define DLR_REF(F, L)                                                                                              \
+    hipLaunchKernelGGL((k_dense_ref<F, L>), dim3(grid), dim3(kRefThreads), kRefLds, s, dd, first, B, w, w, gout, resid, \
+                       sy, Bf, Bd, lr, C)
+    const bool la6 = dd.D / kRefStage >= 7;
+    if (fused && la6)
+        DLR_REF(true, 6);
+    else if (fused)
+        DLR_REF(true, 3);
+    else if (la6)
+        DLR_REF(false, 6);
     else
-        hipLaunchKernelGGL(k_dense_ref_chain<false>, dim3(nstripes), dim3(kRefThreads), kRefChainLds, chain_s, dd,
-                           first, B, w, gout, resid, sy, Bf, Bd, lr, C);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    if (dd.D / kRefStage >= 7)
-        hipLaunchKernelGGL(k_dense_ref_margin<6>, dim3(sy.mgrid), dim3(kRefThreads), kRefMarginLds, margin_s, dd,
-                           first, B, w, resid, sy);
-    else
-        hipLaunchKernelGGL(k_dense_ref_margin<3>, dim3(sy.mgrid), dim3(kRefThreads), kRefMarginLds, margin_s, dd,
-                           first, B, w, resid, sy);
+        DLR_REF(false, 3);
+#undef DLR_REF
     return hipGetLastError();
 }
 

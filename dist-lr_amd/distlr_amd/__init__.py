@@ -47,7 +47,7 @@ SYMBOLS = [
     "dlr_summation_order",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
     "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_train_band_rows", "dlr_train_relabeled", "dlr_train_unit_values", "dlr_train_product_margin", "dlr_train_row_rounds",
-    "dlr_set_exchange_overlap", "dlr_exchange_overlap",
+    "dlr_set_exchange_overlap", "dlr_exchange_overlap", "dlr_set_exchange_pieces", "dlr_exchange_pieces",
     "dlr_memory_info", "dlr_stream_bytes",
 ]
 
@@ -167,6 +167,8 @@ _sig("dlr_train_product_margin", C.c_int, P)
 _sig("dlr_train_row_rounds", C.c_int, P)
 _sig("dlr_set_exchange_overlap", C.c_int, P, C.c_int)
 _sig("dlr_exchange_overlap", C.c_int, P)
+_sig("dlr_set_exchange_pieces", C.c_int, P, C.c_int)
+_sig("dlr_exchange_pieces", C.c_int, P)
 _sig("dlr_memory_info", C.c_int, P, C.POINTER(i64), C.POINTER(i64))
 _sig("dlr_stream_bytes", C.c_int, P, C.POINTER(i64), C.POINTER(i64))
 
@@ -616,6 +618,17 @@ class Engine:
         rc = lib.dlr_exchange_overlap(self._h)
         self._c(min(rc, 0))
         return rc == 1
+
+    def set_exchange_pieces(self, pieces: int) -> None:
+        """Pieces of the overlapped all-gather (1..16, default 4) for the
+        next load_train (dlr_set_exchange_pieces; the ranks must agree)."""
+        self._c(lib.dlr_set_exchange_pieces(self._h, int(pieces)))
+
+    def exchange_pieces(self) -> int:
+        """The loaded shard's piece count (0: the gather is not pieced)."""
+        rc = lib.dlr_exchange_pieces(self._h)
+        self._c(min(rc, 0))
+        return rc
 
     def memory_info(self) -> Tuple[int, int]:
         a, b = i64(), i64()

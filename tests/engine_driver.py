@@ -106,7 +106,7 @@ def run_engine(shards: Sequence[dlr.Dataset], D: int, num_iteration: int, batch_
 def run_group(shards: Sequence, D: int, num_iteration: int, batch_size: int, learning_rate: float,
               test=None, test_interval: int = 10, mode: int = dlr.MODE_SYNC_MEAN, C_: float = 1.0,
               random_state: int = 0, dense: bool = False, device: int = 0, setup=None,
-              order: int = dlr.ORDER_REFERENCE) -> EngineRun:
+              order: int = dlr.ORDER_REFERENCE, preload=None) -> EngineRun:
     """RunWorker (main.cc:124-170) with W = len(shards) ranks of ONE device
     linked by the loopback transport (dlr_create_group): the product's
     world > 1 step -- key-range all-to-all, rank-ordered merge, in-place
@@ -130,6 +130,8 @@ def run_group(shards: Sequence, D: int, num_iteration: int, batch_size: int, lea
         eng = engines[r]
         try:
             eng.set_summation_order(order)
+            if preload is not None:
+                preload(eng, r)
             eng.set_weights(w0)                      # every rank holds InitWeight_'s result (main.cc:141-148)
             nb = eng.load_train_dense(shards[r], batch_size) if dense else eng.load_train(shards[r], batch_size)
             if r == 0 and test is not None:

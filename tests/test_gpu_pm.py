@@ -169,6 +169,50 @@ def test_pm_exchange_overlap_on_off(monkeypatch, W):
     assert_same_weights(got[False].w, orc.w, "plain all-gather")
 
 
+@pytest.mark.parametrize("loop", ["async", "sync"])
+@pytest.mark.parametrize("pieces", [1, 3, 16])
+def test_pm_exchange_pieces(monkeypatch, pieces, loop):
+    # the piece count of the overlapped all-gather (dlr_set_exchange_pieces,
+    # a load-time setting), under the stream-ordered loopback collectives
+    # (default: copies wait on the peers' events, as RCCL's) and the
+    # synchronous ones: the oracle's bits whatever the pieces
+    monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
+    monkeypatch.setenv("DLR_PM", "1")
+    monkeypatch.setenv("DLR_LOOPBACK_SYNC", "1" if loop == "sync" else "0")
+    D, W = 300_000, 3
+    shards = [dlr.Dataset.generate(1500, D, 20, value_mode=1, seed=29, stream=r + 1) for r in range(W)]
+    seen = []
+
+    def pre(eng, r):
+        eng.set_exchange_pieces(pieces)
+
+    def setup(eng):
+        seen.append(eng.exchange_pieces())
+
+    got = run_group(shards, D, 2, 250, 0.2, setup=setup, preload=pre)
+    assert seen == [pieces] * W
+    orc = oracle.run_worker([oracle_shard(s, D) for s in shards], D, 2, 250, 0.2)
+    assert_same_weights(got.w, orc.w, f"{pieces} pieces, {loop} loopback")
+
+
+def test_pm_exchange_pieces_must_agree(monkeypatch):
+    # ranks asking for different piece counts: every rank's load fails
+    # (the pieces are collectives), none hangs
+    monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
+    monkeypatch.setenv("DLR_PM", "1")
+    D, W = 50_000, 2
+    shards = [dlr.Dataset.generate(400, D, 10, value_mode=1, seed=31, stream=r + 1) for r in range(W)]
+    with pytest.raises(dlr.DLRError, match="piece counts"):
+        run_group(shards, D, 1, 100, 0.2, preload=lambda eng, r: eng.set_exchange_pieces(2 + r))
+    eng = dlr.Engine(D)
+    try:
+        for bad in (0, 17):
+            with pytest.raises(dlr.DLRError):
+                eng.set_exchange_pieces(bad)
+    finally:
+        eng.close()
+
+
 def test_pm_overlap_through_rccl_one_rank(monkeypatch):
     # the RCCL transport's pieced all-gather (grouped send/recv; no peers at
     # one rank) with every slice in this rank's own range: the same bits

@@ -4,9 +4,10 @@
 build of the library (make -C dist-lr_amd stamps) through DLR_LIB.
 Development tool, never part of the product.
 
-Chain workgroups: slot 0 start, 1 prologue done, 2 + t/16 the end of slot
-iteration t (t = 0, 16, ...), 50 end.  Margin workgroups: 0 start, 1 prologue done,
-2 + k the publish time of its k-th unit, 44 + k that unit's id, 63 end.
+Chain halves (row b of the buffer): 0 start, 2 + t/16 the end of slot t's
+chain (t = 0, 16, ...), 50 end.  Margin halves (row 256 + b): 1 first claims
+done, 2 + k the publish time of its k-th unit, 22 + k its start (after the
+limit), 42 + k its id (k < 20), 63 end.
 
   python tools/c4_stamps.py [--rows N] [--steps K] [--reps R]
 """
@@ -18,7 +19,10 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ.setdefault("DLR_LIB", os.path.join(ROOT, "dist-lr_amd", "lib", "libdistlr_amd_stamps.so"))
+_abl = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--abl=")), "0")
+_n, _, _v = _abl.partition("_")  # "N" or "N_name": make stamps ABL=N [SVAR=name]
+os.environ.setdefault("DLR_LIB", os.path.join(ROOT, "dist-lr_amd", "lib", "libdistlr_amd_stamps%s%s.so" % (
+    "" if _n == "0" else "_abl" + _n, "_" + _v if _v else "")))
 sys.path.insert(0, os.path.join(ROOT, "dist-lr_amd"))
 
 import numpy as np  # noqa: E402
@@ -41,7 +45,12 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--abl", default="0",
+                    help="ablation / variant build: --abl=N (make stamps ABL=N), --abl=N_name (SVAR=name)")
+    ap.add_argument("--lead", type=int, default=None, help="DLR_DENSE_REF_LEAD (0: no limit)")
     a = ap.parse_args()
+    if a.lead is not None:
+        os.environ["DLR_DENSE_REF_LEAD"] = str(a.lead)
     assert "stamps" in dlr.LIB_PATH, dlr.LIB_PATH
     f = dlr.lib.dlr_debug_stamp_buffer
     f.argtypes, f.restype = [C.c_void_p], C.c_int
@@ -69,28 +78,23 @@ def main():
         if rep == 0:
             continue  # warm-up
         ch, mg = st[:S], st[256:256 + M]
-        t0 = min(ch[:, 0].min(), mg[:, 0].min())
+        t0 = ch[:, 0].min()
         us = lambda x: (x - t0) * 0.01  # noqa: E731
         print(f"--- last launch of rep {rep}: {S} chain + {M} margin workgroups, {nslot} slots")
         print("chain start      ", pct(us(ch[:, 0])))
-        print("chain prologue   ", pct(us(ch[:, 1])))
         for t in range(0, nslot + 1, 32):
             print(f"chain slot {t:4d}  ", pct(us(ch[:, 2 + t // 16])))
         print("chain end        ", pct(us(ch[:, 50])))
-        print("margin start     ", pct(us(mg[:, 0])))
-        print("margin prologue  ", pct(us(mg[:, 1])))
-        units = [[] for _ in range(40)]
+        print("margin claims    ", pct(us(mg[:, 1])))
         ids = []
-        for r in range(M):
-            for kk in range(40):
-                if mg[r, 2 + kk] > 0:
-                    units[kk].append(us(mg[r, 2 + kk]))
-            for kk in range(16):
-                if mg[r, 2 + kk] > 0:
-                    ids.append((mg[r, 44 + kk], us(mg[r, 2 + kk])))
-        for kk in range(0, 40, 2):
-            if units[kk]:
-                print(f"margin unit #{kk:2d}   ", pct(units[kk]), f"({len(units[kk])} WGs)")
+        for kk in range(20):
+            m = mg[:, 2 + kk] > 0
+            if not m.any():
+                break
+            st_, pu = us(mg[m, 22 + kk]), us(mg[m, 2 + kk])
+            print(f"margin unit #{kk:2d} start", pct(st_), f"({m.sum()} WGs)")
+            print(f"              busy ", pct(pu - st_))
+            ids += list(zip(mg[m, 42 + kk], pu))
         print("margin end       ", pct(us(mg[:, 63])))
         ids.sort()
         if ids:
