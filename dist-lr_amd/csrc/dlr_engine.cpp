@@ -142,6 +142,7 @@ struct TrainShard {
     // dense shard (dlr_load_train_dense): X row-major n_rows x D
     bool dense = false, dblocked = false, dfused = false;
     float *dX = nullptr, *dpart = nullptr;
+    bool dtiled = false;  // dX is K6r's tiled image (dense_ref_tiled_floats), not row-major
     // reference order, large batches: the banded one-launch step (K6r,
     // k_dense_ref) and its hand-off words (dlr_kernels.h DevRefSync)
     bool dref = false;
@@ -1604,7 +1605,7 @@ hipError_t build_layout(dlr_ctx *c, int64_t b) {
 hipError_t dense_batch(dlr_ctx *c, int64_t b, dlr::DevDense *dd, int64_t *first) {
     TrainShard &t = c->train;
     if (!t.streamed) {
-        *dd = {t.dX, t.label, t.n_rows, c->D};
+        *dd = {t.dX, t.label, t.n_rows, c->D, t.dtiled};
         *first = t.plan[(size_t)b].first_row;
         return hipSuccess;
     }
@@ -2793,7 +2794,7 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
         // chains: the rows the chains re-read stay in the Infinity Cache
         // (DLR_DENSE_REF_LEAD: A/B; 0 = no limit)
         const char *dl = getenv("DLR_DENSE_REF_LEAD");
-        t.dref_lead = dl ? atoi(dl) : 32;
+        t.dref_lead = dl ? atoi(dl) : 64;
     }
     t.fast = t.dblocked;
     // Residency: device-resident unless asked to stream, or (auto) the rows
@@ -2826,6 +2827,21 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
             if ((rc = dev_alloc(c, (void **)&t.sl[k], (size_t)t.B * 4 + 64))) return rc;
             HIPC(c, hipEventRecord(c->ev_free[k], c->stream));
         }
+    } else if (t.dref) {
+        // K6r's tiled image (64 x 64 tiles, dlr_kernels.hip): the rows staged
+        // row-major, transformed on the device
+        float *tmp = nullptr;
+        if ((rc = upload(c, &tmp, ds->X.data(), ds->X.size(), 64))) return rc;
+        const int64_t nf = dlr::dense_ref_tiled_floats(ds->n_rows, D);
+        if ((rc = dev_alloc(c, (void **)&t.dX, (size_t)nf * 4 + 64))) {
+            dev_free(c, tmp);
+            return rc;
+        }
+        hipError_t e = dlr::launch_dense_tile(tmp, t.dX, ds->n_rows, D, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        dev_free(c, tmp);
+        if (e != hipSuccess) return fail(c, DLR_E_HIP, std::string("dlr_load_train_dense: tiling: ") + hipGetErrorString(e));
+        t.dtiled = true;
     } else if ((rc = upload(c, &t.dX, ds->X.data(), ds->X.size(), 64))) {
         return rc;
     }

@@ -173,15 +173,17 @@ struct DevRt {
     int rounds;
 };
 
-// Dense rows (row-major N x D fp32) and 0/1 labels as floats.
+// Dense rows (row-major N x D fp32, or K6r's tiled image: tiled) and 0/1
+// labels as floats.
 struct DevDense {
     const float *X;
     const float *label;
     int64_t N, D;
+    bool tiled = false;
 };
 
 // K6r (k_dense_ref) hand-off state, device words of the loaded shard
-// (zeroed at load): per chain slot of 256 rows the count of its 32-row
+// (zeroed at load): per chain slot of 256 rows the count of its 64-row
 // margin units published, and the margin unit queue head; both monotonic
 // over the launches of the shard (seq = launches so far).
 struct DevRefSync {
@@ -283,6 +285,11 @@ bool dense_ref_ok(int64_t D, int64_t N, int64_t B);
 int64_t dense_ref_sync_words(int64_t B);
 int64_t dense_ref_resid(int64_t B);
 int dense_ref_grid(int64_t D, int64_t B);  // workgroups of the launch
+// K6r's tiled image of a resident shard (64 x 64 tiles, chunk-major; rows
+// padded to a multiple of 64): its size in floats, and the transform from
+// the row-major rows.
+int64_t dense_ref_tiled_floats(int64_t N, int64_t D);
+hipError_t launch_dense_tile(const float *src, float *dst, int64_t N, int64_t D, hipStream_t s);
 hipError_t launch_dense_ref(const DevDense &dd, int64_t first, int64_t B, float *w, float *gout, float *resid,
                             const DevRefSync &sy, float lr, float C, bool fused, hipStream_t s);
 int predict_dense_grid(int64_t rows);

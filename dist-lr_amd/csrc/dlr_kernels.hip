@@ -333,11 +333,16 @@ __device__ __forceinline__ void ordered_segments_dot_piped(int64_t e0, int64_t e
             const int oe = (int)(hi - ws);
             float s = acc[k];
             if (oe - o >= 64) {
+                // the run's products 32 at a time, the next 32's reads in
+                // flight while these are added (reads past the run are
+                // clamped inside the wave's slab and never added)
                 for (; o & 3; ++o) s = s + lds[o];
-                for (; o + 32 <= oe; o += 32) {
-                    float4 q[8];
+                auto rd = [&](float4(&q)[8], int off) {
+                    off = off < kWin - 32 ? off : kWin - 32;
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) q[u] = *reinterpret_cast<const float4 *>(lds + o + 4 * u);
+                    for (int u = 0; u < 8; ++u) q[u] = *reinterpret_cast<const float4 *>(lds + off + 4 * u);
+                };
+                auto add = [&](const float4(&q)[8]) {
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
                         s = s + q[u].x;
@@ -345,6 +350,20 @@ __device__ __forceinline__ void ordered_segments_dot_piped(int64_t e0, int64_t e
                         s = s + q[u].z;
                         s = s + q[u].w;
                     }
+                };
+                const int n32 = (oe - o) >> 5;
+                float4 qa[8], qb[8];
+                rd(qa, o);
+                int g = 0;
+                for (; g + 2 <= n32; g += 2, o += 64) {
+                    rd(qb, o + 32);
+                    add(qa);
+                    rd(qa, o + 64);
+                    add(qb);
+                }
+                if (g < n32) {
+                    add(qa);
+                    o += 32;
                 }
             }
             for (; o + 4 <= oe; o += 4) {
@@ -844,7 +863,25 @@ namespace {
     do {                                                                                             \
         if (cond) g_stamp[(256 + blockIdx.x) * 64 + (slot)] = (v);                                   \
     } while (0)
+// time accumulators (s_memrealtime ticks) of one wave's loop phases
+#define DLR_TACC_DECL(v) unsigned long long v = 0
+#define DLR_TACC_BEGIN() unsigned long long tacc_t = __builtin_amdgcn_s_memrealtime()
+#define DLR_TACC_LAP(v)                                                  \
+    do {                                                                 \
+        const unsigned long long tn = __builtin_amdgcn_s_memrealtime(); \
+        v += tn - tacc_t;                                                \
+        tacc_t = tn;                                                     \
+    } while (0)
 #else
+#define DLR_TACC_DECL(v) \
+    do {                 \
+    } while (0)
+#define DLR_TACC_BEGIN() \
+    do {                 \
+    } while (0)
+#define DLR_TACC_LAP(v) \
+    do {                \
+    } while (0)
 #define DLR_STAMP(slot) \
     do {                \
     } while (0)
@@ -2563,7 +2600,7 @@ __global__ __launch_bounds__(256) void k_dense_combine(const float *__restrict__
 //   chain half (waves 0-3; workgroup b < D/16 owns columns [16b, 16b + 16)):
 //     wave 0    lane c runs column c's chain over each slot's products (LDS,
 //               16-byte reads, 256 rows per slot) -- its only work;
-//     waves 1-2 load slot t's 256 rows x 16 columns into registers (three
+//     waves 1-2 load slot t's 256 rows x 16 columns into registers (six
 //               slots in flight: the rows were read from HBM moments ago by
 //               the margin halves and come back from the Infinity Cache),
 //               form fl32(r_i * x_ij) and store them transposed;
@@ -2572,42 +2609,47 @@ __global__ __launch_bounds__(256) void k_dense_combine(const float *__restrict__
 //               publishes the margins' LIMIT, `lead` slots past its own
 //               progress, so the rows the chains re-read are still in the
 //               Infinity Cache;
-//   margin half (waves 4-7): claims units of 32 batch rows in row order from
+//   margin half (waves 4-7): claims units of 64 batch rows in row order from
 //     a queue (rows finish in order, and any resident subset of workgroups
 //     drains it), waits for the limit before it starts a unit (holding only
 //     later units: no chain waits on it), streams the unit's rows through a
-//     7-stage LDS ring by LDS-DMA (waves 5-7, six stages in flight) while
-//     lane i of wave 4 runs row i's chain in column order; publishes
-//     sigma - y with sc1 stores and one agent-scope add to the slot's counter
-//     (MI355X_MICROARCH.md, inter-workgroup hand-off, the sc1 row).
+//     7-stage LDS ring, 64 columns a stage, by LDS-DMA (waves 4-6, six stages
+//     in flight) while lane i of wave 7 runs row i's chain in column order;
+//     publishes sigma - y with sc1 stores and one agent-scope add to the
+//     slot's counter (MI355X_MICROARCH.md, inter-workgroup hand-off, the sc1
+//     row).
 //
-// The weights are written only by the chain epilogue, after its last slot:
-// by then every unit -- every read of w -- is done.  Counters and the queue
-// are monotonic over launches (sy.seq), so nothing is reset between steps.
-// Every wait is bounded (kRefSpin polls): a launch whose producers never
-// come runs to the end with wrong sums instead of hanging the GPU.  X is
-// read once from HBM (the margins) and once from the Infinity Cache (the
-// chains).
-#ifndef DLR_REF_SWZ  // A/B (stamps variants): the chunk swizzle of the margin ring
-#define DLR_REF_SWZ 1
-#endif
-#ifndef DLR_REF_WDMA  // A/B: the stage's weights by LDS-DMA (0: timing only, wrong sums)
-#define DLR_REF_WDMA 1
-#endif
-constexpr int kRefCols = 16;     // columns per chain half
-constexpr int kRefSlot = 256;    // batch rows per chain slot
-constexpr int kRefUnit = 32;     // batch rows per margin unit (one lane each)
-constexpr int kRefStage = 128;   // columns per margin stage
-constexpr int kRefRing = 7;      // margin stages in the LDS ring (up to 6 in flight)
+// X in HBM (a resident shard, dense_ref_tiled): tiles of 64 rows x 64
+// columns, 16 KiB each, chunk-major inside (16-byte chunk k of the tile's
+// rows 0..63, then chunk k + 1), the tiles of a 64-row block in column
+// order -- a margin stage is ONE contiguous 16 KiB read whose LDS image the
+// compute lanes read without bank conflicts (lane = row, 16 bytes apart),
+// and a chain slot reads 1 KiB runs.  (Row-major X, a streamed batch: the
+// same kernel with per-row addresses.)  The weights are written only by the
+// chain epilogue, after its last slot: by then every unit -- every read of
+// w -- is done.  Counters and the queue are monotonic over launches
+// (sy.seq), so nothing is reset between steps.  Every wait is bounded
+// (kRefSpin polls): a launch whose producers never come runs to the end with
+// wrong sums instead of hanging the GPU.  X is read once from HBM (the
+// margins) and once from the Infinity Cache (the chains).
+constexpr int kRefCols = 16;      // columns per chain half
+constexpr int kRefSlot = 256;     // batch rows per chain slot
+constexpr int kRefUnit = 64;      // batch rows per margin unit (one lane each) = rows of a tile
+constexpr int kRefStage = 64;     // columns per margin stage = columns of a tile
+constexpr int kRefChunks = kRefStage / 4;  // 16-byte chunks of a tile row
+constexpr int kRefRing = 7;       // margin stages in the LDS ring (6 in flight)
+constexpr int kRefLA = kRefRing - 1;
 constexpr int kRefPad = kRefSlot + 4;
+constexpr int kRefHD = 6;         // chain slots whose rows a helper has in flight
 constexpr int kRefThreads = 512;
 constexpr uint32_t kRefNone = 0xFFFFFFFFu;
 constexpr int kRefSpin = 1 << 22;
 // LDS (floats): chain products [2][16][kRefPad], residuals [2][256], the
-// margin ring [7][32 x 128 + 256], then 16 words of hand-off counters / unit ids
+// margin ring [7][64 x 64 + 256 (the stage's 64 weights, in a 1 KiB area)],
+// then 16 words of hand-off counters / unit ids
+constexpr int kRefSlotF = kRefUnit * kRefStage + 256;
 constexpr int kRefOffR = 2 * kRefCols * kRefPad;
 constexpr int kRefOffRing = kRefOffR + 2 * kRefSlot;
-constexpr int kRefSlotF = kRefUnit * kRefStage + 256;  // a ring slot: the stage's rows + its 128 weights (1 KiB)
 constexpr int kRefOffCtl = kRefOffRing + kRefRing * kRefSlotF;
 constexpr size_t kRefLds = (size_t)(kRefOffCtl + 16) * 4;
 static_assert(kRefLds <= 160 * 1024, "one workgroup per CU");
@@ -2623,6 +2665,16 @@ enum { kCtlH0 = 0, kCtlH1, kCtlChain, kCtlR, kCtlL0, kCtlL1, kCtlL2, kCtlComp, k
 __device__ __forceinline__ int64_t ref_row(int64_t first, int64_t i, int64_t N) {
     const int64_t r = first + i;
     return r >= N ? r - N : r;
+}
+
+// Float offset in X of 16-byte chunk k (columns 4k .. 4k + 3) of shard row
+// `row`: tiled (above) or row-major.
+template <bool TILED>
+__device__ __forceinline__ int64_t ref_xoff(int64_t row, int64_t k, int64_t D) {
+    if constexpr (TILED)
+        return ((((row >> 6) * (D / kRefStage) + (k >> 4)) * kRefChunks + (k & 15)) * kRefUnit + (row & 63)) * 4;
+    else
+        return row * D + 4 * k;
 }
 
 // LDS hand-off words between the waves of one half (no s_barrier: the two
@@ -2641,31 +2693,117 @@ __device__ __forceinline__ void ctl_write(uint32_t *p, uint32_t v) {
 __device__ __forceinline__ void ctl_wait_ge(const uint32_t *p, uint32_t v) {
     for (int k = 0; k < kRefSpin && (int32_t)(ctl_read(p) - v) < 0; ++k) __builtin_amdgcn_s_sleep(0);
 }
+// The per-stage / per-slot hand-offs: a plain ds_write (a wave's LDS
+// operations complete in order, so the data it stored before -- or the
+// LDS-DMA its vmcnt wait covered -- lands first), and polls that return the
+// value seen, so a consumer that is behind its producer (the usual case)
+// skips the next polls: one LDS round trip per hand-off instead of three.
+__device__ __forceinline__ void ctl_post(uint32_t *p, uint32_t v) {
+    asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ uint32_t ctl_poll(const uint32_t *p, uint32_t v) {
+    uint32_t x = ctl_read(p);
+    for (int k = 0; k < kRefSpin && (int32_t)(x - v) < 0; ++k) {
+        __builtin_amdgcn_s_sleep(0);
+        x = ctl_read(p);
+    }
+    return x;
+}
+// min of the counters p[0], p[1] (N = 2) or p[0..2] (N = 3; p 16-byte aligned)
+template <int N>
+__device__ __forceinline__ uint32_t ctl_read_min(const uint32_t *p) {
+    if constexpr (N == 2) {
+        uint2 v;
+        asm volatile("ds_read_b64 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+        return min(v.x, v.y);
+    } else {
+        u32x4 v;
+        asm volatile("ds_read_b128 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+        return min(min(v.x, v.y), v.z);
+    }
+}
+template <int N>
+__device__ __forceinline__ uint32_t ctl_poll_min(const uint32_t *p, uint32_t v) {
+    uint32_t x = ctl_read_min<N>(p);
+    for (int k = 0; k < kRefSpin && (int32_t)(x - v) < 0; ++k) {
+        __builtin_amdgcn_s_sleep(0);
+        x = ctl_read_min<N>(p);
+    }
+    return x;
+}
 
-// A margin stage in the ring: 16 blocks of 1 KiB, block q = 4L + G holds
-// line L (columns [32L, 32L + 32) of the stage, 128 bytes) of the rows
-// [8G, 8G + 8) of the unit, row r at (r & 7) * 128 and its 16-byte chunk k
-// at ((k ^ (r & 7)) * 16) -- each LDS-DMA instruction reads 8 whole lines
-// from HBM, and the compute lanes' 16-byte reads (lane = row) meet no bank
-// conflict.  After the 16 blocks: the stage's 128 weights (w[128 sg ..]).
-// ref_rd8<L, H>: row i's chunks 4H .. 4H + 3 of line L (a[k] = the
-// lane's base + ((k ^ (i & 7)) * 16)) and their 16 weights (wa: the slot,
-// uniform; every lane reads the same 16 bytes, an LDS broadcast) -- eight
-// reads, so that two sets in flight stay within lgkmcnt's 15.
-template <int L, int H>
-__device__ __forceinline__ void ref_rd8(v4f (&d)[4], v4f (&wq)[4], const uint32_t (&a)[8], uint32_t wa) {
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[0]) : "v"(a[4 * H + 0]), "n"(L * 4096));
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[1]) : "v"(a[4 * H + 1]), "n"(L * 4096));
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[2]) : "v"(a[4 * H + 2]), "n"(L * 4096));
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[3]) : "v"(a[4 * H + 3]), "n"(L * 4096));
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(wq[0]) : "v"(wa), "n"(16384 + L * 128 + H * 64 + 0));
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(wq[1]) : "v"(wa), "n"(16384 + L * 128 + H * 64 + 16));
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(wq[2]) : "v"(wa), "n"(16384 + L * 128 + H * 64 + 32));
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(wq[3]) : "v"(wa), "n"(16384 + L * 128 + H * 64 + 48));
+// A margin stage in its ring slot: chunk k of rows 0..63 at k * 1 KiB + row *
+// 16 (the tile's own image), the stage's 64 weights at 16 KiB.  ref_rd8<S>:
+// set S (chunks 4S .. 4S + 3, 16 columns) of the lane's row (a = slot + 16 *
+// lane) and their weights (wa = slot, uniform: every lane reads the same 16
+// bytes, an LDS broadcast) -- eight reads, so that two sets in flight stay
+// within lgkmcnt's 15.
+template <int S>
+__device__ __forceinline__ void ref_rd8(v4f (&d)[4], v4f (&wq)[4], uint32_t a, uint32_t wa) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[0]) : "v"(a), "n"((4 * S + 0) * 1024));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[1]) : "v"(a), "n"((4 * S + 1) * 1024));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[2]) : "v"(a), "n"((4 * S + 2) * 1024));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d[3]) : "v"(a), "n"((4 * S + 3) * 1024));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(wq[0]) : "v"(wa), "n"(16384 + (4 * S + 0) * 16));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(wq[1]) : "v"(wa), "n"(16384 + (4 * S + 1) * 16));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(wq[2]) : "v"(wa), "n"(16384 + (4 * S + 2) * 16));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(wq[3]) : "v"(wa), "n"(16384 + (4 * S + 3) * 16));
 }
 #define DLR_REF_WAIT(N, d, e)                                                                                 \
     asm volatile("s_waitcnt lgkmcnt(" #N ")"                                                                 \
                  : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(e[0]), "+v"(e[1]), "+v"(e[2]), "+v"(e[3]))
+
+// fl32(w_c * x_c) of a set's 16 columns
+__device__ __forceinline__ void ref_products(float (&p)[16], const v4f (&x)[4], const v4f (&wq)[4]) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        p[4 * m + 0] = wq[m].x * x[m].x;
+        p[4 * m + 1] = wq[m].y * x[m].y;
+        p[4 * m + 2] = wq[m].z * x[m].z;
+        p[4 * m + 3] = wq[m].w * x[m].w;
+    }
+}
+// z += p0; n0 = w0 * x0; z += p1; ... : a set's adds in order (each waits
+// for the last: the row chain), the next set's products issued in their
+// shadow.  v_add_f32 / v_mul_f32 round as the C operators do (-ffp-contract
+// =off: never fused).
+#define DLR_REF_ADDMUL4(z, p, n, w4, x4)                                                               \
+    asm volatile("v_add_f32 %0, %0, %5\n v_mul_f32 %1, %9, %13\n"                                     \
+                 "v_add_f32 %0, %0, %6\n v_mul_f32 %2, %10, %14\n"                                    \
+                 "v_add_f32 %0, %0, %7\n v_mul_f32 %3, %11, %15\n"                                    \
+                 "v_add_f32 %0, %0, %8\n v_mul_f32 %4, %12, %16"                                       \
+                 : "+v"(z), "=&v"(n[0]), "=&v"(n[1]), "=&v"(n[2]), "=&v"(n[3])                         \
+                 : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(w4.x), "v"(w4.y), "v"(w4.z), "v"(w4.w), \
+                   "v"(x4.x), "v"(x4.y), "v"(x4.z), "v"(x4.w))
+// Set S of the stage's four (data of set s in buffer s % 3, products of set
+// s in pp[s & 1]): wait for set S + 1's reads (set S + 2's still in flight),
+// issue set S + 3's into set S's buffer (its products were formed in set
+// S - 1), then add set S's products while forming set S + 1's.
+template <int S>
+__device__ __forceinline__ void ref_set(float &z, v4f (&xd)[3][4], v4f (&wd)[3][4], float (&pp)[2][16], uint32_t a,
+                                        uint32_t wa) {
+    constexpr int NS = kRefChunks / 4;
+    constexpr int N1 = (S + 1) % 3, N3 = S % 3;
+    if constexpr (S + 1 < NS) {
+        if constexpr (S + 2 < NS)
+            DLR_REF_WAIT(8, xd[N1], wd[N1]);
+        else
+            DLR_REF_WAIT(0, xd[N1], wd[N1]);
+    }
+    if constexpr (S + 3 < NS) ref_rd8<S + 3>(xd[N3], wd[N3], a, wa);
+    float(&pc)[16] = pp[S & 1];
+    if constexpr (S + 1 < NS) {
+        float(&pn)[16] = pp[(S + 1) & 1];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            float *pcm = pc + 4 * m, *pnm = pn + 4 * m;
+            DLR_REF_ADDMUL4(z, pcm, pnm, wd[N1][m], xd[N1][m]);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) z = z + pc[k];
+    }
+}
 
 // The queue position (claims so far) at the start of launch seq: every
 // launch makes nunits successful claims and one failed claim per margin half.
@@ -2674,7 +2812,7 @@ __device__ __forceinline__ uint32_t ref_base(const DevRefSync &sy, int64_t nunit
 }
 
 // The chain half of workgroup blockIdx.x (< D / 16).
-template <bool FUSED>
+template <bool FUSED, bool TILED>
 __device__ __forceinline__ void ref_chain_half(const DevDense &dd, int64_t first, int64_t B, float *w,
                                                float *__restrict__ gout, float *resid, const DevRefSync &sy,
                                                float Bf, double Bd, float lr, float C, float *rsm, int wv,
@@ -2692,69 +2830,95 @@ __device__ __forceinline__ void ref_chain_half(const DevDense &dd, int64_t first
         cg = ((k >> 1) << 4) | ((blockIdx.x & 7) << 1) | (k & 1);
     }
     const int64_t c0 = (int64_t)cg * kRefCols;
-    // helpers: lane hl in [0, 128) owns 4x4 blocks b = hl, hl + 128 of the
-    // slot (row quad b >> 2, column quad b & 3)
+    // helpers: lane hl in [0, 128); its load v (0..7) is chunk v >> 1 of
+    // the stripe for slot row r = 128 (v & 1) + hl -- a wave reads 64
+    // consecutive rows of one chunk (1 KiB of a tile)
     const int hl = (wv - 1) * kWave + lane;
     auto load = [&](int64_t t, v4f (&x)[8]) {
         const int64_t tc = t < nslot ? t : nslot - 1;  // past the end: the last slot again (never used)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int b = hl + 128 * h;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int64_t i = min<int64_t>(tc * kRefSlot + 4 * (b >> 2) + u, B - 1);
-                x[4 * h + u] = __builtin_nontemporal_load(
-                    reinterpret_cast<const v4f *>(dd.X + ref_row(first, i, N) * D + c0 + 4 * (b & 3)));
-            }
+        for (int v = 0; v < 8; ++v) {
+            const int64_t i = min<int64_t>(tc * kRefSlot + 128 * (v & 1) + hl, B - 1);
+            x[v] = __builtin_nontemporal_load(
+                reinterpret_cast<const v4f *>(dd.X + ref_xoff<TILED>(ref_row(first, i, N), c0 / 4 + (v >> 1), D)));
         }
     };
     auto transform = [&](int64_t t, const v4f (&x)[8]) {
         const float *sr = s_r + (t & 1) * kRefSlot;
         float *sp = s_p + (t & 1) * kRefCols * kRefPad;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int b = hl + 128 * h, rq = b >> 2, cq = b & 3;
-            const v4f r4 = *reinterpret_cast<const v4f *>(sr + 4 * rq);
-            const float rr[4] = {r4.x, r4.y, r4.z, r4.w};
-            float p[4][4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const bool ok = t * kRefSlot + 4 * rq + u < B;  // rows past B: +0 (never -0 in a sum from +0)
-                const v4f xv = x[4 * h + u];
-                p[u][0] = ok ? rr[u] * xv.x : 0.0f;
-                p[u][1] = ok ? rr[u] * xv.y : 0.0f;
-                p[u][2] = ok ? rr[u] * xv.z : 0.0f;
-                p[u][3] = ok ? rr[u] * xv.w : 0.0f;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                *reinterpret_cast<v4f *>(sp + (4 * cq + q) * kRefPad + 4 * rq) = v4f{p[0][q], p[1][q], p[2][q], p[3][q]};
+        for (int v = 0; v < 8; ++v) {
+            const int r = 128 * (v & 1) + hl, cc = v >> 1;
+            const bool ok = t * kRefSlot + r < B;  // rows past B: +0 (never -0 in a sum from +0)
+            const float rr = sr[r];
+            sp[(4 * cc + 0) * kRefPad + r] = ok ? rr * x[v].x : 0.0f;
+            sp[(4 * cc + 1) * kRefPad + r] = ok ? rr * x[v].y : 0.0f;
+            sp[(4 * cc + 2) * kRefPad + r] = ok ? rr * x[v].z : 0.0f;
+            sp[(4 * cc + 3) * kRefPad + r] = ok ? rr * x[v].w : 0.0f;
         }
     };
     if (wv == 0) {
         // the chain: slot t once both helpers have stored it
         float acc = 0.0f;
-        for (int64_t t = 0; t < nslot; ++t) {
-            ctl_wait_ge(ctl + kCtlH0, (uint32_t)t + 1);
-            ctl_wait_ge(ctl + kCtlH1, (uint32_t)t + 1);
-            const float *sp = s_p + (t & 1) * kRefCols * kRefPad + (lane & (kRefCols - 1)) * kRefPad;
-#pragma unroll 2
-            for (int k = 0; k < kRefSlot; k += 32) {
-                v4f d[8];
+        uint32_t hk = 0;  // slots both helpers are known to have stored
+        DLR_TACC_DECL(t_cw);
+        DLR_TACC_DECL(t_ca);
+        DLR_STAMP64V(60, lane == 0, __builtin_amdgcn_s_memtime());  // shader clock: the clock under load
+        DLR_STAMP64V(61, lane == 0, __builtin_amdgcn_s_memrealtime());
+        // 256 products a slot, 32 at a time: the next 32's reads -- across
+        // the slot boundary too, once the helpers have stored the next slot
+        // -- in flight while these are added
+        const int cl = lane & (kRefCols - 1);
+        auto sp_of = [&](int64_t t) { return s_p + (t & 1) * kRefCols * kRefPad + cl * kRefPad; };
+        auto rd = [&](v4f(&d)[8], const float *q) {
 #pragma unroll
-                for (int u = 0; u < 8; ++u) d[u] = *reinterpret_cast<const v4f *>(sp + k + 4 * u);
+            for (int u = 0; u < 8; ++u) d[u] = *reinterpret_cast<const v4f *>(q + 4 * u);
+        };
+        auto add = [&](const v4f(&d)[8]) {
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    acc = acc + d[u].x;
-                    acc = acc + d[u].y;
-                    acc = acc + d[u].z;
-                    acc = acc + d[u].w;
-                }
+            for (int u = 0; u < 8; ++u) {
+                acc = acc + d[u].x;
+                acc = acc + d[u].y;
+                acc = acc + d[u].z;
+                acc = acc + d[u].w;
             }
-            if (lane == 0) ctl_write(ctl + kCtlChain, (uint32_t)t + 1);
+        };
+        v4f da[8], db[8];
+        {
+            DLR_TACC_BEGIN();
+            hk = ctl_poll_min<2>(ctl + kCtlH0, 1u);
+            DLR_TACC_LAP(t_cw);
+        }
+        rd(da, sp_of(0));
+        for (int64_t t = 0; t < nslot; ++t) {
+            DLR_TACC_BEGIN();
+            const float *sp = sp_of(t);
+#pragma unroll 1
+            for (int k = 0; k < kRefSlot - 64; k += 64) {
+                rd(db, sp + k + 32);
+                add(da);
+                rd(da, sp + k + 64);
+                add(db);
+            }
+            rd(db, sp + kRefSlot - 32);
+            add(da);
+            const bool more = t + 1 < nslot;
+            if (more && (int32_t)(hk - ((uint32_t)t + 2)) < 0) {
+                DLR_TACC_LAP(t_ca);
+                hk = ctl_poll_min<2>(ctl + kCtlH0, (uint32_t)t + 2);
+                DLR_TACC_LAP(t_cw);
+            }
+            rd(da, more ? sp_of(t + 1) : sp);  // (after the last slot: a re-read, unused)
+            add(db);
+            if (lane == 0) ctl_post(ctl + kCtlChain, (uint32_t)t + 1);
+            DLR_TACC_LAP(t_ca);
             DLR_STAMP64(2 + (int)(t >> 4), lane == 0 && (t & 15) == 0 && t < 16 * 40);
         }
         DLR_STAMP64(50, lane == 0);
+        DLR_STAMP64V(62, lane == 0, __builtin_amdgcn_s_memtime());
+        DLR_STAMP64V(63, lane == 0, __builtin_amdgcn_s_memrealtime());
+        DLR_STAMP64V(52, lane == 0, t_cw);
+        DLR_STAMP64V(53, lane == 0, t_ca);
         const int64_t j = c0 + lane;
         if (lane >= kRefCols || j >= D) return;
         const float wj = w[j];
@@ -2772,23 +2936,36 @@ __device__ __forceinline__ void ref_chain_half(const DevDense &dd, int64_t first
     if (wv <= 2) {
         // helpers: slot t needs its residuals staged and the products buffer
         // of slot t - 2 consumed by the chain
+        // (kRefHD slots' loads in flight: the re-read rows come from the
+        // Infinity Cache, microseconds away under the margins' stream)
         uint32_t *mine = ctl + (wv == 1 ? kCtlH0 : kCtlH1);
-        v4f xa[8], xb[8], xc[8];
-        load(0, xa);
-        load(1, xb);
-        load(2, xc);
-        auto step = [&](int64_t t, v4f (&x)[8]) {
-            ctl_wait_ge(ctl + kCtlR, (uint32_t)t + 1);
-            if (t >= 2) ctl_wait_ge(ctl + kCtlChain, (uint32_t)t - 1);
-            transform(t, x);
-            if (lane == 0) ctl_write(mine, (uint32_t)t + 1);
-            load(t + 3, x);
-        };
-        for (int64_t t = 0; t < nslot; t += 3) {
-            step(t, xa);
-            if (t + 1 < nslot) step(t + 1, xb);
-            if (t + 2 < nslot) step(t + 2, xc);
+        uint32_t rk = 0, ck = 0;  // residual slots known staged, chain slots known done
+        DLR_TACC_DECL(t_hr);
+        DLR_TACC_DECL(t_hc);
+        DLR_TACC_DECL(t_hx);
+        v4f x[kRefHD][8];
+#pragma unroll
+        for (int d = 0; d < kRefHD; ++d) load(d, x[d]);
+        for (int64_t t0 = 0; t0 < nslot; t0 += kRefHD) {
+#pragma unroll
+            for (int d = 0; d < kRefHD; ++d) {
+                const int64_t t = t0 + d;
+                if (t < nslot) {
+                    DLR_TACC_BEGIN();
+                    if ((int32_t)(rk - ((uint32_t)t + 1)) < 0) rk = ctl_poll(ctl + kCtlR, (uint32_t)t + 1);
+                    DLR_TACC_LAP(t_hr);
+                    if (t >= 2 && (int32_t)(ck - ((uint32_t)t - 1)) < 0) ck = ctl_poll(ctl + kCtlChain, (uint32_t)t - 1);
+                    DLR_TACC_LAP(t_hc);
+                    transform(t, x[d]);
+                    if (lane == 0) ctl_post(mine, (uint32_t)t + 1);
+                    load(t + kRefHD, x[d]);
+                    DLR_TACC_LAP(t_hx);
+                }
+            }
         }
+        DLR_STAMP64V(54, lane == 0 && wv == 1, t_hr);
+        DLR_STAMP64V(55, lane == 0 && wv == 1, t_hc);
+        DLR_STAMP64V(56, lane == 0 && wv == 1, t_hx);
         return;
     }
     // wave 3: the residuals.  Its view of the margins: every slot <= ready
@@ -2814,6 +2991,8 @@ __device__ __forceinline__ void ref_chain_half(const DevDense &dd, int64_t first
         if (lane == 0) __builtin_amdgcn_raw_buffer_store_b32(qbase + (uint32_t)lim, lrs, 0, 0, 16);
     };
     int64_t ready = -1;
+    DLR_TACC_DECL(t_rp);
+    DLR_TACC_DECL(t_rh);
     auto poll_from = [&](int64_t t0) {
         const uint32_t want0 = slot_target(t0);
         for (int k = 0; k < kRefSpin; ++k) {
@@ -2830,19 +3009,23 @@ __device__ __forceinline__ void ref_chain_half(const DevDense &dd, int64_t first
     };
     auto r_issue = [&](int64_t t, v4f &rv) {
         const int64_t tc = t < nslot ? t : nslot - 1;  // past the end: a load of a published slot, unused
-        if (tc > ready) poll_from(tc);
+        if (tc > ready) {
+            DLR_TACC_BEGIN();
+            poll_from(tc);
+            DLR_TACC_LAP(t_rp);
+        }
         const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rrs, (int)((tc * kRefSlot + 4 * lane) * 4), 0, 16);
         __builtin_memcpy(&rv, &q, 16);
     };
     // slot t's residuals into s_r[t & 1] once both helpers are done with
     // slot t - 2 (the same buffer)
+    uint32_t hk = 0;  // slots both helpers are known to have stored
     auto r_store = [&](int64_t t, const v4f &rv) {
-        if (t >= 2) {
-            ctl_wait_ge(ctl + kCtlH0, (uint32_t)t - 1);
-            ctl_wait_ge(ctl + kCtlH1, (uint32_t)t - 1);
-        }
+        DLR_TACC_BEGIN();
+        if (t >= 2 && (int32_t)(hk - ((uint32_t)t - 1)) < 0) hk = ctl_poll_min<2>(ctl + kCtlH0, (uint32_t)t - 1);
+        DLR_TACC_LAP(t_rh);
         *reinterpret_cast<v4f *>(s_r + (t & 1) * kRefSlot + 4 * lane) = rv;
-        if (lane == 0) ctl_write(ctl + kCtlR, (uint32_t)t + 1);
+        if (lane == 0) ctl_post(ctl + kCtlR, (uint32_t)t + 1);
     };
     v4f ra, rb, rc;
     if (leader) publish_limit(0);
@@ -2859,56 +3042,62 @@ __device__ __forceinline__ void ref_chain_half(const DevDense &dd, int64_t first
         if (t + 1 < nslot) step(t + 1, rb);
         if (t + 2 < nslot) step(t + 2, rc);
     }
+    DLR_STAMP64V(57, lane == 0, t_rp);
+    DLR_STAMP64V(58, lane == 0, t_rh);
 }
 
-// The margin half (the workgroup's waves 4-7; mw = wave - 4).  LA: stages a
-// loader keeps in flight ahead of the one computed (6; 3 when a unit has
-// fewer than 7 stages, D < 896, so that a loader never needs a unit two
-// ahead).  wr: read-only here (the chains update w after every margin is
-// published).
-template <int LA>
+// The margin half (the workgroup's waves 4-7; mw = wave - 4).  wr: read-only
+// here (the chains update w after every margin is published).
+template <bool TILED>
 __device__ __forceinline__ void ref_margin_half(const DevDense &dd, int64_t first, int64_t B,
                                                 const float *__restrict__ wr, float *resid, const DevRefSync &sy,
                                                 float *rsm, int mw, int lane) {
     const int64_t D = dd.D, N = dd.N;
     const int64_t nunits = (B + kRefUnit - 1) / kRefUnit;
-    float *ring = rsm + kRefOffRing;  // [kRefRing][16 x 2 x 32][16 B]
+    float *ring = rsm + kRefOffRing;  // [kRefRing][kRefSlotF]
     uint32_t *ctl = reinterpret_cast<uint32_t *>(rsm + kRefOffCtl);
     uint32_t *s_unit = ctl + kCtlUnit;  // [4]
-    const int spu = (int)(D / kRefStage);  // stages per unit (>= 4)
+    const int spu = (int)(D / kRefStage);  // stages per unit (>= 8)
     const uint32_t base = ref_base(sy, nunits);
     if (mw < 3) {
-        // loaders: stage g of this half's unit sequence into ring[g % 7]: the
-        // 16 blocks above, one LDS-DMA instruction each (lane l: row
-        // 8G + (l >> 3), chunk (l & 7) ^ (l >> 3) of line L).  Stage g + LA
-        // goes into the slot stage g + LA - 7 used, once the compute is past
-        // it; stage g is published (kCtlL0 + lw) once this loader's blocks of
-        // it have landed.
-        const int lw = mw;                   // loader 0..2: blocks lw, lw + 3, ...
+        // loaders: stage g of this half's unit sequence into ring[g % 7]:
+        // chunk q of the unit's 64 rows per LDS-DMA instruction (1 KiB; lane
+        // l: row l), and loader 1 the stage's 64 weights too.  Stage g is
+        // published (kCtlL0 + lw) once this loader's pieces of it have
+        // landed; stage g + 6 goes into the slot stage g - 1 used, once the
+        // compute is past it.
+        const int lw = mw;                    // loader 0..2: chunks lw, lw + 3, ...
         const int npieces = lw == 2 ? 5 : 6;  // of the 16 + 1 (6 + 5 + 5, and loader 1 the weights)
-        const int lrow = lane >> 3, lchunk = DLR_REF_SWZ ? (lane & 7) ^ (lane >> 3) : (lane & 7);
+        uint32_t compk = 0;  // stages the compute is known to be past
+        int kc = -1;         // the unit whose id uc is
+        uint32_t uc = kRefNone;
         auto issue = [&](int k, int sg, int ri, int g) {
-            if (g >= kRefRing) ctl_wait_ge(ctl + kCtlComp, (uint32_t)(g - kRefRing + 1));
-            ctl_wait_ge(ctl + kCtlIds, (uint32_t)k + 1);
-            const uint32_t u = ctl_read(s_unit + (k & 3));
-            const int64_t ubase = (int64_t)(u == kRefNone ? 0 : u) * kRefUnit;
-            const int64_t col0 = (int64_t)sg * kRefStage + 4 * lchunk;
-            float *dst = ring + (size_t)ri * kRefSlotF;
-            for (int q = lw; q < 16; q += 3) {
-                const int L = q >> 2, G = q & 3;
-                const int64_t i = min(ubase + 8 * G + lrow, B - 1);
-                const float *src = dd.X + ref_row(first, i, N) * D + col0 + 32 * L;
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                                 (__attribute__((address_space(3))) void *)(dst + q * 256), 16, 0, 0);
+            if (g >= kRefRing && (int32_t)(compk - (uint32_t)(g - kRefRing + 1)) < 0)
+                compk = ctl_poll(ctl + kCtlComp, (uint32_t)(g - kRefRing + 1));
+            if (k != kc) {
+                ctl_wait_ge(ctl + kCtlIds, (uint32_t)k + 1);
+                uc = ctl_read(s_unit + (k & 3));
+                kc = k;
             }
-            if (DLR_REF_WDMA && lw == 1)  // the stage's weights (lanes 32..63 again into the slot's last 512 bytes, unused)
+            const uint32_t u = uc;
+            const int64_t i = min((int64_t)(u == kRefNone ? 0 : u) * kRefUnit + lane, B - 1);
+            const int64_t row = ref_row(first, i, N);
+            float *dst = ring + (size_t)ri * kRefSlotF;
+            for (int q = lw; q < kRefChunks; q += 3)
                 __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void *)(wr + (int64_t)sg * kRefStage + 4 * (lane & 31)),
+                    (const __attribute__((address_space(1))) void *)(dd.X +
+                                                                     ref_xoff<TILED>(row, sg * kRefChunks + q, D)),
+                    (__attribute__((address_space(3))) void *)(dst + q * 256), 16, 0, 0);
+            if (lw == 1)  // the stage's weights (lanes 16..63 again into the rest of the 1 KiB area)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(wr + (int64_t)sg * kRefStage + 4 * (lane & 15)),
                     (__attribute__((address_space(3))) void *)(dst + kRefUnit * kRefStage), 16, 0, 0);
             return u;
         };
-        // issue stages [0, LA) first; then per stage g: issue g + LA, wait
-        // for g, publish it
+        // issue stages [0, 6) first; then per stage g: wait for g (the five
+        // later stages still in flight), publish it, issue g + 6 (whose ring
+        // slot frees when the compute is past g - 1: by then it is usually
+        // adding g)
         int ka = 0, sa = 0, ria = 0;  // the next stage to issue
         auto issue_next = [&](int g) {
             const uint32_t u = issue(ka, sa, ria, g);
@@ -2919,43 +3108,38 @@ __device__ __forceinline__ void ref_margin_half(const DevDense &dd, int64_t firs
             if (++ria == kRefRing) ria = 0;
             return u;
         };
-        for (int g = 0; g < LA; ++g) issue_next(g);
+        for (int g = 0; g < kRefLA; ++g) issue_next(g);
         uint32_t *mine = ctl + kCtlL0 + lw;
+        DLR_TACC_DECL(t_issue);
+        DLR_TACC_DECL(t_land);
         for (int g = 0, k = 0, sg = 0;; ++g) {
-            ctl_wait_ge(ctl + kCtlIds, (uint32_t)k + 1);
-            const uint32_t u = ctl_read(s_unit + (k & 3));
-            if (u == kRefNone) break;
-            issue_next(g + LA);
-            if (LA == 6) {  // stage g landed (the LA later stages still in flight)
-                if (npieces == 6)
-                    asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
-                else
-                    asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
-            } else {
-                if (npieces == 6)
-                    asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-                else
-                    asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+            if (sg == 0) {  // a new unit: stop at the end of the sequence
+                ctl_wait_ge(ctl + kCtlIds, (uint32_t)k + 1);
+                if (ctl_read(s_unit + (k & 3)) == kRefNone) break;
             }
-            if (lane == 0) ctl_write(mine, (uint32_t)g + 1);
+            DLR_TACC_BEGIN();
+            if (npieces == 6)
+                asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(25)" ::: "memory");
+            DLR_TACC_LAP(t_land);
+            if (lane == 0) ctl_post(mine, (uint32_t)g + 1);
+            issue_next(g + kRefLA);
+            DLR_TACC_LAP(t_issue);
             if (++sg == spu) {
                 sg = 0;
                 ++k;
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives its wave
+        DLR_STAMP64MV(56 + 2 * lw, lane == 0 && lw < 2, t_issue);
+        DLR_STAMP64MV(57 + 2 * lw, lane == 0 && lw < 2, t_land);
         return;
     }
     // compute wave (wave 7: its SIMD's other wave is the chain half's
-    // mostly idle wave 3, not the column chain): lane i < 32 runs row i's
-    // chain; the weights come with the stage (w is read-only until the chain
+    // mostly idle wave 3, not the column chain): lane i runs row i's chain;
+    // the weights come with the stage (w is read-only until the chain
     // epilogue, after every margin)
-    const uint32_t xr = (uint32_t)(lane & 7);
-    uint32_t abase[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        abase[k] = lds_addr(ring) + (uint32_t)((lane & 31) >> 3) * 1024 + xr * 128 +
-                   (((uint32_t)k ^ (DLR_REF_SWZ ? xr : 0u)) << 4);
     const __amdgpu_buffer_rsrc_t rres = __builtin_amdgcn_make_buffer_rsrc(resid, 0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc(sy.limit, 0, 0x7FFFFFFF, 0x00020000);
     // claims: unit ids in row order; after the first failed claim none more
@@ -2986,14 +3170,18 @@ __device__ __forceinline__ void ref_margin_half(const DevDense &dd, int64_t firs
         ctl_write(ctl + kCtlIds, 2u);
     }
     DLR_STAMP64M(1, lane == 0);
+    DLR_TACC_DECL(t_wait);
+    DLR_TACC_DECL(t_comp);
     float z = 0.0f, y = 0.0f;
     int64_t urow = -1;  // batch row of this lane in the current unit (-1: none)
     uint32_t pend = 0;  // lane 0: the raw claim issued at the start of the unit
     bool have_pend = false;
+    uint32_t lk = 0;  // stages all three loaders are known to have landed
+    uint32_t u = kRefNone;
     for (int g = 0, k = 0, sg = 0, ri = 0;; ++g) {
-        const uint32_t u = ctl_read(s_unit + (k & 3));
-        if (u == kRefNone) break;
         if (sg == 0) {
+            u = ctl_read(s_unit + (k & 3));
+            if (u == kRefNone) break;
             // the margins' limit: start unit u only once the chains are
             // within `lead` slots of it (every unit this half still holds is
             // later: nothing a chain waits for is held here)
@@ -3004,61 +3192,35 @@ __device__ __forceinline__ void ref_margin_half(const DevDense &dd, int64_t firs
                     __builtin_amdgcn_s_sleep(16);
                 }
             DLR_STAMP64M(22 + k, lane == 0 && k < 20);
-            urow = lane < kRefUnit && (int64_t)u * kRefUnit + lane < B ? (int64_t)u * kRefUnit + lane : -1;
+            urow = (int64_t)u * kRefUnit + lane < B ? (int64_t)u * kRefUnit + lane : -1;
             if (urow >= 0) y = dd.label[ref_row(first, urow, N)];
             z = 0.0f;
             have_pend = lane == 0 && claiming;
             if (have_pend) pend = claim_issue();  // the unit after the next one
         }
         // stage g landed: every loader's pieces of it
-        ctl_wait_ge(ctl + kCtlL0, (uint32_t)g + 1);
-        ctl_wait_ge(ctl + kCtlL1, (uint32_t)g + 1);
-        ctl_wait_ge(ctl + kCtlL2, (uint32_t)g + 1);
-        if (!(DLR_ABL & 64) && lane < kRefUnit) {
-            // row chain over the stage's 128 columns in order: 4 groups of 8
-            // reads (piece p, half h -> columns 8p + 4h .. + 3), the next
-            // group in flight while this one is added
-            uint32_t a[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) a[k] = abase[k] + (uint32_t)ri * (kRefSlotF * 4);
+        DLR_TACC_BEGIN();
+        if ((int32_t)(lk - ((uint32_t)g + 1)) < 0) lk = ctl_poll_min<3>(ctl + kCtlL0, (uint32_t)g + 1);
+        DLR_TACC_LAP(t_wait);
+        if (!(DLR_ABL & 64)) {
+            // the stage's 64 columns in order, 4 sets of 16: set S's adds
+            // interleaved with set S + 1's products (ref_set), set S + 2's
+            // reads in flight
             const uint32_t wa = lds_addr(ring) + (uint32_t)ri * (kRefSlotF * 4);
-            v4f xa[4], xb[4], wa4[4], wb4[4];
-            auto grp = [&](const v4f(&x)[4], const v4f(&wq)[4]) {
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    z = z + wq[m].x * x[m].x;
-                    z = z + wq[m].y * x[m].y;
-                    z = z + wq[m].z * x[m].z;
-                    z = z + wq[m].w * x[m].w;
-                }
-            };
-            // the stage's 128 columns in order: 8 sets of 16, the next set in
-            // flight while one is added
-            ref_rd8<0, 0>(xa, wa4, a, wa);
-            ref_rd8<0, 1>(xb, wb4, a, wa);
-            DLR_REF_WAIT(8, xa, wa4);
-            grp(xa, wa4);
-            ref_rd8<1, 0>(xa, wa4, a, wa);
-            DLR_REF_WAIT(8, xb, wb4);
-            grp(xb, wb4);
-            ref_rd8<1, 1>(xb, wb4, a, wa);
-            DLR_REF_WAIT(8, xa, wa4);
-            grp(xa, wa4);
-            ref_rd8<2, 0>(xa, wa4, a, wa);
-            DLR_REF_WAIT(8, xb, wb4);
-            grp(xb, wb4);
-            ref_rd8<2, 1>(xb, wb4, a, wa);
-            DLR_REF_WAIT(8, xa, wa4);
-            grp(xa, wa4);
-            ref_rd8<3, 0>(xa, wa4, a, wa);
-            DLR_REF_WAIT(8, xb, wb4);
-            grp(xb, wb4);
-            ref_rd8<3, 1>(xb, wb4, a, wa);
-            DLR_REF_WAIT(8, xa, wa4);
-            grp(xa, wa4);
-            DLR_REF_WAIT(0, xb, wb4);
-            grp(xb, wb4);
+            const uint32_t a = wa + 16 * lane;
+            v4f xd[3][4], wd[3][4];
+            float pp[2][16];
+            ref_rd8<0>(xd[0], wd[0], a, wa);
+            ref_rd8<1>(xd[1], wd[1], a, wa);
+            DLR_REF_WAIT(8, xd[0], wd[0]);
+            ref_products(pp[0], xd[0], wd[0]);
+            ref_rd8<2>(xd[2], wd[2], a, wa);
+            ref_set<0>(z, xd, wd, pp, a, wa);
+            ref_set<1>(z, xd, wd, pp, a, wa);
+            ref_set<2>(z, xd, wd, pp, a, wa);
+            ref_set<3>(z, xd, wd, pp, a, wa);
         }
+        DLR_TACC_LAP(t_comp);
         if (sg == spu - 1) {
             if (urow >= 0) {
                 const float r = sigmoid_ref(z) - y;
@@ -3076,19 +3238,21 @@ __device__ __forceinline__ void ref_margin_half(const DevDense &dd, int64_t firs
             DLR_STAMP64M(2 + k, lane == 0 && k < 20);
             DLR_STAMP64MV(42 + k, lane == 0 && k < 20, (unsigned long long)u);
         }
-        if (lane == 0) ctl_write(ctl + kCtlComp, (uint32_t)g + 1);  // ring slot ri free
+        if (lane == 0) ctl_post(ctl + kCtlComp, (uint32_t)g + 1);  // ring slot ri free
         if (++sg == spu) {
             sg = 0;
             ++k;
         }
         if (++ri == kRefRing) ri = 0;
     }
+    DLR_STAMP64MV(60, lane == 0, t_wait);
+    DLR_STAMP64MV(61, lane == 0, t_comp);
     DLR_STAMP64M(63, lane == 0);
 }
 
 // grid: max(D / 16, margin halves) workgroups; workgroup b runs the chain
 // half of stripe b (b < D / 16) and a margin half (b < sy.mgrid)
-template <bool FUSED, int LA>
+template <bool FUSED, bool TILED>
 __global__ __launch_bounds__(kRefThreads) void k_dense_ref(DevDense dd, int64_t first, int64_t B,
                                                            const float *__restrict__ wr, float *w,
                                                            float *__restrict__ gout, float *resid, DevRefSync sy,
@@ -3102,9 +3266,29 @@ __global__ __launch_bounds__(kRefThreads) void k_dense_ref(DevDense dd, int64_t 
     __syncthreads();  // the only workgroup barrier: the halves go their own ways
     if (wv < 4) {
         if (!(DLR_ABL & 32) && (int)blockIdx.x < (int)(dd.D / kRefCols))
-            ref_chain_half<FUSED>(dd, first, B, w, gout, resid, sy, Bf, Bd, lr, C, rsm, wv, lane);
+            ref_chain_half<FUSED, TILED>(dd, first, B, w, gout, resid, sy, Bf, Bd, lr, C, rsm, wv, lane);
     } else if ((int)blockIdx.x < sy.mgrid) {
-        ref_margin_half<LA>(dd, first, B, wr, resid, sy, rsm, wv - 4, lane);
+        ref_margin_half<TILED>(dd, first, B, wr, resid, sy, rsm, wv - 4, lane);
+    }
+}
+
+// The tiled image of a row-major N x D shard (dense_ref_tiled): workgroup
+// (S, R0) writes tile S of the 64-row blocks R0, R0 + gridDim.y, ...; thread
+// t its chunks t + 256 m, in image order (rows past N: zeros).  No divisions
+// (test_abi's FMA census).
+__global__ __launch_bounds__(256) void k_dense_tile(const float *__restrict__ src, float *__restrict__ dst, int64_t N,
+                                                    int64_t D, int64_t nR) {
+    const int64_t nS = D / kRefStage, S = blockIdx.x;
+    for (int64_t R = blockIdx.y; R < nR; R += gridDim.y) {
+        float *tile = dst + (R * nS + S) * (kRefUnit * kRefStage);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int q = (int)threadIdx.x + 256 * m, i = q & 63, k = q >> 6;
+            const int64_t row = R * kRefUnit + i;
+            v4f v = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (row < N) v = *reinterpret_cast<const v4f *>(src + row * D + (S * kRefChunks + k) * 4);
+            *reinterpret_cast<v4f *>(tile + 4 * q) = v;
+        }
     }
 }
 #undef DLR_REF_WAIT
@@ -3696,19 +3880,28 @@ hipError_t launch_dense_ref(const DevDense &dd, int64_t first, int64_t B, float 
     const unsigned grid = (unsigned)std::max<int64_t>(dd.D / kRefCols, sy.mgrid);
     const float Bf = (float)B;
     const double Bd = (double)B;
-#define DLR_REF(F, L)                                                                                              \
-    hipLaunchKernelGGL((k_dense_ref<F, L>), dim3(grid), dim3(kRefThreads), kRefLds, s, dd, first, B, w, w, gout, resid, \
+#define DLR_REF(F, T)                                                                                              \
+    hipLaunchKernelGGL((k_dense_ref<F, T>), dim3(grid), dim3(kRefThreads), kRefLds, s, dd, first, B, w, w, gout, resid, \
                        sy, Bf, Bd, lr, C)
-    const bool la6 = dd.D / kRefStage >= 7;
-    if (fused && la6)
-        DLR_REF(true, 6);
+    if (fused && dd.tiled)
+        DLR_REF(true, true);
     else if (fused)
-        DLR_REF(true, 3);
-    else if (la6)
-        DLR_REF(false, 6);
+        DLR_REF(true, false);
+    else if (dd.tiled)
+        DLR_REF(false, true);
     else
-        DLR_REF(false, 3);
+        DLR_REF(false, false);
 #undef DLR_REF
+    return hipGetLastError();
+}
+
+int64_t dense_ref_tiled_floats(int64_t N, int64_t D) { return (N + kRefUnit - 1) / kRefUnit * kRefUnit * D; }
+
+hipError_t launch_dense_tile(const float *src, float *dst, int64_t N, int64_t D, hipStream_t s) {
+    if (D % kRefStage != 0 || N <= 0) return hipErrorInvalidValue;
+    const int64_t nR = (N + kRefUnit - 1) / kRefUnit;
+    hipLaunchKernelGGL(k_dense_tile, dim3((unsigned)(D / kRefStage), (unsigned)std::min<int64_t>(nR, 4096)), dim3(256), 0,
+                       s, src, dst, N, D, nR);
     return hipGetLastError();
 }
 

@@ -5,9 +5,16 @@ build of the library (make -C dist-lr_amd stamps) through DLR_LIB.
 Development tool, never part of the product.
 
 Chain halves (row b of the buffer): 0 start, 2 + t/16 the end of slot t's
-chain (t = 0, 16, ...), 50 end.  Margin halves (row 256 + b): 1 first claims
+chain (t = 0, 16, ...), 50 end; totals (us): 52 / 53 the chain wave waiting
+for the helpers / adding, 54 / 55 / 56 helper 1 waiting for residuals / for
+the chain / transforming and issuing loads, 57 / 58 wave 3 waiting for the
+margins / for the helpers; 60-63 s_memtime / s_memrealtime at the chain's
+start and end (the shader clock under load).  Margin halves (row 256 + b): 1 first claims
 done, 2 + k the publish time of its k-th unit, 22 + k its start (after the
-limit), 42 + k its id (k < 20), 63 end.
+limit), 42 + k its id (k < 20), 63 end; totals over the launch (us): 60 the
+compute wave waiting for stages, 61 adding; loaders 0 / 1: 56 / 58 issuing
+(including the waits for ring slots and unit ids), 57 / 59 waiting for
+their DMA to land.
 
   python tools/c4_stamps.py [--rows N] [--steps K] [--reps R]
 """
@@ -56,7 +63,7 @@ def main():
     f.argtypes, f.restype = [C.c_void_p], C.c_int
     D, B = a.features, a.batch
     S = D // 16
-    M = min(256, (B + 31) // 32)
+    M = min(256, (B + 63) // 64)
     G = 512  # chain workgroups write rows [0, S), margin workgroups rows [256, 256 + M)
     buf = torch.zeros(G * 64, dtype=torch.int64, device="cuda")
     assert f(buf.data_ptr()) == 0
@@ -85,6 +92,16 @@ def main():
         for t in range(0, nslot + 1, 32):
             print(f"chain slot {t:4d}  ", pct(us(ch[:, 2 + t // 16])))
         print("chain end        ", pct(us(ch[:, 50])))
+        ctick = lambda c: pct(ch[:, c] * 0.01)  # noqa: E731
+        print("chain: waiting for helpers ", ctick(52))
+        print("chain: adding              ", ctick(53))
+        print("helper 1: waiting residuals", ctick(54))
+        print("helper 1: waiting the chain", ctick(55))
+        print("helper 1: transform + loads", ctick(56))
+        print("wave 3: waiting margins    ", ctick(57))
+        print("wave 3: waiting helpers    ", ctick(58))
+        ghz = (ch[:, 62] - ch[:, 60]) / np.maximum(1.0, (ch[:, 63] - ch[:, 61])) * 0.1
+        print("shader clock over the chain (GHz)", pct(ghz))
         print("margin claims    ", pct(us(mg[:, 1])))
         ids = []
         for kk in range(20):
@@ -96,11 +113,18 @@ def main():
             print(f"              busy ", pct(pu - st_))
             ids += list(zip(mg[m, 42 + kk], pu))
         print("margin end       ", pct(us(mg[:, 63])))
+        tick = lambda c: pct(mg[:, c] * 0.01)  # noqa: E731
+        print("compute: waiting for stages", tick(60))
+        print("compute: adding            ", tick(61))
+        print("loader 0: issuing          ", tick(56))
+        print("loader 0: waiting to land  ", tick(57))
+        print("loader 1: issuing          ", tick(58))
+        print("loader 1: waiting to land  ", tick(59))
         ids.sort()
         if ids:
             u = np.array([x for x, _ in ids])
             t = np.array([y for _, y in ids])
-            slots = u // 8
+            slots = u // 4
             print("slot publish time (last unit of slot):")
             for s_ in range(0, nslot, 32):
                 m = slots == s_
