@@ -130,7 +130,8 @@ def test_dense_c4_shape_ranks(monkeypatch, W, order):
     # bitwise.  FAST (the fused blocked pass, opt-in): it does NOT meet the
     # north-star bar here -- the test pins that it stays
     # deterministic, reports how many weights leave 1e-5*|b| + 1e-7, and
-    # bounds the drift at 1e-3 relative so a regression is still caught.
+    # bounds the drift at 1e-3 relative (1e-5 absolute) so a regression is
+    # still caught.
     D, B, rows, lr = 4096, 65536, 150_000, 0.2
     o = dlr.ORDER_REFERENCE if order == "reference" else dlr.ORDER_FAST
     if order == "fast":
@@ -157,6 +158,9 @@ def test_dense_c4_shape_ranks(monkeypatch, W, order):
     assert np.array_equal(got.w.view(np.uint32), again.w.view(np.uint32)), "FAST is not deterministic"
     a, b = got.w.astype(np.float64), orc.w.astype(np.float64)
     rel = np.abs(a - b) / np.maximum(np.abs(b), 1e-30)
-    print(f"\nFAST fused dense, W = {W}, lr {lr}: max rel {rel[np.abs(b) >= 1e-2].max():.3g}, "
+    print(f"\nFAST fused dense, W = {W}, lr {lr}: max rel {rel[np.abs(b) >= 1e-2].max():.3g} (|b| >= 1e-2), "
+          f"max abs {np.abs(a - b).max():.3g}, "
           f"outside 1e-5*|b| + 1e-7: {int((np.abs(a - b) > 1e-5 * np.abs(b) + 1e-7).sum())} of {D}")
-    assert np.all(np.abs(a - b) <= 1e-3 * np.abs(b) + 1e-7)
+    # the drift bound (not the north-star bar): 1e-3 relative, 1e-5 absolute
+    # for the small weights
+    assert np.all(np.abs(a - b) <= 1e-3 * np.abs(b) + 1e-5)
