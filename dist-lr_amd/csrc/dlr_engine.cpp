@@ -180,14 +180,16 @@ struct TrainShard {
     // cptr/crow/cval/wsched; band k of batch b is bands[bfirst[b] + k]
     struct Band {
         int64_t pair, ptr, ent, ws, nwaves;  // offsets into bcols, bptr, brow/bval, bws
+        int64_t hw = 0, nhot = 0;            // the band's hot waves (k_band_hot): bhw[hw .. hw + nhot)
     };
+    int64_t max_hot = 0;  // the most hot waves of a band (CUs the pipelined margin leaves them)
     int band_shift = 0;
     bool band_longrun = false;  // band mode without the long-column split: runs of 10^5 entries in a band
     // margin with the hot (lowest, frequency-ordered) weights in LDS
     bool margin_hot = false;
     std::vector<Band> bands;
     std::vector<int64_t> bfirst;
-    uint32_t *bcols = nullptr, *bptr = nullptr, *bws = nullptr;
+    uint32_t *bcols = nullptr, *bptr = nullptr, *bws = nullptr, *bhw = nullptr;
     void *brow = nullptr;
     float *bval = nullptr;
     float *gacc = nullptr;  // D running column sums
@@ -288,6 +290,9 @@ struct dlr_ctx {
     hipStream_t gstream = nullptr;
     std::vector<hipEvent_t> ev_band;
     hipEvent_t ev_bstart = nullptr, ev_bdone = nullptr;
+    // ... and the hot pairs' stream (k_band_hot, band after band)
+    hipStream_t hstream = nullptr;
+    hipEvent_t ev_hdone = nullptr;
     hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
     std::vector<void *> allocs;
     // timing
@@ -380,7 +385,7 @@ void free_train(dlr_ctx *c) {
     TrainShard &t = c->train;
     // a reload frees what the last steps' kernels and copies may still read
     // (hipFree alone is not relied on to order them)
-    for (hipStream_t s : {c->stream, c->cstream, c->gstream, c->xstream})
+    for (hipStream_t s : {c->stream, c->cstream, c->gstream, c->hstream, c->xstream})
         if (s) (void)hipStreamSynchronize(s);
     if (t.sparse_stream) {
         if (c->cstream) (void)hipStreamSynchronize(c->cstream);
@@ -405,7 +410,7 @@ void free_train(dlr_ctx *c) {
                     (void *)t.gval, (void *)t.gscratch, (void *)t.tcols,
                     (void *)t.lcols, (void *)t.lcseg, (void *)t.lsptr, t.lrow, (void *)t.lval, (void *)t.lpart, (void *)t.lsched,
                     (void *)t.dX, (void *)t.dpart, (void *)t.wsched, (void *)t.bcols, (void *)t.bptr,
-                    (void *)t.bws, t.brow, (void *)t.bval, (void *)t.gacc, (void *)t.lpdesc, (void *)t.lpptr,
+                    (void *)t.bws, (void *)t.bhw, t.brow, (void *)t.bval, (void *)t.gacc, (void *)t.lpdesc, (void *)t.lpptr,
                     (void *)t.lpslot, (void *)t.lpws, (void *)t.lprow, (void *)t.lpval, (void *)t.pm_lbeg,
                     (void *)t.pm_list, (void *)t.pm_pofs, (void *)t.pm_rg, (void *)t.pm_qoff, (void *)t.pm_val,
                     (void *)t.pm_p, (void *)t.pm_qs, (void *)t.xslices, (void *)t.rt_gq, (void *)t.rt_val,
@@ -825,7 +830,7 @@ void build_csc(const CsrView &ds, const std::vector<dlr::BatchSpan> &plan, int64
 // schedule (as the classic one: <= 64 pairs, ~kWin entries per wave).
 template <typename RowT>
 struct BandBuild {
-    std::vector<uint32_t> cols, ptr, ws;
+    std::vector<uint32_t> cols, ptr, ws, hw;
     std::vector<RowT> row;
     std::vector<float> val;
     std::vector<TrainShard::Band> bands;
@@ -835,7 +840,7 @@ struct BandBuild {
 template <typename RowT>
 void build_bands(const std::vector<uint32_t> &cptr, const std::vector<RowT> &crow, const std::vector<float> &cval,
                  const std::vector<int64_t> &coff, int64_t nb, int64_t D, int64_t B, int shift, bool unit,
-                 int nthreads, BandBuild<RowT> &out) {
+                 int nthreads, int64_t hot_min, BandBuild<RowT> &out) {
     const int64_t nbands = (B + ((int64_t)1 << shift) - 1) >> shift;
     const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, D / 4096 + 1));
     out.bfirst.assign((size_t)nb + 1, 0);
@@ -927,21 +932,38 @@ void build_bands(const std::vector<uint32_t> &cptr, const std::vector<RowT> &cro
             out.ptr[(size_t)(bd.ptr + p)] = (uint32_t)e;
             bd.ws = ws_at;
             const uint32_t *pp = out.ptr.data() + bd.ptr;
+            // a HOT column's pair (hot_min > 0: >= hot_min entries in the
+            // batch) gets a wave of its own, marked in bit 31 of its start
+            // (k_band_hot's; k_grad_band skips it when launched beside it)
+            auto hot = [&](int64_t q) {
+                if (hot_min <= 0) return false;
+                const uint32_t j = out.cols[(size_t)(bd.pair + q)];
+                return (int64_t)(cp[j + 1] & 0x7FFFFFFFu) - (int64_t)(cp[j] & 0x7FFFFFFFu) >= hot_min;
+            };
+            bd.hw = (int64_t)out.hw.size();
             out.ws.push_back(0);
             int64_t acc = 0;
             int cols = 0;
+            bool prev_hot = false;
             for (int64_t q = 0; q < p; ++q) {
                 const int64_t cq = (int64_t)pp[q + 1] - (int64_t)pp[q];
-                if (cols == 64 * dlr::kBandPairsPerLane || (cols > 0 && acc + cq > 1024)) {
+                const bool hq = hot(q);
+                if (cols > 0 && (hq || prev_hot || cols == 64 * dlr::kBandPairsPerLane || acc + cq > 1024)) {
                     out.ws.push_back((uint32_t)q);
                     acc = 0;
                     cols = 0;
                 }
+                if (hq) {
+                    out.ws.back() |= 0x80000000u;
+                    out.hw.push_back((uint32_t)((int64_t)out.ws.size() - 1 - ws_at));
+                }
+                prev_hot = hq;
                 acc += cq;
                 ++cols;
             }
             out.ws.push_back((uint32_t)p);
             bd.nwaves = p > 0 ? (int64_t)out.ws.size() - ws_at - 1 : 0;
+            bd.nhot = (int64_t)out.hw.size() - bd.hw;
             ws_at = (int64_t)out.ws.size();
         }
         out.bfirst[(size_t)b + 1] = (int64_t)out.bands.size();
@@ -1799,6 +1821,21 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_bdone, hipEventDisableTiming);
         if (e != hipSuccess) return e;
     }
+    const bool hot = t.bhw != nullptr;
+    // with hot chains beside it, the persistent margin leaves their CUs (and
+    // DLR_BAND_CUS more to the other columns' band kernel, whose workgroups
+    // cannot share a CU with the margin's: A/B, measured no better at 32,
+    // 64, 96)
+    static const int band_cus = [] {
+        const char *e = getenv("DLR_BAND_CUS");
+        return e ? atoi(e) : 0;
+    }();
+    const int margin_reserve = hot ? (int)t.max_hot + band_cus : 0;
+    if (hot && !c->hstream) {
+        e = hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_hdone, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
     while ((int64_t)c->ev_band.size() < nbands) {
         hipEvent_t ev;
         if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
@@ -1813,6 +1850,7 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
     e = hipMemsetAsync(t.gacc, 0, (size_t)c->D * 4, c->stream);
     if (e == hipSuccess) e = hipEventRecord(c->ev_bstart, c->stream);
     if (e == hipSuccess) e = hipStreamWaitEvent(c->gstream, c->ev_bstart, 0);
+    if (e == hipSuccess && hot) e = hipStreamWaitEvent(c->hstream, c->ev_bstart, 0);
     for (int64_t k = 0; e == hipSuccess && k < nbands; ++k) {
         const int64_t r0 = k * BR, r1 = std::min(all.rows, r0 + BR);
         dlr::DevBatch sub = all;
@@ -1820,22 +1858,26 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
         sub.label = all.label + r0;
         sub.rows = r1 - r0;
         sub.nnz = all.rows > 0 ? all.nnz * sub.rows / all.rows : 0;  // the margin's rows-per-wave heuristic
-        e = t.margin_hot ? dlr::launch_margin_hot(sub, c->w, c->D, c->resid + r0, c->stream)
+        e = t.margin_hot ? dlr::launch_margin_hot(sub, c->w, c->D, c->resid + r0, c->stream, margin_reserve)
                          : dlr::launch_margin_residual(sub, c->w, c->resid + r0, c->stream);
         if (e == hipSuccess) e = hipEventRecord(c->ev_band[(size_t)k], c->stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(c->gstream, c->ev_band[(size_t)k], 0);
-        if (e == hipSuccess) {
-            const TrainShard::Band &bd = t.bands[(size_t)(t.bfirst[bb] + k)];
-            dlr::DevBand dv{t.bcols + bd.pair, t.bptr + bd.ptr, t.bws + bd.ws, (const char *)t.brow + esz * (size_t)bd.ent,
-                            t.bval ? t.bval + bd.ent : nullptr, bd.nwaves, t.row16};
-            e = dlr::launch_grad_band(dv, c->resid, t.gacc, c->gstream, t.band_longrun);
-        }
+        const TrainShard::Band &bd = t.bands[(size_t)(t.bfirst[bb] + k)];
+        const dlr::DevBand dv{t.bcols + bd.pair, t.bptr + bd.ptr, t.bws + bd.ws, (const char *)t.brow + esz * (size_t)bd.ent,
+                              t.bval ? t.bval + bd.ent : nullptr, bd.nwaves, t.row16};
+        if (e == hipSuccess) e = dlr::launch_grad_band(dv, c->resid, t.gacc, c->gstream, t.band_longrun, hot);
+        // the hot pairs: their chains continue band after band on their own
+        // stream, beside the next band's margin and the other columns
+        if (e == hipSuccess && hot) e = hipStreamWaitEvent(c->hstream, c->ev_band[(size_t)k], 0);
+        if (e == hipSuccess && hot) e = dlr::launch_band_hot(dv, t.bhw + bd.hw, bd.nhot, c->resid, t.gacc, c->hstream);
     }
     if (e == hipSuccess) e = hipEventRecord(c->ev_bdone, c->gstream);
+    if (e == hipSuccess && hot) e = hipEventRecord(c->ev_hdone, c->hstream);
     // the long columns' raw sums go to their own gacc entries (disjoint from
     // the short columns' the bands write)
     if (e == hipSuccess) e = launch_long_columns(c, b, B, gout, lr, C, fused);
     if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_bdone, 0);
+    if (e == hipSuccess && hot) e = hipStreamWaitEvent(c->stream, c->ev_hdone, 0);
     if (e == hipSuccess) e = dlr::launch_band_finalize(t.gacc, c->w, gout, c->D, B, lr, C, fused, c->stream);
     return e;
 }
@@ -1953,6 +1995,7 @@ void dlr_destroy(dlr_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->cstream) (void)hipStreamSynchronize(ctx->cstream);
     if (ctx->gstream) (void)hipStreamSynchronize(ctx->gstream);
+    if (ctx->hstream) (void)hipStreamSynchronize(ctx->hstream);
     if (ctx->xstream) (void)hipStreamSynchronize(ctx->xstream);
     free_train(ctx);  // unregisters a streamed shard's host rows
     delete ctx->comm;  // RCCL: ncclCommDestroy; loopback: drops the group reference
@@ -1968,6 +2011,8 @@ void dlr_destroy(dlr_ctx *ctx) {
     if (ctx->ev_bstart) (void)hipEventDestroy(ctx->ev_bstart);
     if (ctx->ev_bdone) (void)hipEventDestroy(ctx->ev_bdone);
     if (ctx->gstream) (void)hipStreamDestroy(ctx->gstream);
+    if (ctx->ev_hdone) (void)hipEventDestroy(ctx->ev_hdone);
+    if (ctx->hstream) (void)hipStreamDestroy(ctx->hstream);
     if (ctx->ev_xmerged) (void)hipEventDestroy(ctx->ev_xmerged);
     for (hipEvent_t e : ctx->ev_xpiece)
         if (e) (void)hipEventDestroy(e);
@@ -2624,7 +2669,12 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 return DLR_OK;
             }
             BandBuild<RowT> bb;
-            build_bands(cptr, crow, cval, t.coff, nb, D, t.B, shift, t.unit, nthreads, bb);
+            // REFERENCE order: the hot columns' pairs run in k_band_hot
+            // (DLR_BAND_HOT: entries in the batch that make a column hot;
+            // 0 = none)
+            const char *bh = getenv("DLR_BAND_HOT");
+            const int64_t hot_min = long_min == 0 ? (bh ? atoll(bh) : (int64_t)1 << 17) : 0;
+            build_bands(cptr, crow, cval, t.coff, nb, D, t.B, shift, t.unit, nthreads, hot_min, bb);
             t.band_shift = shift;
             t.band_longrun = long_min == 0;
             t.bands = std::move(bb.bands);
@@ -2632,6 +2682,8 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             if ((r = upload(c, &t.bcols, bb.cols.data(), bb.cols.size(), 64))) return r;
             if ((r = upload(c, &t.bptr, bb.ptr.data(), bb.ptr.size()))) return r;
             if ((r = upload(c, &t.bws, bb.ws.data(), bb.ws.size()))) return r;
+            if (!bb.hw.empty() && (r = upload(c, &t.bhw, bb.hw.data(), bb.hw.size()))) return r;
+            for (const TrainShard::Band &x : t.bands) t.max_hot = std::max(t.max_hot, x.nhot);
             if ((r = upload(c, (RowT **)&t.brow, bb.row.data(), bb.row.size(), kPad))) return r;
             if (!t.unit && (r = upload(c, &t.bval, bb.val.data(), bb.val.size(), kPad))) return r;
             if ((r = dev_alloc(c, (void **)&t.gacc, (size_t)D * 4))) return r;

@@ -208,7 +208,8 @@ hipError_t launch_margin_residual(const DevBatch &bt, const float *w, float *res
 // shards; needs D >= kMarginHot).
 constexpr int kMarginHot = 8192;
 constexpr int kMarginHotWaves = 8;
-hipError_t launch_margin_hot(const DevBatch &bt, const float *w, int64_t D, float *resid, hipStream_t s);
+hipError_t launch_margin_hot(const DevBatch &bt, const float *w, int64_t D, float *resid, hipStream_t s,
+                             int reserve = 0);
 int predict_grid(int64_t rows);
 hipError_t launch_predict(const DevBatch &bt, const float *w, unsigned long long *correct, double *ll_part,
                           double *ll_out, hipStream_t s);
@@ -224,7 +225,13 @@ hipError_t launch_grad_long(const DevLong &lg, int64_t B, const float *resid, fl
 // before the first band); then the update of every column from gacc.
 // longrun: the band holds runs of >= 64 entries of one column (band mode
 // without the long-column split, DLR_LONG_COLUMN=0): 16-byte LDS reads.
-hipError_t launch_grad_band(const DevBand &bd, const float *resid, float *gacc, hipStream_t s, bool longrun = false);
+hipError_t launch_grad_band(const DevBand &bd, const float *resid, float *gacc, hipStream_t s, bool longrun = false,
+                            bool skip_hot = false);
+// The band's hot pairs (waves marked in bit 31 of wstart; hw: their nhot wave
+// ids): one workgroup each, beside launch_grad_band(..., skip_hot = true) of
+// the same band (dlr_kernels.hip k_band_hot; bitwise the same sums).
+hipError_t launch_band_hot(const DevBand &bd, const uint32_t *hw, int64_t nhot, const float *resid, float *gacc,
+                           hipStream_t s);
 // Long columns in row phases: piece partials part[slot], then the fixed
 // combine of each column's partials [cseg[l], cseg[l+1]) into graw[j].
 hipError_t launch_long_phase(const DevLPhase &lp, const uint32_t *cols, const uint32_t *cseg, int64_t ncols,

@@ -1582,7 +1582,7 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad_touched(DevCsc cs, const
 template <typename RowT, bool UNIT = false, bool LONGRUN = false>
 __global__ __launch_bounds__(kWaves *kWave) void k_grad_band(DevBand bd, const RowT *__restrict__ brow,
                                                              const float *__restrict__ resid,
-                                                             float *__restrict__ gacc) {
+                                                             float *__restrict__ gacc, bool skip_hot) {
     __shared__ float s_p[kWaves][kWin];
     constexpr int K = kBandPairsPerLane;
     const int lane = threadIdx.x & (kWave - 1);
@@ -1592,7 +1592,10 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad_band(DevBand bd, const R
     // every access but the residual gathers is non-temporal: the pairs'
     // columns and pointers (37 MB per band at C3) and the running sums (a
     // 64 MB array) must not evict the band's residual slice from L2
-    const int64_t s0 = __builtin_nontemporal_load(bd.wstart + wid), sl = __builtin_nontemporal_load(bd.wstart + wid + 1);
+    // (bit 31: a hot pair's own wave, k_band_hot's when skip_hot)
+    const uint32_t w0 = __builtin_nontemporal_load(bd.wstart + wid);
+    if (skip_hot && (w0 >> 31)) return;
+    const int64_t s0 = w0 & 0x7FFFFFFFu, sl = __builtin_nontemporal_load(bd.wstart + wid + 1) & 0x7FFFFFFFu;
     const int64_t e0 = __builtin_nontemporal_load(bd.ptr + s0), e1 = __builtin_nontemporal_load(bd.ptr + sl);
     // lane l owns pairs s0 + l + 64k
     int64_t a[K], b[K];
@@ -1615,6 +1618,201 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad_band(DevBand bd, const R
 #pragma unroll
     for (int k = 0; k < K; ++k)
         if (s0 + lane + (int64_t)k * kWave < sl) __builtin_nontemporal_store(acc[k], gacc + j[k]);
+}
+
+// Bounded polls: a hand-off whose producer never comes ends after kCtlSpin
+// polls (wrong sums instead of a hung GPU).
+constexpr int kCtlSpin = 1 << 22;
+// LDS hand-off words between the waves of one half (no s_barrier: the two
+// halves run at their own pace).  A producer's data writes (or, for LDS-DMA,
+// its covering vmcnt wait) complete before the word is written; a consumer
+// reads the data only after it has seen the word.
+__device__ __forceinline__ uint32_t ctl_read(const uint32_t *p) {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+    return v;
+}
+__device__ __forceinline__ void ctl_write(uint32_t *p, uint32_t v) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n ds_write_b32 %0, %1\n s_waitcnt lgkmcnt(0)" ::"v"(lds_addr(p)), "v"(v)
+                 : "memory");
+}
+__device__ __forceinline__ void ctl_wait_ge(const uint32_t *p, uint32_t v) {
+    for (int k = 0; k < kCtlSpin && (int32_t)(ctl_read(p) - v) < 0; ++k) __builtin_amdgcn_s_sleep(0);
+}
+// The per-stage / per-slot hand-offs: a plain ds_write (a wave's LDS
+// operations complete in order, so the data it stored before -- or the
+// LDS-DMA its vmcnt wait covered -- lands first), and polls that return the
+// value seen, so a consumer that is behind its producer (the usual case)
+// skips the next polls: one LDS round trip per hand-off instead of three.
+__device__ __forceinline__ void ctl_post(uint32_t *p, uint32_t v) {
+    asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ uint32_t ctl_poll(const uint32_t *p, uint32_t v) {
+    uint32_t x = ctl_read(p);
+    for (int k = 0; k < kCtlSpin && (int32_t)(x - v) < 0; ++k) {
+        __builtin_amdgcn_s_sleep(0);
+        x = ctl_read(p);
+    }
+    return x;
+}
+// min of the counters p[0], p[1] (N = 2) or p[0..2] (N = 3; p 16-byte aligned)
+template <int N>
+__device__ __forceinline__ uint32_t ctl_read_min(const uint32_t *p) {
+    if constexpr (N == 2) {
+        uint2 v;
+        asm volatile("ds_read_b64 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+        return min(v.x, v.y);
+    } else {
+        u32x4 v;
+        asm volatile("ds_read_b128 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+        return min(min(v.x, v.y), v.z);
+    }
+}
+template <int N>
+__device__ __forceinline__ uint32_t ctl_poll_min(const uint32_t *p, uint32_t v) {
+    uint32_t x = ctl_read_min<N>(p);
+    for (int k = 0; k < kCtlSpin && (int32_t)(x - v) < 0; ++k) {
+        __builtin_amdgcn_s_sleep(0);
+        x = ctl_read_min<N>(p);
+    }
+    return x;
+}
+
+// HOT columns of a band (REFERENCE order, band mode): a column whose chain
+// over a full-shard batch is ~10^6 adds (C3's Zipf heads: ~130,000 entries
+// per 2^20-row band) is the critical path of its band's launch -- one lane
+// of k_grad_band adds it while the launch's other work is long done.  The
+// layout builder gives each such (column, band) pair a wave of its own,
+// marked in bit 31 of its wstart entry; k_grad_band skips those waves
+// (skip_hot) and k_band_hot runs them beside it, one 256-thread workgroup
+// per hot pair holding a CU by itself (dynamic LDS: nothing else fits
+// beside it, the chain's SIMD is not shared):
+//   wave 0    the chain: gacc[j] + the pair's products in entry order, 256
+//             at a time from a 16-chunk LDS ring (16-byte broadcast reads,
+//             the next 32 in flight while 32 are added, across chunks);
+//   waves 1-2 the products: lane l of the 128 forms entries 256c + l and
+//             256c + 128 + l of chunk c -- the rows loaded 16 chunks ahead,
+//             the residual gathers (L2: the band's slice) eight ahead -- and
+//             stores fl32(r * x) into the ring.
+// The same products added in the same order from the same start: bitwise
+// k_grad_band's sum.  Hand-offs through LDS counters (as K6r's); waits
+// bounded.
+constexpr int kHotChunk = 256;
+constexpr int kHotRing = 16;
+constexpr size_t kHotLds = 150 * 1024;  // requested: the workgroup holds its CU alone
+template <typename RowT, bool UNIT>
+__global__ __launch_bounds__(256) void k_band_hot(DevBand bd, const uint32_t *__restrict__ hw,
+                                                  const RowT *__restrict__ brow, const float *__restrict__ resid,
+                                                  float *__restrict__ gacc) {
+    extern __shared__ __attribute__((aligned(16))) float hsm[];
+    float *ring = hsm;                                                    // [kHotRing][kHotChunk]
+    uint32_t *ctl = reinterpret_cast<uint32_t *>(hsm + kHotRing * kHotChunk);  // helper 1, helper 2, chain
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    if (threadIdx.x < 4) ctl[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t wid = hw[blockIdx.x];
+    const int64_t s0 = bd.wstart[wid] & 0x7FFFFFFFu;
+    const uint32_t j = bd.cols[s0];
+    const int64_t e0 = bd.ptr[s0], e1 = bd.ptr[s0 + 1];
+    const int64_t n = e1 - e0;
+    const int64_t nch = (n + kHotChunk - 1) / kHotChunk;
+    if (wv == 0) {
+        float acc = __builtin_nontemporal_load(gacc + j);
+        uint32_t pk = 0;  // chunks both helpers are known to have stored
+        auto rd = [&](v4f(&d)[8], const float *q) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) d[u] = *reinterpret_cast<const v4f *>(q + 4 * u);
+        };
+        auto add = [&](const v4f(&d)[8]) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                acc = acc + d[u].x;
+                acc = acc + d[u].y;
+                acc = acc + d[u].z;
+                acc = acc + d[u].w;
+            }
+        };
+        // full chunks: the next 32 products' reads in flight while 32 are
+        // added, across chunk boundaries once the helpers have stored the
+        // next chunk; the last (partial) chunk one by one
+        const int64_t nfull = n / kHotChunk;
+        v4f da[8], db[8];
+        if (nfull > 0) {
+            pk = ctl_poll_min<2>(ctl, 1u);
+            rd(da, ring);
+        }
+        for (int64_t c = 0; c < nfull; ++c) {
+            const float *q = ring + (c % kHotRing) * kHotChunk;
+#pragma unroll 1
+            for (int k = 0; k < kHotChunk - 64; k += 64) {
+                rd(db, q + k + 32);
+                add(da);
+                rd(da, q + k + 64);
+                add(db);
+            }
+            rd(db, q + kHotChunk - 32);
+            add(da);
+            const bool more = c + 1 < nfull;
+            if (more && (int32_t)(pk - ((uint32_t)c + 2)) < 0) pk = ctl_poll_min<2>(ctl, (uint32_t)c + 2);
+            rd(da, more ? ring + ((c + 1) % kHotRing) * kHotChunk : q);  // (after the last: a re-read, unused)
+            add(db);
+            if (lane == 0) ctl_post(ctl + 2, (uint32_t)c + 1);
+        }
+        if (nfull < nch) {
+            const int64_t c = nfull;
+            if ((int32_t)(pk - ((uint32_t)c + 1)) < 0) pk = ctl_poll_min<2>(ctl, (uint32_t)c + 1);
+            const float *q = ring + (c % kHotRing) * kHotChunk;
+            const int cnt = (int)(n - c * kHotChunk);
+            for (int k = 0; k < cnt; ++k) acc = acc + q[k];
+        }
+        if (lane == 0) __builtin_nontemporal_store(acc, gacc + j);
+        return;
+    }
+    if (wv > 2) return;
+    // helpers: chunk c's entries 256c + hl, 256c + 128 + hl (hl: 0..127)
+    const int hl = (wv - 1) * kWave + lane;
+    uint32_t *mine = ctl + (wv - 1);
+    uint32_t ck = 0;  // chunks the chain is known to have added
+    auto ent = [&](int64_t c, int h) { return min<int64_t>(e0 + c * kHotChunk + 128 * h + hl, e1 - 1); };
+    constexpr int RA = 16, GA = 8;  // rows RA chunks ahead, gathers GA (32 / 16 measured no better)
+    uint32_t rw[RA][2];
+    float vl[RA][2], g[GA][2];
+    auto load_rows = [&](int64_t c, int d) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t e = ent(c < nch ? c : 0, h);
+            rw[d][h] = (uint32_t)__builtin_nontemporal_load(brow + e);
+            vl[d][h] = UNIT ? 1.0f : __builtin_nontemporal_load(bd.val + e);
+        }
+    };
+#pragma unroll
+    for (int d = 0; d < RA; ++d) load_rows(d, d);
+#pragma unroll
+    for (int d = 0; d < GA; ++d) {
+        g[d][0] = resid[rw[d][0]];
+        g[d][1] = resid[rw[d][1]];
+    }
+    for (int64_t c0 = 0; c0 < nch; c0 += RA) {
+#pragma unroll
+        for (int d = 0; d < RA; ++d) {
+            const int64_t c = c0 + d;
+            if (c < nch) {
+                // chunk c's gathers landed GA chunks ago; issue chunk c + GA's
+                // (its rows landed RA - GA chunks ago), then chunk c + RA's rows
+                const float p0 = g[d % GA][0] * vl[d][0], p1 = g[d % GA][1] * vl[d][1];
+                g[d % GA][0] = resid[rw[(d + GA) % RA][0]];
+                g[d % GA][1] = resid[rw[(d + GA) % RA][1]];
+                load_rows(c + RA, d);
+                if (c >= kHotRing && (int32_t)(ck - (uint32_t)(c - kHotRing + 1)) < 0)
+                    ck = ctl_poll(ctl + 2, (uint32_t)(c - kHotRing + 1));
+                float *q = ring + (c % kHotRing) * kHotChunk;
+                q[hl] = p0;
+                q[128 + hl] = p1;
+                if (lane == 0) ctl_post(mine, (uint32_t)c + 1);
+            }
+        }
+    }
 }
 
 // Long columns in ROW PHASES (band mode).  The chunked long path gathers
@@ -2643,7 +2841,7 @@ constexpr int kRefPad = kRefSlot + 4;
 constexpr int kRefHD = 6;         // chain slots whose rows a helper has in flight
 constexpr int kRefThreads = 512;
 constexpr uint32_t kRefNone = 0xFFFFFFFFu;
-constexpr int kRefSpin = 1 << 22;
+constexpr int kRefSpin = kCtlSpin;
 // LDS (floats): chain products [2][16][kRefPad], residuals [2][256], the
 // margin ring [7][64 x 64 + 256 (the stage's 64 weights, in a 1 KiB area)],
 // then 16 words of hand-off counters / unit ids
@@ -2677,60 +2875,6 @@ __device__ __forceinline__ int64_t ref_xoff(int64_t row, int64_t k, int64_t D) {
         return row * D + 4 * k;
 }
 
-// LDS hand-off words between the waves of one half (no s_barrier: the two
-// halves run at their own pace).  A producer's data writes (or, for LDS-DMA,
-// its covering vmcnt wait) complete before the word is written; a consumer
-// reads the data only after it has seen the word.
-__device__ __forceinline__ uint32_t ctl_read(const uint32_t *p) {
-    uint32_t v;
-    asm volatile("ds_read_b32 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
-    return v;
-}
-__device__ __forceinline__ void ctl_write(uint32_t *p, uint32_t v) {
-    asm volatile("s_waitcnt lgkmcnt(0)\n ds_write_b32 %0, %1\n s_waitcnt lgkmcnt(0)" ::"v"(lds_addr(p)), "v"(v)
-                 : "memory");
-}
-__device__ __forceinline__ void ctl_wait_ge(const uint32_t *p, uint32_t v) {
-    for (int k = 0; k < kRefSpin && (int32_t)(ctl_read(p) - v) < 0; ++k) __builtin_amdgcn_s_sleep(0);
-}
-// The per-stage / per-slot hand-offs: a plain ds_write (a wave's LDS
-// operations complete in order, so the data it stored before -- or the
-// LDS-DMA its vmcnt wait covered -- lands first), and polls that return the
-// value seen, so a consumer that is behind its producer (the usual case)
-// skips the next polls: one LDS round trip per hand-off instead of three.
-__device__ __forceinline__ void ctl_post(uint32_t *p, uint32_t v) {
-    asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
-}
-__device__ __forceinline__ uint32_t ctl_poll(const uint32_t *p, uint32_t v) {
-    uint32_t x = ctl_read(p);
-    for (int k = 0; k < kRefSpin && (int32_t)(x - v) < 0; ++k) {
-        __builtin_amdgcn_s_sleep(0);
-        x = ctl_read(p);
-    }
-    return x;
-}
-// min of the counters p[0], p[1] (N = 2) or p[0..2] (N = 3; p 16-byte aligned)
-template <int N>
-__device__ __forceinline__ uint32_t ctl_read_min(const uint32_t *p) {
-    if constexpr (N == 2) {
-        uint2 v;
-        asm volatile("ds_read_b64 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
-        return min(v.x, v.y);
-    } else {
-        u32x4 v;
-        asm volatile("ds_read_b128 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
-        return min(min(v.x, v.y), v.z);
-    }
-}
-template <int N>
-__device__ __forceinline__ uint32_t ctl_poll_min(const uint32_t *p, uint32_t v) {
-    uint32_t x = ctl_read_min<N>(p);
-    for (int k = 0; k < kRefSpin && (int32_t)(x - v) < 0; ++k) {
-        __builtin_amdgcn_s_sleep(0);
-        x = ctl_read_min<N>(p);
-    }
-    return x;
-}
 
 // A margin stage in its ring slot: chunk k of rows 0..63 at k * 1 KiB + row *
 // 16 (the tile's own image), the stage's 64 weights at 16 KiB.  ref_rd8<S>:
@@ -3430,14 +3574,18 @@ hipError_t launch_mh(const DevBatch &bt, const float *w, float *resid, unsigned 
     return hipGetLastError();
 }
 
-hipError_t launch_margin_hot(const DevBatch &bt, const float *w, int64_t D, float *resid, hipStream_t s) {
+hipError_t launch_margin_hot(const DevBatch &bt, const float *w, int64_t D, float *resid, hipStream_t s,
+                             int reserve) {
     if (bt.rows <= 0) return hipSuccess;
-    static const int ncu = [] {
+    static const int ncu_all = [] {
         int dev = 0, n = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             n = 256;
         return n > 0 ? n : 256;
     }();
+    // reserve: CUs left to the band-hot chains running beside this launch
+    // (its persistent workgroups would otherwise take every CU's LDS)
+    const int ncu = std::max(ncu_all / 2, ncu_all - std::max(0, reserve));
     // 24,576 (below) or 16,384 hot weights x 16 waves, one workgroup per CU,
     // when D allows (C3 margin 1.749 ms with 16,384, round 2), else 8,192 x
     // 8, two per CU (1.779 ms).  Also
@@ -3762,13 +3910,14 @@ hipError_t launch_grad_long(const DevLong &lg, int64_t B, const float *resid, fl
     return hipGetLastError();
 }
 
-hipError_t launch_grad_band(const DevBand &bd, const float *resid, float *gacc, hipStream_t s, bool longrun) {
+hipError_t launch_grad_band(const DevBand &bd, const float *resid, float *gacc, hipStream_t s, bool longrun,
+                            bool skip_hot) {
     if (bd.nwaves <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((bd.nwaves + kWaves - 1) / kWaves);
     const dim3 blk(kWaves * kWave);
 #define DLR_GB(RT, U, L)                                                                                     \
     hipLaunchKernelGGL((k_grad_band<RT, U, L>), dim3(grid), blk, 0, s, bd, static_cast<const RT *>(bd.row), resid, \
-                       gacc)
+                       gacc, skip_hot)
 #define DLR_GBL(RT, U)      \
     if (longrun)            \
         DLR_GB(RT, U, true); \
@@ -3785,6 +3934,24 @@ hipError_t launch_grad_band(const DevBand &bd, const float *resid, float *gacc, 
     }
 #undef DLR_GBL
 #undef DLR_GB
+    return hipGetLastError();
+}
+
+hipError_t launch_band_hot(const DevBand &bd, const uint32_t *hw, int64_t nhot, const float *resid, float *gacc,
+                           hipStream_t s) {
+    if (nhot <= 0) return hipSuccess;
+#define DLR_BH(RT, U)                                                                                                \
+    hipLaunchKernelGGL((k_band_hot<RT, U>), dim3((unsigned)nhot), dim3(256), kHotLds, s, bd, hw,                       \
+                       static_cast<const RT *>(bd.row), resid, gacc)
+    if (bd.row16 && bd.val == nullptr)
+        DLR_BH(uint16_t, true);
+    else if (bd.row16)
+        DLR_BH(uint16_t, false);
+    else if (bd.val == nullptr)
+        DLR_BH(uint32_t, true);
+    else
+        DLR_BH(uint32_t, false);
+#undef DLR_BH
     return hipGetLastError();
 }
 

@@ -176,6 +176,39 @@ def test_band_pipeline_bitwise_vs_sequential(monkeypatch, W, order):
     assert_same_weights(got.w, ref.w)
 
 
+@pytest.mark.parametrize("hot", ["64", "2000", "0"])
+@pytest.mark.parametrize("W", [1, 2])
+def test_band_hot_pairs_bitwise(monkeypatch, W, hot):
+    # REFERENCE order, band mode, pipelined: the hot columns' pairs (>= hot
+    # entries in the batch; DLR_BAND_HOT, "0" = none) run in k_band_hot on
+    # a third stream, band after band, the other columns in k_grad_band
+    # beside them -- the same chains: bitwise the oracle (and the sequential
+    # DLR_BAND_PIPE=0 path, which keeps every pair in k_grad_band)
+    D = 1 << 24
+    shards = _c3_shards(W, rows=80_000)
+    monkeypatch.setenv("DLR_BAND_ROWS", "8192")
+    monkeypatch.setenv("DLR_BAND_HOT", hot)
+    got = run_engine(shards, D, 3, -1, 0.2)
+    orc = oracle.run_worker([_csr_shard(s) for s in shards], D, 3, -1, 0.2)
+    compare_runs(got, orc)
+    monkeypatch.setenv("DLR_BAND_PIPE", "0")
+    seq = run_engine(shards, D, 3, -1, 0.2)
+    assert_same_weights(got.w, seq.w)
+
+
+@pytest.mark.parametrize("value_mode", [1, 2])
+def test_band_hot_pairs_valued(classic, monkeypatch, value_mode):
+    # fp32 values (the hot kernel's products r * x, uint16 rows at this
+    # size): bitwise the oracle with every column of >= 32 entries hot
+    monkeypatch.setenv("DLR_BAND_ROWS", "16")
+    monkeypatch.setenv("DLR_BAND_HOT", "32")
+    D = 400
+    ds = dlr.Dataset.generate(700, D, 40, value_mode=value_mode, seed=37, stream=3)
+    eng = run_engine([ds], D, 2, -1, 0.3)
+    orc = oracle.run_worker([oracle_shard(ds, D)], D, 2, -1, 0.3)
+    compare_runs(eng, orc)
+
+
 def test_c3_banded_pushed_gradient(monkeypatch):
     # the N > 1 path's pushed gradient (non-fused finalize), FAST order:
     # short columns bitwise the unbanded classic kernel's, long columns
