@@ -426,6 +426,7 @@ def run_rank(args):
     band_rows = eng.train_band_rows() if args.kind != "dense" else 0
     # which summation order the numbers below are for: what
     # the loaded shard's kernels actually use (dlr_summation_order)
+    order_name = "reference" if eng.summation_order() == dlr.ORDER_REFERENCE else "fast"
     if eng.summation_order() == dlr.ORDER_REFERENCE:
         order = "reference: one chain per row (margin) and per column (gradient), lr.cc:35-40/108-112 -- bitwise"
     elif args.kind == "dense":
@@ -539,7 +540,8 @@ def run_rank(args):
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("workload_key") == f"D{D}_nnz{args.nnz}_B{B}" and tj.get("layout", layout) == layout:
+            if (tj.get("workload_key") == f"D{D}_nnz{args.nnz}_B{B}" and tj.get("layout", layout) == layout
+                    and tj.get("summation_order", order_name) == order_name):
                 traffic = tj.get("hbm_bytes_per_step")
         except Exception:
             traffic = None

@@ -89,9 +89,10 @@ def main() -> int:
     # Product margin (C2): pass 2 is the margin role, a separate pass 1
     # (k_pm_products) too; a fused pass 1 is inside k_grad_lds (grad role).
     roles = [("margin", ["k_margin", "k_pm_margin", "k_pm_products", "k_dense_fused", "k_dense_margin"]),
-             ("grad", ["k_grad", "k_long_", "k_band_finalize", "k_dense_grad", "k_dense_combine"]),
+             ("step", ["k_dense_ref<"]),  # K6r: margin + gradient + update in one launch
+             ("grad", ["k_grad", "k_long_", "k_band_finalize", "k_band_hot", "k_dense_grad", "k_dense_combine"]),
              ("update", ["k_dense_l2", "k_scatter", "k_merge_update", "k_sparse_merge"])]
-    steps = args.steps or len([x for k in ["k_margin", "k_pm_margin", "k_dense_fused", "k_dense_margin"]
+    steps = args.steps or len([x for k in ["k_margin", "k_pm_margin", "k_dense_fused", "k_dense_margin", "k_dense_ref<"]
                                for x in pick(bf, k)]) or 1
     total = 0.0
     for short, keys in roles:
