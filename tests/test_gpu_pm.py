@@ -226,6 +226,37 @@ def test_pm_overlap_through_rccl_one_rank(monkeypatch):
     compare_runs(eng, orc)
 
 
+def test_rccl_abort_from_another_thread(monkeypatch):
+    # dlr_comm_abort on an RCCL communicator from a thread that does not
+    # drive it (bin/distlr's in-process topology aborts every rank's
+    # communicator from the failing rank's thread): it only flags the
+    # communicator; the driving thread's next stream wait or collective
+    # aborts it (ncclCommAbort) and fails with the reason, and the context
+    # still closes
+    import threading
+
+    monkeypatch.setenv("DLR_FORCE_COLLECTIVES", "1")
+    monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
+    monkeypatch.setenv("DLR_PM", "1")
+    D = 300_000
+    ds = dlr.Dataset.generate(1500, D, 20, value_mode=1, seed=43, stream=1)
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(dlr.init_weight(D))
+        nb = eng.load_train(ds, 250)
+        eng.train_step(0, 0.2, 1.0)
+        eng.sync()
+        th = threading.Thread(target=eng.comm_abort, args=("rank 0 lost its shard",))
+        th.start()
+        th.join()
+        with pytest.raises(dlr.DLRError, match="lost its shard"):
+            for b in range(1, nb):
+                eng.train_step(b, 0.2, 1.0)
+            eng.sync()
+    finally:
+        eng.close()
+
+
 def test_pm_parameter_server_topology(pm_on):
     # W workers through dlr_worker_gradient / dlr_server_apply
     D = 200_000
