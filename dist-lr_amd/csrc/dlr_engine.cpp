@@ -2210,6 +2210,11 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
     while (band_rows > 0 && ((int64_t)2 << shift) <= band_rows) ++shift;
     const bool band = !t.touched && band_rows > 0 && shift > 0 &&
                       (brs ? t.B > ((int64_t)1 << shift) : t.B >= ((int64_t)2 << shift));
+    // REFERENCE order: half-size bands (2^19 rows) by default -- the hot
+    // columns' chains (k_band_hot) start after the first band's margin and
+    // sync at each band boundary (C3: 7.0-7.3 ms vs 7.2-7.5 with 2^20, 7.4
+    // with 2^18, 8.2 with 2^21; profiles/r04br*)
+    if (band && !brs && c->order == DLR_ORDER_REFERENCE) shift -= 1;
     // Residency (K1, data_iter.h:40-55's batches): resident in HBM, or --
     // DLR_RESIDENCY_STREAM, or AUTO when the shard would not leave 8 GiB of
     // HBM free -- kept in page-locked host memory and staged batch by batch
