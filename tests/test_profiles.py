@@ -19,7 +19,8 @@ CASES = [
     # equivalents (bench --steps 6 --warmup 2: 2 + 6 timed + 6 + 6 stage and
     # breakdown steps)
     ("traffic_c3.json", "r03_pmc_c3", "D16777216_nnz39_B-1", "classic", 20),
-    ("traffic_c4.json", "r02_pmc_c4", "D4096_nnz4096_B65536", "dense", 0),
+    # round 4: C4 in the reference order (K6r, one launch per step)
+    ("traffic_c4.json", "r04_pmc_c4", "D4096_nnz4096_B65536", "dense", 0),
     ("traffic_c5.json", "r02_pmc_c5", "D268435456_nnz10_B1024", "touched", 0),
 ]
 
