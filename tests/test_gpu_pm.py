@@ -195,6 +195,30 @@ def test_pm_exchange_pieces(monkeypatch, pieces, loop):
     assert_same_weights(got.w, orc.w, f"{pieces} pieces, {loop} loopback")
 
 
+@pytest.mark.parametrize("loop", ["async", "sync"])
+def test_pm_exchange_form_agreed_over_ranks(monkeypatch, loop):
+    # one rank asks for the plain all-gather before loading, the others for
+    # the pieced one (the default): the ranks agree at load on the plain
+    # form (the two forms are different collective sequences),
+    # every rank reports it, and the weights are the oracle's
+    monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
+    monkeypatch.setenv("DLR_PM", "1")
+    monkeypatch.setenv("DLR_LOOPBACK_SYNC", "1" if loop == "sync" else "0")
+    D, W = 300_000, 3
+    shards = [dlr.Dataset.generate(1500, D, 20, value_mode=1, seed=47, stream=r + 1) for r in range(W)]
+    seen = []
+
+    def pre(eng, r):
+        if r == 1:
+            eng.set_exchange_overlap(False)
+
+    got = run_group(shards, D, 2, 250, 0.2, preload=pre,
+                    setup=lambda eng: seen.append((eng.train_product_margin(), eng.exchange_overlap())))
+    assert len(seen) == W and all(pm == 1 and not ov for pm, ov in seen), seen
+    orc = oracle.run_worker([oracle_shard(s, D) for s in shards], D, 2, 250, 0.2)
+    assert_same_weights(got.w, orc.w, "agreed plain all-gather")
+
+
 def test_pm_exchange_pieces_must_agree(monkeypatch):
     # ranks asking for different piece counts: every rank's load fails
     # (the pieces are collectives), none hangs
