@@ -438,7 +438,9 @@ def run_rank(args):
     row_rounds = eng.train_row_rounds() if args.kind != "dense" else 0
     margin_kind = "dense rows" if args.kind == "dense" else \
         ["gathers", "product margin (pass 1 separate)",
-         "product margin (pass 1 fused into the previous step's gradient)"][eng.train_product_margin()]
+         "product margin (pass 1 fused into the previous step's gradient)",
+         "product margin (pass 1 fused into the previous step's gradient, pass 2 into this step's)"][
+            eng.train_product_margin()]
     log(f"[rank {rank}] shard {args.rows} x {D}, nnz/row {args.nnz}: generated {t_gen:.1f}s, "
         f"{'streamed from host' if streamed else 'resident'} {train_bytes / 2**30:.2f} GiB in {t_load:.1f}s, "
         f"{nb} batches/epoch, gradient layout {layout}")

@@ -96,7 +96,12 @@ struct TrainShard {
     // chunk offsets at pmo_pofs[b], regions and slot-list offsets at pmo_rg[b]
     // (rg, qoff), slot lists at pmo_qs[b]; pm_p holds one batch's products.
     // pm_fused: the fused k_grad_lds forms the next batch's products.
-    bool pm = false, pm_fused = false;
+    // pm_mg: (one rank, pm_fused) the fused k_grad_lds also runs this
+    // batch's pass 2 (DevP2): pm_cnt its hand-off counters, pm_gen the
+    // launches so far.
+    bool pm = false, pm_fused = false, pm_mg = false;
+    uint32_t *pm_cnt = nullptr;
+    uint32_t pm_gen = 0;
     int64_t pmS = 0;
     int pm_groups = 0, pm_split = 1;
     uint32_t *pm_lbeg = nullptr, *pm_list = nullptr, *pm_pofs = nullptr, *pm_rg = nullptr, *pm_qoff = nullptr;
@@ -414,7 +419,7 @@ void free_train(dlr_ctx *c) {
                     (void *)t.lpslot, (void *)t.lpws, (void *)t.lprow, (void *)t.lpval, (void *)t.pm_lbeg,
                     (void *)t.pm_list, (void *)t.pm_pofs, (void *)t.pm_rg, (void *)t.pm_qoff, (void *)t.pm_val,
                     (void *)t.pm_p, (void *)t.pm_qs, (void *)t.xslices, (void *)t.rt_gq, (void *)t.rt_val,
-                    (void *)t.rt_cend, (void *)t.dref_sync})
+                    (void *)t.rt_cend, (void *)t.dref_sync, (void *)t.pm_cnt})
         dev_free(c, p);
     t = TrainShard();
     c->pm_ready = -1;
@@ -1656,9 +1661,19 @@ hipError_t dense_batch_done(dlr_ctx *c, int64_t b) {
     return e;
 }
 
+// Whether batch b's pass 2 runs inside its fused gradient launch (one rank,
+// k_grad_lds MG): launch_margin then forms only the products, if missing.
+bool pm_mg_ok(const dlr_ctx *c, int64_t b) {
+    const TrainShard &t = c->train;
+    if (!t.pm_mg || c->comm || !t.pcsc || t.rt) return false;
+    return dlr::grad_lds_mg_ok(pm_view(c, b), c->D, t.plan[(size_t)b].rows, t.phases);
+}
+
 // rowsum_only (dlr_stage_time): the product margin's pass 2 alone, on
 // whatever products pm_p holds (the same work; the residuals are not used).
-hipError_t launch_margin(dlr_ctx *c, int64_t b, bool rowsum_only = false) {
+// mg_next: the caller's next launch is batch b's fused gradient (one rank),
+// which then runs the product margin's pass 2 itself when pm_mg_ok.
+hipError_t launch_margin(dlr_ctx *c, int64_t b, bool rowsum_only = false, bool mg_next = false) {
     const TrainShard &t = c->train;
     if (t.dense) {
         dlr::DevDense dd;
@@ -1676,6 +1691,7 @@ hipError_t launch_margin(dlr_ctx *c, int64_t b, bool rowsum_only = false) {
             const hipError_t e = dlr::launch_pm_products(pm_view(c, b), c->w, c->D, t.pm_p, c->stream);
             if (e != hipSuccess) return e;
         }
+        if (mg_next && pm_mg_ok(c, b)) return hipSuccess;  // pass 2 runs in the gradient's launch (launch_gradient)
         c->pm_ready = -1;  // this step changes the weights
         return dlr::launch_pm_margin(pm_view(c, b), batch_view(c, b), t.pm_p, c->resid, c->stream);
     }
@@ -1763,6 +1779,16 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
         if (t.pm_fused && fused) {
             // the update, then the next batch's products from the new weights
             const int64_t nx = (b + 1) % (int64_t)t.plan.size();
+            if (pm_mg_ok(c, b)) {
+                const dlr::DevP2 mg{pm_view(c, b), batch_view(c, b), c->resid, t.pm_cnt, t.pm_gen};
+                const hipError_t e = dlr::launch_grad_lds_pm(pcsc_view(c, b), c->D, B, c->resid, c->w, lr, C,
+                                                             pm_view(c, nx), t.pm_p, c->stream, &mg);
+                if (e == hipSuccess) {
+                    ++t.pm_gen;
+                    c->pm_ready = nx;
+                }
+                return e;
+            }
             const hipError_t e = dlr::launch_grad_lds_pm(pcsc_view(c, b), c->D, B, c->resid, c->w, lr, C,
                                                          pm_view(c, nx), t.pm_p, c->stream);
             if (e == hipSuccess) c->pm_ready = nx;
@@ -2483,6 +2509,16 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 t.pm = true;
                 const char *pf = getenv("DLR_PM_FUSED");
                 t.pm_fused = !c->comm && !(pf && strcmp(pf, "0") == 0);
+                // the margin inside the gradient launch (DLR_PM_MG=0: its own
+                // launch, k_pm_margin)
+                const char *pg = getenv("DLR_PM_MG");
+                t.pm_mg = t.pm_fused && !t.rt && !(pg && strcmp(pg, "0") == 0);
+                if (t.pm_mg) {
+                    const size_t cb = (size_t)dlr::DevP2::kMgCntWords * 4;
+                    if ((rc = dev_alloc(c, (void **)&t.pm_cnt, cb))) return rc;
+                    HIPC(c, hipMemsetAsync(t.pm_cnt, 0, cb, c->stream));
+                    t.pm_gen = 0;
+                }
                 if (c->comm && (rc = build_overlap_groups(c))) return rc;
             } else if (pme && strcmp(pme, "1") == 0) {
                 return fail(c, DLR_E_ARG, "dlr_load_train: DLR_PM=1 but the batches do not fit the product margin");
@@ -2978,7 +3014,7 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
     const bool piped = band_pipeline_ok(c, b);  // margin and band gradients interleaved (band mode)
     if (!piped) {
         time_begin(c, &t0);
-        HIPC(c, launch_margin(c, b));
+        HIPC(c, launch_margin(c, b, false, !c->comm));
         time_end(c, 0, t0);
     }
     if (piped) {
@@ -3217,8 +3253,9 @@ int dlr_stage_time(dlr_ctx *c, int stage, int64_t first, int64_t count, float lr
         const int64_t rows = t.plan[(size_t)bb].rows;
         if (stage == DLR_STAGE_MARGIN) {
             // product margin: pass 2 alone -- in the training step pass 1 runs
-            // inside the previous step's gradient (counted there)
-            e = launch_margin(c, bb, t.pm_fused);
+            // inside the previous step's gradient (counted there); nothing
+            // when pass 2 runs in the gradient's launch too (pm_mg_ok)
+            e = launch_margin(c, bb, t.pm_fused, !c->comm);
         } else if (t.touched) {
             const int64_t n = t.tncols[(size_t)bb];
             const uint32_t *cols = t.tcols + t.tcoff[(size_t)bb];
@@ -3273,7 +3310,7 @@ int dlr_train_unit_values(dlr_ctx *c) {
 int dlr_train_product_margin(dlr_ctx *c) {
     if (!c) return DLR_E_ARG;
     if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_product_margin: no training shard loaded");
-    return c->train.pm ? (c->train.pm_fused ? 2 : 1) : 0;
+    return c->train.pm ? (c->train.pm_fused ? (c->train.pm_mg ? 3 : 2) : 1) : 0;
 }
 
 int dlr_train_row_rounds(dlr_ctx *c) {

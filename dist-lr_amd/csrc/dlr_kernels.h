@@ -151,6 +151,22 @@ struct DevPm {
     int split;             // pass-1 workgroups per slice (standalone pass)
 };
 
+// The product margin's pass 2 run INSIDE the fused gradient (k_grad_lds MG,
+// one rank): batch bt's blocks (pm) are summed at the launch's start and
+// published per gradient phase: phase p's blocks done are counted in 8
+// sub-counters cnt[((bank * 64 + p) * 8 + s) * 32] (block k in s = k % 8;
+// one 128-byte line each), bank = gen & 1, which is zero when launch gen
+// starts (each launch zeroes the other bank for the next; both zero when
+// cnt is allocated), so gen must go up by exactly one per launch.
+struct DevP2 {
+    DevPm pm;
+    DevBatch bt;
+    float *resid;
+    uint32_t *cnt;  // kMgCntWords words
+    static constexpr int64_t kMgCntWords = 2 * 64 * 8 * 32;
+    uint32_t gen;
+};
+
 // ROW-ROUND gradient (RT) of a product-margin batch (dlr_kernels.hip
 // "Row-round gradient").  Round t covers batch rows [t * kRtRows, (t + 1) *
 // kRtRows).  The entries of slice s in round t are gq / val [(s * rounds +
@@ -254,8 +270,12 @@ hipError_t launch_pm_margin(const DevPm &pm, const DevBatch &bt, const float *p,
 // k_grad_lds (fused update) that also forms the products of the NEXT batch
 // (next: its product-margin view) from the weights it has just updated:
 // pass 1 for free in the gradient's workgroups (slice s = workgroup s).
+// mg != null: this batch's pass 2 too, in the same launch (DevP2; resid is
+// then mg->resid, written by the launch; p holds this batch's products);
+// grad_lds_mg_ok says whether the batch's shape allows it.
+bool grad_lds_mg_ok(const DevPm &cur, int64_t D, int64_t B, int phases);
 hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const float *resid, float *w, float lr,
-                              float C, const DevPm &next, float *p, hipStream_t s);
+                              float C, const DevPm &next, float *p, hipStream_t s, const DevP2 *mg = nullptr);
 // The row-round gradient (DevRt): the update (fused) or the pushed gradient
 // (gout); next != null (fused only): also the next batch's products, as
 // launch_grad_lds_pm.  resid must hold rounds * kRtRows floats.

@@ -908,6 +908,16 @@ namespace {
 #ifndef DLR_ABL
 #define DLR_ABL 0
 #endif
+#ifndef DLR_MG_SLEEP  // the fused margin's poll interval (x 64 cycles)
+#define DLR_MG_SLEEP 8
+#endif
+#ifndef DLR_MG_HOLD  // 1: C2 26.8 vs 28.0 us per step (profiles/r04mg5)
+#define DLR_MG_HOLD 1
+#endif
+constexpr int kMgSub = 8;  // sub-counters per phase (DevP2)
+#ifndef DLR_MG_FILL_SC1
+#define DLR_MG_FILL_SC1 0
+#endif
 #ifndef DLR_PM_SC1
 #define DLR_PM_SC1 ((DLR_ABL & 16) != 0)
 #endif
@@ -1056,15 +1066,14 @@ __global__ __launch_bounds__(1024) void k_pm_products(DevPm pm, const float *__r
     pp.store(pm, s_w, s_po, p);
 }
 
-// Pass 2: a wave per block; lane l owns row 64k + l of bt.
-template <int QG>
-__global__ __launch_bounds__(256) void k_pm_margin(DevPm pm, DevBatch bt, const float *__restrict__ p,
-                                                   float *__restrict__ resid) {
-    __shared__ __attribute__((aligned(16))) float s_reg[4][kPmCap];
-    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
-    const int64_t blk = (int64_t)blockIdx.x * 4 + wv;
+// Pass 2 of block blk (one wave; lane l owns row 64 blk + l of bt) in the
+// wave's kPmCap-float LDS region sr.  SC1: the residuals are stored with sc1
+// (device scope), for readers on other CUs in the same launch (the fused
+// margin of k_grad_lds below).
+template <int QG, bool SC1>
+__device__ __forceinline__ void pm_rowsum(const DevPm &pm, const DevBatch &bt, const float *__restrict__ p,
+                                          float *resid, int64_t blk, float *sr, int lane) {
     const int64_t r0 = blk * kPmRows;
-    if (r0 >= bt.rows) return;  // wave-uniform
     const uint32_t a = pm.rg[blk], b = pm.rg[blk + 1];
     const uint32_t q0 = pm.qoff[blk], q1 = pm.qoff[blk + 1];
     const int64_t my = r0 + lane;
@@ -1072,7 +1081,6 @@ __global__ __launch_bounds__(256) void k_pm_margin(DevPm pm, DevBatch bt, const 
     const int64_t mc = valid ? my : r0;
     const int len = valid ? (int)(bt.row_ptr[mc + 1] - bt.row_ptr[mc]) : 0;
     const float y = bt.label[mc];
-    float *sr = s_reg[wv];
     const int n4 = (int)((b - a) >> 2);
     const int ngrp = (int)((q1 - q0) >> 9);
     constexpr int R4 = kPmCap / 4 / kWave;
@@ -1112,17 +1120,48 @@ __global__ __launch_bounds__(256) void k_pm_margin(DevPm pm, DevBatch bt, const 
             acc = (g * 8 + u < len) ? t : acc;
         }
     }
-    if (valid) resid[my] = sigmoid_ref(acc) - y;
+    if (valid) {
+        const float r = sigmoid_ref(acc) - y;
+        if (SC1) {
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(resid, 0, 0x7FFFFFFF, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), rs, (int)(my * 4), 0, 16);  // sc1
+        } else {
+            resid[my] = r;
+        }
+    }
+}
+
+// Pass 2: a wave per block.
+template <int QG>
+__global__ __launch_bounds__(256) void k_pm_margin(DevPm pm, DevBatch bt, const float *__restrict__ p,
+                                                   float *__restrict__ resid) {
+    __shared__ __attribute__((aligned(16))) float s_reg[4][kPmCap];
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    const int64_t blk = (int64_t)blockIdx.x * 4 + wv;
+    if (blk * kPmRows >= bt.rows) return;  // wave-uniform
+    pm_rowsum<QG, false>(pm, bt, p, resid, blk, s_reg[wv], lane);
 }
 
 // PM (with FUSED): after the update, form the NEXT batch's products of this
 // workgroup's slice (pm_pass1 below) from the new weights.
-template <int FILL, bool FUSED, bool NTW, bool PM = false>
+// MG (with PM; one rank): this batch's pass 2 (the margin) runs in the same
+// launch, first thing (dlr_kernels.h DevP2): wave v of workgroup x sums
+// block x + v * grid in LDS that the residual fills use only later, stores
+// the residuals with sc1 and adds 1 to its phase's counter (agent scope);
+// every workgroup waits for phase p's count before its fill of phase p
+// (wave 0 polls with sc1 loads, bounded; the fill is sc1 too).  The grid is
+// one workgroup per CU (LDS), so all of them are resident and every block
+// is summed; the pass-1 stores into p come after the last phase's wait, so
+// after every block's copy of its region.  The launch boundary between the
+// margin and the gradient is gone and the gradient's window loads stream
+// while the blocks are summed.
+template <int FILL, bool FUSED, bool NTW, bool PM = false, bool MG = false>
 __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int64_t D, int64_t B,
                                                                 const float *__restrict__ resid,
                                                                 float *__restrict__ w, float *__restrict__ gout,
                                                                 float Bf, double Bd, float lr, float C,
-                                                                DevPm pn = DevPm{}, float *__restrict__ pm_p = nullptr) {
+                                                                DevPm pn = DevPm{}, float *__restrict__ pm_p = nullptr,
+                                                                DevP2 p2 = DevP2{}) {
     constexpr int R = FILL * 4096;
     constexpr int NG = kGradNG;
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1136,6 +1175,50 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     const int64_t gfirst = (int64_t)blockIdx.x * (kGradWaves * NG) + wv;
     PmPass1<kGradWaves * kWave, 4> pm;
     if (PM && !(DLR_ABL & 4)) pm.bounds(pn, blockIdx.x);  // first (PmPass1::bounds)
+    static_assert(!MG || (PM && FUSED), "the fused margin comes with the fused pass 1");
+    if constexpr (MG) {
+        DLR_STAMP(11);
+        if (blockIdx.x == 0 && wv < 8)  // the next launch's bank: 64 phases x 8 sub-counters
+            p2.cnt[(((p2.gen + 1) & 1) * 64 + lane) * kMgSub * 32 + wv * 32] = 0u;
+        const int64_t k2 = blockIdx.x + (int64_t)gridDim.x * wv;  // wv < FILL (launch_grad_lds_pm)
+        if (k2 < p2.pm.nblk) {  // wave-uniform
+            pm_rowsum<8, true>(p2.pm, p2.bt, pm_p, p2.resid, k2, smem + wv * kPmCap, lane);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every residual of the block stored
+            // sub-counter k2 % 8 of the phase (each on a line of its own:
+            // the adds and the polls spread over 8 lines)
+            if (lane == 0)
+                __hip_atomic_fetch_add(
+                    p2.cnt + (((p2.gen & 1) * 64 + (k2 * kPmRows) / R) * kMgSub + (k2 % kMgSub)) * 32, 1u,
+                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        DLR_STAMP(12);
+        // the other waves' window loads wait for the workgroup's blocks (the
+        // blocks' loads have the CU's memory path to themselves: the phases
+        // wait for the slowest block; DLR_MG_HOLD=0 issues them at once)
+        if (DLR_MG_HOLD) lds_barrier();
+    }
+    // wave 0 waits until every block of phase p is published (the caller's
+    // barrier then holds the other waves' fills)
+    auto mg_wait = [&](int p) {
+        if constexpr (MG) {
+            if (wv == 0) {
+                constexpr int64_t bpp = R / kPmRows;
+                const uint32_t want = (uint32_t)(min<int64_t>(p2.pm.nblk, (p + 1) * bpp) - p * bpp);
+                const __amdgpu_buffer_rsrc_t crs =
+                    __builtin_amdgcn_make_buffer_rsrc(p2.cnt, 0, 0x7FFFFFFF, 0x00020000);
+                // lane s < 8 reads sub-counter s
+                const int off = (int)(((((p2.gen & 1) * 64 + p) * kMgSub + (lane & (kMgSub - 1))) * 32) * 4);
+                for (int k = 0; k < (1 << 20); ++k) {
+                    const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(crs, off, 0, 16);
+                    uint32_t n = 0;
+#pragma unroll
+                    for (int i = 0; i < kMgSub; ++i) n += __builtin_amdgcn_readlane(v, i);
+                    if (n >= want) break;
+                    __builtin_amdgcn_s_sleep(DLR_MG_SLEEP);
+                }
+            }
+        }
+    };
     unsigned bs[NG][2], off[NG][2], cnt[NG][2], nblk[NG][2];
     float acc[NG], wj[NG];
     ushort4 rq[NG][2];
@@ -1186,13 +1269,21 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     };
     // Residual fills by LDS-DMA (no VGPRs): each wave-instruction copies
     // 1 KiB -- lane l's 16 bytes land at the wave-uniform base + 16*l.
+    // (MG: the residuals were stored in this launch by other CUs, through
+    // p2.resid.  Plain loads: no CU reads a residual line before its block
+    // is published -- the launch starts with this XCD's L2 and every L1
+    // holding no residual line (the kernel-start acquire), the blocks' sc1
+    // stores have reached memory before their counter moved, and a line
+    // belongs to one block -- so the first read of a line, and every later
+    // hit on it, sees the stored values.  DLR_MG_FILL_SC1=1: sc1 fills.)
+    const float *rsrc = MG ? p2.resid : resid;
     auto fill = [&](int64_t lo) {
 #pragma unroll
         for (int f = 0; f < R / (kGradWaves * kWave * 4); ++f) {  // FILL with 16 waves
             const int o = (f * kGradWaves + wv) * kWave * 4;  // floats; this wave's 1 KiB slot
             __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void *)(resid + lo + o + lane * 4),
-                (__attribute__((address_space(3))) void *)(s_r + o), 16, 0, 0);
+                (const __attribute__((address_space(1))) void *)(rsrc + lo + o + lane * 4),
+                (__attribute__((address_space(3))) void *)(s_r + o), 16, 0, MG && DLR_MG_FILL_SC1 ? 16 : 0);
         }
     };
     // Phase 0's windows and the first fill are issued up front; phase 1's
@@ -1201,6 +1292,11 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     // the rest of phase 0 computes instead of delaying its start.
     DLR_STAMP(0);
     windows(0);
+    if constexpr (MG) {
+        mg_wait(0);
+        lds_barrier();  // and this workgroup's pass-2 regions are read
+        DLR_STAMP(13);
+    }
     if (!(DLR_ABL & 1)) fill(0);
     DLR_STAMP(8);
 #ifdef DLR_STAMPS
@@ -1213,6 +1309,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
         if (p >= P) break;  // uniform
         if (p > 0) {
             DLR_STAMP(2);
+            mg_wait(p);
             lds_barrier();  // every wave is done reading the previous phase
             DLR_STAMP(3);
             fill((int64_t)p * R);  // resid is padded to P*R floats
@@ -3751,13 +3848,21 @@ hipError_t launch_pm_margin(const DevPm &pm, const DevBatch &bt, const float *p,
     return hipGetLastError();
 }
 
+bool grad_lds_mg_ok(const DevPm &cur, int64_t D, int64_t B, int phases) {
+    const int64_t grid = (D + kPmSlice - 1) / kPmSlice;
+    return D > 0 && cur.groups <= 8 && cur.nblk == (B + kPmRows - 1) / kPmRows &&
+           cur.nblk <= grid * grad_lds_fill(B) && phases >= 1 && phases <= 64;
+}
+
 hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const float *resid, float *w, float lr,
-                              float C, const DevPm &next, float *p, hipStream_t s) {
+                              float C, const DevPm &next, float *p, hipStream_t s, const DevP2 *mg) {
     if (D <= 0) return hipSuccess;
     const int64_t ng = (D + 63) / 64;
     const unsigned grid = (unsigned)((ng + kGradWaves * kGradNG - 1) / (kGradWaves * kGradNG));
     static_assert(kGradWaves * kGradNG * 64 == kPmSlice, "a gradient workgroup's columns are one slice");
     if ((int64_t)grid != next.S || next.nblk > kPmMaxBlocks) return hipErrorInvalidValue;
+    if (mg && (!grad_lds_mg_ok(mg->pm, D, B, pc.phases) || mg->bt.rows != B || !mg->cnt || !mg->resid))
+        return hipErrorInvalidValue;
     const dim3 blk(kGradWaves * kWave);
     const float Bf = (float)B;
     const double Bd = (double)B;
@@ -3766,8 +3871,12 @@ hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const flo
                                 (size_t)(kPmSlice + kPmMaxBlocks) * 4);
 #define DLR_GLP(F)                                                                                            \
     case F:                                                                                                   \
-        hipLaunchKernelGGL((k_grad_lds<F, true, false, true>), dim3(grid), blk, lds, s, pc, D, B, resid, w,   \
-                           nullptr, Bf, Bd, lr, C, next, p);                                                 \
+        if (mg)                                                                                               \
+            hipLaunchKernelGGL((k_grad_lds<F, true, false, true, true>), dim3(grid), blk, lds, s, pc, D, B,   \
+                               resid, w, nullptr, Bf, Bd, lr, C, next, p, *mg);                               \
+        else                                                                                                  \
+            hipLaunchKernelGGL((k_grad_lds<F, true, false, true>), dim3(grid), blk, lds, s, pc, D, B, resid,  \
+                               w, nullptr, Bf, Bd, lr, C, next, p);                                           \
         break;
     switch (fill) {
         DLR_GLP(1)

@@ -379,7 +379,11 @@ int dlr_train_unit_values(dlr_ctx *ctx);
 
 /* The margin of the loaded sparse training shard: 0 = gathers (one weight
  * read per entry), 1 = PRODUCT MARGIN with a separate pass 1, 2 = product
- * margin with pass 1 inside the previous step's gradient (one rank).  The
+ * margin with pass 1 inside the previous step's gradient (one rank), 3 = as
+ * 2 and pass 2 inside the step's own gradient launch (one rank, LDS-phase
+ * gradient, rows of <= 64 entries: the launch sums the batch's rows first and
+ * hands the residuals to the gradient's phases through device-scope counters;
+ * DLR_PM_MG=0 keeps it a launch of its own).  The
  * product margin (LDS-layout batches, >= 128 column slices of 4,096; resident
  * shards) forms every product fl32(w_j * x_ij) by column slice from LDS-staged
  * weights, then sums each row's products in column order from LDS: bitwise

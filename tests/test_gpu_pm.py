@@ -44,12 +44,24 @@ def _mode_of(ds, D, B):
         eng.close()
 
 
-@pytest.fixture(params=["fused", "separate"])
+def _rounds_of(ds, D, B):
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(dlr.init_weight(D))
+        eng.load_train(ds, B)
+        return eng.train_row_rounds()
+    finally:
+        eng.close()
+
+
+@pytest.fixture(params=["fused-mg", "fused", "separate"])
 def pm_on(request, monkeypatch):
+    # fused-mg: pass 2 in the gradient's launch too (DLR_PM_MG, the default)
     monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
     monkeypatch.setenv("DLR_PM", "1")
-    monkeypatch.setenv("DLR_PM_FUSED", "1" if request.param == "fused" else "0")
-    return 2 if request.param == "fused" else 1
+    monkeypatch.setenv("DLR_PM_FUSED", "0" if request.param == "separate" else "1")
+    monkeypatch.setenv("DLR_PM_MG", "1" if request.param == "fused-mg" else "0")
+    return {"fused-mg": 3, "fused": 2, "separate": 1}[request.param]
 
 
 @pytest.mark.parametrize("value_mode", [0, 1])
@@ -59,7 +71,9 @@ def test_pm_batch_sizes_and_wraps(pm_on, B, value_mode):
     # divide N, wrap at the epoch end, or wrap twice (B > N)
     D = 30000
     ds = dlr.Dataset.generate(1000, D, 20, value_mode=value_mode, seed=3, stream=1)
-    assert _mode_of(ds, D, B) == pm_on
+    # the margin in the gradient's launch (3) needs the LDS-phase gradient:
+    # row-round batches (small B) keep pass 2 a launch of its own (2)
+    assert _mode_of(ds, D, B) == (2 if pm_on == 3 and _rounds_of(ds, D, B) else pm_on)
     eng = run_engine([ds], D, 3, B, 0.1)
     orc = oracle.run_worker([oracle_shard(ds, D)], D, 3, B, 0.1)
     compare_runs(eng, orc)
@@ -108,7 +122,7 @@ def test_pm_guess_misses_and_weight_changes(monkeypatch):
             eng.set_weights(dlr.init_weight(D))
             assert eng.load_train(ds, 500) == nb
             eng.load_test(test)
-            assert eng.train_product_margin() == (2 if pm == "1" else 0)
+            assert eng.train_product_margin() == (2 if pm == "1" else 0)  # row rounds: pass 2 separate
             out = []
             for k, b in enumerate(order):
                 if k in perturb:
@@ -301,7 +315,7 @@ def test_pm_default_on_c2_shape():
     try:
         eng.set_weights(w0)
         nb = eng.load_train(ds, 65536)
-        assert eng.train_layout() == dlr.LAYOUT_LDS and eng.train_product_margin() == 2
+        assert eng.train_layout() == dlr.LAYOUT_LDS and eng.train_product_margin() == 3
         w = w0.copy()
         for b in range(2 * nb + 1):
             bb = b % nb
@@ -331,7 +345,7 @@ def test_pm_row_round_gradient(monkeypatch, rt, B):
     try:
         eng.set_weights(w)
         nb = eng.load_train(ds, B)
-        assert eng.train_product_margin() == 2
+        assert eng.train_product_margin() == (2 if rt == "1" else 3)
         assert eng.train_row_rounds() == ((B + 8191) // 8192 if rt == "1" else 0)
         for b in range(nb + 1):  # an epoch (the last batch wraps) + the next epoch's first
             eng.train_step(b % nb, 0.2, 1.0)
@@ -340,3 +354,57 @@ def test_pm_row_round_gradient(monkeypatch, rt, B):
         assert_same_weights(eng.get_weights(), w)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("B", [20000, 65536])
+def test_pm_margin_in_gradient_launch(monkeypatch, B):
+    # Pass 2 inside the fused gradient's launch (dlr_train_product_margin 3,
+    # k_grad_lds MG): ragged rows of 0..64 entries (empty rows, whole empty
+    # 64-row blocks), a wrapping last batch, steps out of order and repeated,
+    # set_weights between steps (the products are re-formed: a guess missed)
+    # -- bitwise the separate pass 2 (DLR_PM_MG=0) and the oracle.
+    D = 1 << 20
+    rng = np.random.default_rng(21)
+    n = 150_000
+    lens = rng.integers(0, 65, size=n)
+    lens[rng.choice(n, 5000, replace=False)] = 0
+    lens[64 * 100:64 * 102] = 0  # two empty blocks
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    col = np.concatenate([np.sort(rng.choice(D, k, replace=False)) for k in lens]).astype(np.int32)
+    val = rng.integers(1, 10001, size=len(col)).astype(np.float32) / np.float32(10000)
+    lab = rng.integers(0, 2, size=n).astype(np.int32)
+    ds = dlr.Dataset.from_csr(rp, col, val, lab, D)
+    w0 = dlr.init_weight(D)
+    order = [0, 1, 2, 2, 0, 1, 1, 2, 0]
+    bump = {4: rng.standard_normal(D).astype(np.float32) * np.float32(0.01)}
+
+    def run(mg):
+        monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
+        monkeypatch.setenv("DLR_PM", "1")
+        monkeypatch.setenv("DLR_PM_MG", mg)
+        eng = dlr.Engine(D)
+        try:
+            eng.set_weights(w0)
+            nb = eng.load_train(ds, B)
+            assert eng.train_product_margin() == (3 if mg == "1" else 2)
+            assert eng.train_row_rounds() == 0
+            out = []
+            for k, b in enumerate(order):
+                if k in bump:
+                    eng.set_weights(eng.get_weights() + bump[k])
+                eng.train_step(b % nb, 0.2, 1.0)
+                out.append(eng.get_weights())
+            return out, nb
+        finally:
+            eng.close()
+
+    (got, nb), (ref, _) = run("1"), run("0")
+    for a, b in zip(got, ref):
+        assert_same_weights(a, b)
+    w = w0.copy()
+    for k, b in enumerate(order):
+        if k in bump:
+            w = w + bump[k]
+        g = oracle.grad_csr((rp, col, val), lab, oracle.batch_rows(n, B, b % nb), w)
+        oracle.server_update(w, [g], 0.2)
+    assert_same_weights(got[-1], w)

@@ -14,7 +14,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CASES = [
-    ("traffic.json", "r03_pmc_c2", "D1000000_nnz50_B65536", "lds", 0),
+    # round 4: the margin in the gradient's launch (one launch per step)
+    ("traffic.json", "r04_pmc_c2", "D1000000_nnz50_B65536", "lds", 0),
     # round 3: the band-pipelined margin is dispatched per band; 20 step-
     # equivalents (bench --steps 6 --warmup 2: 2 + 6 timed + 6 + 6 stage and
     # breakdown steps)

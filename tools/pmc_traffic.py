@@ -88,18 +88,29 @@ def main() -> int:
     # (C5): the dense L2 pass and the scatter are the update role.
     # Product margin (C2): pass 2 is the margin role, a separate pass 1
     # (k_pm_products) too; a fused pass 1 is inside k_grad_lds (grad role).
+    # The product margin in the gradient's launch (k_grad_lds<F, true,
+    # false, true, true>: pass 2 + gradient + update + next pass 1) is a step
+    # of its own, like K6r.  A kernel counts in the first role that matches.
+    mg = ", true, false, true, true>"
     roles = [("margin", ["k_margin", "k_pm_margin", "k_pm_products", "k_dense_fused", "k_dense_margin"]),
-             ("step", ["k_dense_ref<"]),  # K6r: margin + gradient + update in one launch
+             ("step", ["k_dense_ref<", mg]),  # one launch: margin + gradient + update
              ("grad", ["k_grad", "k_long_", "k_band_finalize", "k_band_hot", "k_dense_grad", "k_dense_combine"]),
              ("update", ["k_dense_l2", "k_scatter", "k_merge_update", "k_sparse_merge"])]
-    steps = args.steps or len([x for k in ["k_margin", "k_pm_margin", "k_dense_fused", "k_dense_margin", "k_dense_ref<"]
-                               for x in pick(bf, k)]) or 1
+    steps = args.steps or len([x for k in ["k_margin", "k_pm_margin", "k_dense_fused", "k_dense_margin", "k_dense_ref<",
+                                           mg] for x in pick(bf, k)]) or 1
+    taken: set[str] = set()
+
+    def take(d, keys):
+        out = []
+        for name, v in d.items():
+            if name not in taken and any(k in name for k in keys):
+                out.extend(v)
+        return out
+
     total = 0.0
     for short, keys in roles:
-        f = [x for k in keys for x in pick(bf, k)]
-        w = [x for k in keys for x in pick(bw, k)]
-        h = [x for k in keys for x in pick(hits, k)]
-        m = [x for k in keys for x in pick(miss, k)]
+        f, w, h, m = take(bf, keys), take(bw, keys), take(hits, keys), take(miss, keys)
+        taken.update(n for d in (bf, bw, hits, miss) for n in d if any(k in n for k in keys))
         if not f:
             continue
         fk, wk = sum(f) / steps, (sum(w) / steps if w else 0.0)
