@@ -914,6 +914,9 @@ namespace {
 #ifndef DLR_MG_HOLD  // 1: C2 26.8 vs 28.0 us per step (profiles/r04mg5)
 #define DLR_MG_HOLD 1
 #endif
+#ifndef DLR_MG_EVEN  // workgroups past the slices to even out the blocks
+#define DLR_MG_EVEN 1
+#endif
 constexpr int kMgSub = 8;  // sub-counters per phase (DevP2)
 #ifndef DLR_MG_FILL_SC1
 #define DLR_MG_FILL_SC1 0
@@ -1174,7 +1177,8 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     const int64_t ng = (D + 63) / 64;
     const int64_t gfirst = (int64_t)blockIdx.x * (kGradWaves * NG) + wv;
     PmPass1<kGradWaves * kWave, 4> pm;
-    if (PM && !(DLR_ABL & 4)) pm.bounds(pn, blockIdx.x);  // first (PmPass1::bounds)
+    // (MG: workgroups past the slices only sum blocks)
+    if (PM && !(DLR_ABL & 4) && (!MG || blockIdx.x < pn.S)) pm.bounds(pn, blockIdx.x);  // first (PmPass1::bounds)
     static_assert(!MG || (PM && FUSED), "the fused margin comes with the fused pass 1");
     if constexpr (MG) {
         DLR_STAMP(11);
@@ -1192,6 +1196,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         DLR_STAMP(12);
+        if (blockIdx.x >= pn.S) return;  // a block-only workgroup (launch_grad_lds_pm): done
         // the other waves' window loads wait for the workgroup's blocks (the
         // blocks' loads have the CU's memory path to themselves: the phases
         // wait for the slowest block; DLR_MG_HOLD=0 issues them at once)
@@ -3863,6 +3868,20 @@ hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const flo
     if ((int64_t)grid != next.S || next.nblk > kPmMaxBlocks) return hipErrorInvalidValue;
     if (mg && (!grad_lds_mg_ok(mg->pm, D, B, pc.phases) || mg->bt.rows != B || !mg->cnt || !mg->resid))
         return hipErrorInvalidValue;
+    // MG: up to one workgroup per CU (every workgroup must be resident: the
+    // phases wait for every block), past the slices when that evens the
+    // blocks out (C2: 1,024 blocks on 256 workgroups, 4 each, not 245 with
+    // up to 5); the extra workgroups only sum blocks
+    unsigned mgrid = grid;
+    if (mg) {
+        static int ncu[64] = {};
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidValue;
+        if (!ncu[dev] && hipDeviceGetAttribute(&ncu[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return hipErrorInvalidValue;
+        const int64_t even = (mg->pm.nblk + 3) / 4;
+        if (DLR_MG_EVEN && even > (int64_t)grid && even <= ncu[dev]) mgrid = (unsigned)even;
+    }
     const dim3 blk(kGradWaves * kWave);
     const float Bf = (float)B;
     const double Bd = (double)B;
@@ -3872,7 +3891,7 @@ hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const flo
 #define DLR_GLP(F)                                                                                            \
     case F:                                                                                                   \
         if (mg)                                                                                               \
-            hipLaunchKernelGGL((k_grad_lds<F, true, false, true, true>), dim3(grid), blk, lds, s, pc, D, B,   \
+            hipLaunchKernelGGL((k_grad_lds<F, true, false, true, true>), dim3(mgrid), blk, lds, s, pc, D, B,  \
                                resid, w, nullptr, Bf, Bd, lr, C, next, p, *mg);                               \
         else                                                                                                  \
             hipLaunchKernelGGL((k_grad_lds<F, true, false, true>), dim3(grid), blk, lds, s, pc, D, B, resid,  \
