@@ -845,6 +845,11 @@ namespace {
     do {                                                                                     \
         if (threadIdx.x == 0) g_stamp[blockIdx.x * 16 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+// the same, written by thread tid (another wave's view)
+#define DLR_STAMPW(slot, tid)                                                                \
+    do {                                                                                     \
+        if (threadIdx.x == (tid)) g_stamp[blockIdx.x * 16 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 // k_dense_ref: 64 slots per workgroup, written by one chosen lane
 #define DLR_STAMP64(slot, cond)                                                                      \
     do {                                                                                             \
@@ -884,6 +889,9 @@ namespace {
     } while (0)
 #define DLR_STAMP(slot) \
     do {                \
+    } while (0)
+#define DLR_STAMPW(slot, tid) \
+    do {                      \
     } while (0)
 #define DLR_STAMP64(slot, cond) \
     do {                        \
@@ -1196,6 +1204,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         DLR_STAMP(12);
+        DLR_STAMPW(14, 3 * kWave);  // wave 3's block (the last of a CU's four)
         if (blockIdx.x >= pn.S) return;  // a block-only workgroup (launch_grad_lds_pm): done
         // the other waves' window loads wait for the workgroup's blocks (the
         // blocks' loads have the CU's memory path to themselves: the phases

@@ -23,7 +23,7 @@ import torch  # noqa: E402  (one HIP runtime: torch's)
 
 import distlr_amd as dlr  # noqa: E402
 
-SLOTS = {11: "mg start", 12: "mg p2 pub", 13: "mg ph0 ok", 0: "start", 8: "win0+fill0 out", 9: "w0 drained", 10: "pass1 ld out", 1: "ph0 go", 2: "ph0 done",
+SLOTS = {11: "mg start", 12: "mg p2 pub", 14: "mg p2 pub w3", 13: "mg ph0 ok", 0: "start", 8: "win0+fill0 out", 9: "w0 drained", 10: "pass1 ld out", 1: "ph0 go", 2: "ph0 done",
          3: "fill1 out", 4: "ph1 go", 5: "compute end", 6: "pass1 go", 7: "end"}
 # the row-round kernel (k_grad_rt, the default for product-margin batches)
 SLOTS_RT = {0: "start", 1: "issued", **{2 + t: f"round {t} go" for t in range(8)}, 10: "rounds done",
