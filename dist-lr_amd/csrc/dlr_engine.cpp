@@ -256,6 +256,11 @@ struct dlr_ctx {
     int64_t ll_cap = 0;
     unsigned long long *h_correct = nullptr;  // pinned
     double *h_ll = nullptr;                   // pinned
+    // in-launch hand-off errors (dlr_kernels.h DevErr): kErrWords words of
+    // host-mapped memory the kernels store to when a bounded wait runs out
+    // (h_err: host view, d_err: device view); checked by check_device
+    uint32_t *h_err = nullptr, *d_err = nullptr;
+    int fault = dlr::kFaultNone;  // dlr_set_fault (tests)
     TrainShard train;
     TestShard test;
     // exchange / next-margin overlap (TrainShard::xslices): asked for unless
@@ -345,6 +350,37 @@ int wait_stream(dlr_ctx *c, hipStream_t s, const char *who) {
     return DLR_OK;
 }
 
+// The hand-off errors the context's kernels have recorded (sticky until the
+// next load): a bounded wait inside a launch ran out, so the launch computed
+// on data that never arrived -- the step fails instead of returning weights
+// (lr.cc:122, 131: the reference's worker waits until its data is there).
+// Reads host memory only: the caller has synchronized for a definitive
+// answer, or (dlr_train_step) sees what earlier steps recorded.
+int check_device(dlr_ctx *c, const char *who) {
+    if (!c->h_err) return DLR_OK;
+    static const char *what[dlr::kErrWords] = {
+        "the fused margin's blocks of a phase were never all published (k_grad_lds, one-launch step)",
+        "a chain slot's margin units were never published (k_dense_ref)",
+        "the column chains' limit never reached a margin unit (k_dense_ref)",
+        "a hand-off between the waves of a workgroup never came (k_dense_ref)",
+        "a hand-off between the waves of a workgroup never came (k_band_hot)",
+        "unknown", "unknown", "unknown"};
+    std::string msg;
+    for (int k = 0; k < dlr::kErrWords; ++k) {
+        if (__atomic_load_n(c->h_err + k, __ATOMIC_ACQUIRE) == 0u) continue;
+        msg += msg.empty() ? "" : "; ";
+        msg += what[k];
+    }
+    if (msg.empty()) return DLR_OK;
+    return fail(c, DLR_E_DEVICE, std::string(who) + ": in-launch wait ran out: " + msg +
+                                     " -- the weights are not the reference's; reload the shard");
+}
+
+void clear_device_errors(dlr_ctx *c) {
+    if (c->h_err)
+        for (int k = 0; k < dlr::kErrWords; ++k) __atomic_store_n(c->h_err + k, 0u, __ATOMIC_RELEASE);
+}
+
 int dev_alloc(dlr_ctx *c, void **p, size_t bytes) {
     *p = nullptr;
     if (bytes == 0) bytes = 16;
@@ -374,7 +410,7 @@ int upload(dlr_ctx *c, T **dst, const T *src, size_t n, size_t pad = 0) {
     if (rc) return rc;
     if (n) HIPC(c, hipMemcpyAsync(*dst, src, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
     if (pad) HIPC(c, hipMemsetAsync(*dst + n, 0, pad * sizeof(T), c->stream));
-    HIPC(c, hipStreamSynchronize(c->stream));
+    if (int rc_ = wait_stream(c, c->stream, __func__)) return rc_;
     return DLR_OK;
 }
 
@@ -423,6 +459,7 @@ void free_train(dlr_ctx *c) {
         dev_free(c, p);
     t = TrainShard();
     c->pm_ready = -1;
+    clear_device_errors(c);  // nothing of the old shard runs any more
 }
 
 template <typename T>
@@ -528,8 +565,10 @@ int coll_reduce_i64(dlr_ctx *c, int64_t *v, size_t n, bool max) {
     hipError_t e = hipMemcpyAsync(d, v, n * 8, hipMemcpyHostToDevice, c->stream);
     const bool ok = e == hipSuccess && c->comm->all_reduce_i64(d, n, max, c->stream, err);
     if (ok) e = hipMemcpyAsync(v, d, n * 8, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    // through the transport: a peer's abort ends the wait
+    const int wrc = wait_stream(c, c->stream, "coll_reduce_i64");
     dev_free(c, d);
+    if (wrc) return wrc;
     if (e != hipSuccess) return fail(c, DLR_E_HIP, std::string("coll_reduce_i64: ") + hipGetErrorString(e));
     if (!ok) return fail(c, DLR_E_RCCL, std::string(c->comm->kind()) + " " + err);
     return DLR_OK;
@@ -551,8 +590,9 @@ int coll_gather_f32(dlr_ctx *c, float v, std::vector<float> &out) {
     hipError_t e = hipMemcpyAsync(d + W, &v, 4, hipMemcpyHostToDevice, c->stream);
     const bool ok = e == hipSuccess && c->comm->all_gather(d + W, d, 1, c->stream, err);
     if (ok) e = hipMemcpyAsync(out.data(), d, (size_t)W * 4, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    const int wrc = wait_stream(c, c->stream, "coll_gather_f32");
     dev_free(c, d);
+    if (wrc) return wrc;
     if (e != hipSuccess) return fail(c, DLR_E_HIP, std::string("coll_gather_f32: ") + hipGetErrorString(e));
     if (!ok) return fail(c, DLR_E_RCCL, std::string(c->comm->kind()) + " " + err);
     return DLR_OK;
@@ -698,7 +738,7 @@ int change_perm(dlr_ctx *c, std::vector<int32_t> &&np) {
     const int64_t D = c->D;
     std::vector<float> oldw((size_t)D), neww((size_t)D);
     HIPC(c, hipMemcpyAsync(oldw.data(), c->w, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipStreamSynchronize(c->stream));
+    if (int rc_ = wait_stream(c, c->stream, __func__)) return rc_;
     for (int64_t j = 0; j < D; ++j) neww[(size_t)pid(np, j)] = oldw[(size_t)pid(c->perm, j)];
     c->pm_ready = -1;
     HIPC(c, hipMemcpyAsync(c->w, neww.data(), (size_t)D * 4, hipMemcpyHostToDevice, c->stream));
@@ -711,11 +751,11 @@ int change_perm(dlr_ctx *c, std::vector<int32_t> &&np) {
         }
         std::vector<int32_t> col((size_t)t.nnz);
         HIPC(c, hipMemcpyAsync(col.data(), t.col, (size_t)t.nnz * 4, hipMemcpyDeviceToHost, c->stream));
-        HIPC(c, hipStreamSynchronize(c->stream));
+        if (int rc_ = wait_stream(c, c->stream, __func__)) return rc_;
         for (auto &x : col) x = (int32_t)pid(np, inv.empty() ? x : inv[(size_t)x]);
         HIPC(c, hipMemcpyAsync(t.col, col.data(), (size_t)t.nnz * 4, hipMemcpyHostToDevice, c->stream));
     }
-    HIPC(c, hipStreamSynchronize(c->stream));
+    if (int rc_ = wait_stream(c, c->stream, __func__)) return rc_;
     c->perm = std::move(np);
     return DLR_OK;
 }
@@ -1751,7 +1791,7 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
         if (e == hipSuccess && t.dref) {
             const int64_t nw = dlr::dense_ref_sync_words(B);
             const dlr::DevRefSync sy{t.dref_sync, t.dref_sync + nw - 64, t.dref_sync + nw - 32, t.dref_seq,
-                                     t.dref_lead, 0};
+                                     t.dref_lead, 0, c->d_err, c->fault};
             e = dlr::launch_dense_ref(dd, first, B, c->w, gout, c->resid, sy, lr, C, fused, c->stream);
             if (e == hipSuccess) ++c->train.dref_seq;
         } else if (e == hipSuccess)
@@ -1780,7 +1820,7 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
             // the update, then the next batch's products from the new weights
             const int64_t nx = (b + 1) % (int64_t)t.plan.size();
             if (pm_mg_ok(c, b)) {
-                const dlr::DevP2 mg{pm_view(c, b), batch_view(c, b), c->resid, t.pm_cnt, t.pm_gen};
+                const dlr::DevP2 mg{pm_view(c, b), batch_view(c, b), c->resid, t.pm_cnt, t.pm_gen, c->d_err, c->fault};
                 const hipError_t e = dlr::launch_grad_lds_pm(pcsc_view(c, b), c->D, B, c->resid, c->w, lr, C,
                                                              pm_view(c, nx), t.pm_p, c->stream, &mg);
                 if (e == hipSuccess) {
@@ -1895,7 +1935,7 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
         // the hot pairs: their chains continue band after band on their own
         // stream, beside the next band's margin and the other columns
         if (e == hipSuccess && hot) e = hipStreamWaitEvent(c->hstream, c->ev_band[(size_t)k], 0);
-        if (e == hipSuccess && hot) e = dlr::launch_band_hot(dv, t.bhw + bd.hw, bd.nhot, c->resid, t.gacc, c->hstream);
+        if (e == hipSuccess && hot) e = dlr::launch_band_hot(dv, t.bhw + bd.hw, bd.nhot, c->resid, t.gacc, c->hstream, c->d_err, c->fault);
     }
     if (e == hipSuccess) e = hipEventRecord(c->ev_bdone, c->gstream);
     if (e == hipSuccess && hot) e = hipEventRecord(c->ev_hdone, c->hstream);
@@ -1945,6 +1985,9 @@ int create_ctx(int device, int rank, int world, int64_t D, dlr::Comm *comm, dlr_
     if ((rc = dev_alloc(c.get(), (void **)&c->correct, 64))) return rc;
     HIPC(c.get(), hipHostMalloc((void **)&c->h_correct, 64, hipHostMallocDefault));
     HIPC(c.get(), hipHostMalloc((void **)&c->h_ll, 64, hipHostMallocDefault));
+    HIPC(c.get(), hipHostMalloc((void **)&c->h_err, dlr::kErrWords * 4, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPC(c.get(), hipHostGetDevicePointer((void **)&c->d_err, c->h_err, 0));
+    clear_device_errors(c.get());
     // Gradient + receive buffers serve both the exchange and the
     // host-exchange (worker/server) entry points.
     if ((rc = dev_alloc(c.get(), (void **)&c->g, (size_t)c->Dpad * 4))) return rc;
@@ -2029,6 +2072,7 @@ void dlr_destroy(dlr_ctx *ctx) {
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->h_correct) (void)hipHostFree(ctx->h_correct);
     if (ctx->h_ll) (void)hipHostFree(ctx->h_ll);
+    if (ctx->h_err) (void)hipHostFree(ctx->h_err);
     for (int k = 0; k < 2; ++k) {
         if (ctx->ev_ready[k]) (void)hipEventDestroy(ctx->ev_ready[k]);
         if (ctx->ev_free[k]) (void)hipEventDestroy(ctx->ev_free[k]);
@@ -2059,7 +2103,7 @@ int dlr_set_weights(dlr_ctx *c, const float *w, int64_t D) {
     }
     c->pm_ready = -1;
     HIPC(c, hipMemcpyAsync(c->w, w, (size_t)D * 4, hipMemcpyHostToDevice, c->stream));
-    HIPC(c, hipStreamSynchronize(c->stream));
+    if (int rc_ = wait_stream(c, c->stream, __func__)) return rc_;
     return DLR_OK;
 }
 
@@ -2068,11 +2112,13 @@ int dlr_get_weights(dlr_ctx *c, float *w, int64_t D) {
     HIPC(c, hipSetDevice(c->device));
     if (c->perm.empty()) {
         HIPC(c, hipMemcpyAsync(w, c->w, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
-        return wait_stream(c, c->stream, "dlr_get_weights");
+        if (int rc = wait_stream(c, c->stream, "dlr_get_weights")) return rc;
+        return check_device(c, "dlr_get_weights");
     }
     std::vector<float> tmp((size_t)D);
     HIPC(c, hipMemcpyAsync(tmp.data(), c->w, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
     if (int rc = wait_stream(c, c->stream, "dlr_get_weights")) return rc;
+    if (int rc = check_device(c, "dlr_get_weights")) return rc;
     for (int64_t j = 0; j < D; ++j) w[j] = tmp[(size_t)c->perm[(size_t)j]];
     return DLR_OK;
 }
@@ -2154,7 +2200,9 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         int rc = coll_agree_load(c, "dlr_load_train", msg.empty() ? DLR_OK : DLR_E_ARG, msg, nb);
         if (rc || (rc = coll_agree_order(c, "dlr_load_train"))) return rc;
     }
-    HIPC(c, hipStreamSynchronize(c->stream));
+    if (int rc_ = wait_stream(c, c->stream, __func__)) return rc_;
+    if (c->xstream)  // the pieced all-gather's stream carries collectives too
+        if (int rc_ = wait_stream(c, c->xstream, __func__)) return rc_;
     free_train(c);
     TrainShard &t = c->train;
     t.xpieces = c->xpieces;
@@ -2513,6 +2561,10 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 // launch, k_pm_margin)
                 const char *pg = getenv("DLR_PM_MG");
                 t.pm_mg = t.pm_fused && !t.rt && !(pg && strcmp(pg, "0") == 0);
+                // ... only if every batch's launch is resident at once
+                // (grad_lds_mg_ok; otherwise pass 2 runs in k_pm_margin)
+                for (int64_t b = 0; t.pm_mg && b < nb; ++b)
+                    t.pm_mg = dlr::grad_lds_mg_ok(pm_view(c, b), c->D, t.plan[(size_t)b].rows, t.phases);
                 if (t.pm_mg) {
                     const size_t cb = (size_t)dlr::DevP2::kMgCntWords * 4;
                     if ((rc = dev_alloc(c, (void **)&t.pm_cnt, cb))) return rc;
@@ -2791,7 +2843,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         c->resid = nullptr;
         if ((rc = dev_alloc(c, (void **)&c->resid, (size_t)resid_need * 4))) return rc;
         HIPC(c, hipMemsetAsync(c->resid, 0, (size_t)resid_need * 4, c->stream));
-        HIPC(c, hipStreamSynchronize(c->stream));
+        if (int rc_ = wait_stream(c, c->stream, __func__)) return rc_;
         c->resid_cap = resid_need;
     }
     if (t.sparse_stream && (rc = coalesce_stream(c, nthreads))) return rc;
@@ -2809,7 +2861,7 @@ int dlr_load_test(dlr_ctx *c, const dlr_dataset *ds) {
     if (!c || !ds) return fail(c, DLR_E_ARG, "dlr_load_test: bad argument");
     if (ds->D != c->D) return fail(c, DLR_E_ARG, "dlr_load_test: dataset D != context D");
     HIPC(c, hipSetDevice(c->device));
-    HIPC(c, hipStreamSynchronize(c->stream));
+    if (int rc_ = wait_stream(c, c->stream, __func__)) return rc_;
     free_test(c);
     TestShard &t = c->test;
     t.n_rows = ds->n_rows;
@@ -2854,7 +2906,9 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
         int rc = coll_agree_load(c, "dlr_load_train_dense", msg.empty() ? DLR_OK : DLR_E_ARG, msg, nb);
         if (rc || (rc = coll_agree_order(c, "dlr_load_train_dense"))) return rc;
     }
-    HIPC(c, hipStreamSynchronize(c->stream));
+    if (int rc_ = wait_stream(c, c->stream, __func__)) return rc_;
+    if (c->xstream)  // the pieced all-gather's stream carries collectives too
+        if (int rc_ = wait_stream(c, c->xstream, __func__)) return rc_;
     free_train(c);
     free_touched_bufs(c);
     int rc;
@@ -2974,7 +3028,7 @@ int dlr_load_test_dense(dlr_ctx *c, const dlr_dense *ds) {
                     "dlr_load_test_dense: the loaded sparse training shard uses relabeled columns (DLR_RELABEL=0 "
                     "keeps the original order)");
     HIPC(c, hipSetDevice(c->device));
-    HIPC(c, hipStreamSynchronize(c->stream));
+    if (int rc_ = wait_stream(c, c->stream, __func__)) return rc_;
     free_test(c);
     TestShard &t = c->test;
     t.dense = true;
@@ -3000,6 +3054,7 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
     if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_step: no training shard loaded");
     if (b < 0 || b >= (int64_t)c->train.plan.size()) return fail(c, DLR_E_ARG, "dlr_train_step: batch out of range");
     if (mode < 0 || mode > 2) return fail(c, DLR_E_ARG, "dlr_train_step: bad mode");
+    if (int rc = check_device(c, "dlr_train_step")) return rc;  // what earlier steps recorded
     HIPC(c, hipSetDevice(c->device));
     struct {
         int64_t rows;
@@ -3140,12 +3195,13 @@ int dlr_worker_gradient(dlr_ctx *c, int64_t b, float C, float *grad_out, int64_t
     if (c->train.sparse_stream) HIPC(c, sparse_batch_done(c, b));
     if (c->perm.empty()) {
         HIPC(c, hipMemcpyAsync(grad_out, c->g, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
-        HIPC(c, hipStreamSynchronize(c->stream));
-        return DLR_OK;
+        if (int rc_ = wait_stream(c, c->stream, __func__)) return rc_;
+        return check_device(c, "dlr_worker_gradient");
     }
     std::vector<float> tmp((size_t)D);
     HIPC(c, hipMemcpyAsync(tmp.data(), c->g, (size_t)D * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipStreamSynchronize(c->stream));
+    if (int rc_ = wait_stream(c, c->stream, __func__)) return rc_;
+    if (int rc = check_device(c, "dlr_worker_gradient")) return rc;
     for (int64_t j = 0; j < D; ++j) grad_out[j] = tmp[(size_t)c->perm[(size_t)j]];
     return DLR_OK;
 }
@@ -3190,6 +3246,7 @@ int dlr_predict(dlr_ctx *c, int64_t *correct, int64_t *n_rows, double *logloss) 
     HIPC(c, hipMemcpyAsync(c->h_correct, c->correct, 8, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipMemcpyAsync(c->h_ll, c->ll, 8, hipMemcpyDeviceToHost, c->stream));
     if (int rc = wait_stream(c, c->stream, "dlr_predict")) return rc;
+    if (int rc = check_device(c, "dlr_predict")) return rc;
     if (correct) *correct = (int64_t)*c->h_correct;
     if (n_rows) *n_rows = t.n_rows;
     if (logloss) *logloss = *c->h_ll;
@@ -3201,7 +3258,7 @@ int dlr_sync(dlr_ctx *c) {
     HIPC(c, hipSetDevice(c->device));
     if (int rc = wait_stream(c, c->stream, "dlr_sync")) return rc;
     if (c->cstream) HIPC(c, hipStreamSynchronize(c->cstream));  // a streamed shard's batch copies
-    return DLR_OK;
+    return check_device(c, "dlr_sync");
 }
 
 int dlr_timing(dlr_ctx *c, int enable) {
@@ -3280,6 +3337,13 @@ int dlr_stage_time(dlr_ctx *c, int stage, int64_t first, int64_t count, float lr
     c->pm_ready = -1;  // the stages ran without their partners
     if (e != hipSuccess) return fail(c, DLR_E_HIP, std::string("dlr_stage_time: ") + hipGetErrorString(e));
     if (avg_ms) *avg_ms = (double)ms / (double)count;
+    return check_device(c, "dlr_stage_time");
+}
+
+int dlr_set_fault(dlr_ctx *c, int fault) {
+    if (!c || fault < dlr::kFaultNone || fault > dlr::kFaultHotRing)
+        return fail(c, DLR_E_ARG, "dlr_set_fault: bad fault");
+    c->fault = fault;
     return DLR_OK;
 }
 
@@ -3333,7 +3397,7 @@ int dlr_train_layout(dlr_ctx *c) {
 int dlr_set_exchange_overlap(dlr_ctx *c, int on) {
     if (!c) return DLR_E_ARG;
     HIPC(c, hipSetDevice(c->device));
-    HIPC(c, hipStreamSynchronize(c->stream));
+    if (int rc_ = wait_stream(c, c->stream, __func__)) return rc_;
     c->xoverlap = on != 0;
     c->pm_ready = -1;  // products formed under the other setting are not assumed
     // with a shard loaded the ranks re-agree now (collective): every rank's

@@ -115,6 +115,32 @@ struct DevLPhase {
     uint32_t npart;  // partials; part[npart, npart + 64) is a write sink for idle lanes
 };
 
+// In-launch hand-off errors.  The one-launch kernels (k_grad_lds MG,
+// k_dense_ref, k_band_hot) hand data between workgroups or waves through
+// counters; every wait is bounded (dlr_kernels.hip Spin).  A wait that runs
+// out sets word [kind] of the context's error words (host-mapped, zero when
+// healthy), which the engine turns into DLR_E_DEVICE.
+enum DevErr {
+    kErrMgPublish = 0,  // k_grad_lds MG: a phase's margin blocks were never all published
+    kErrRefSlot = 1,    // k_dense_ref: a chain slot's margin units were never published
+    kErrRefLimit = 2,   // k_dense_ref: the chains' limit never reached a margin unit
+    kErrRefLds = 3,     // k_dense_ref: a hand-off between the waves of a workgroup
+    kErrHotLds = 4,     // k_band_hot: a hand-off between the waves of a workgroup
+    kErrWords = 8
+};
+// Test-only fault injection (dlr_set_fault): a producer that never comes.
+enum DevFault {
+    kFaultNone = 0,
+    kFaultMgPublish = 1,   // k_grad_lds MG: margin block 0 never adds to its counter
+    kFaultRefPublish = 2,  // k_dense_ref: margin unit 0 never adds to its slot's counter
+    kFaultHotRing = 3      // k_band_hot: the product waves never post a chunk
+};
+
+// The largest grid of `threads`-thread workgroups with `lds` bytes of
+// dynamic LDS that is resident at once on the current device (occupancy
+// per CU x CUs) for kernel `fn`; 0 if the runtime cannot say.
+int resident_grid(const void *fn, int threads, size_t lds);
+
 // PRODUCT MARGIN of one batch (dlr_kernels.hip "Product margin"; LDS-layout
 // batches).  The batch's rows fall in blocks of kPmRows; its columns in
 // slices of kPmSlice (the columns of one k_grad_lds workgroup).  Every
@@ -165,6 +191,8 @@ struct DevP2 {
     uint32_t *cnt;  // kMgCntWords words
     static constexpr int64_t kMgCntWords = 2 * 64 * 8 * 32;
     uint32_t gen;
+    uint32_t *err = nullptr;  // DevErr words
+    int fault = 0;            // kFaultMgPublish: block 0 is never published (tests)
 };
 
 // ROW-ROUND gradient (RT) of a product-margin batch (dlr_kernels.hip
@@ -209,6 +237,8 @@ struct DevRefSync {
     uint32_t seq;
     int lead;         // slots the margins may run ahead of the chains (0: no limit)
     int mgrid;        // margin workgroups (set by launch_dense_ref)
+    uint32_t *err = nullptr;  // DevErr words
+    int fault = 0;            // kFaultRefPublish (tests)
 };
 
 // Batch size of every rank (the L2 term of rank r's push is
@@ -247,7 +277,7 @@ hipError_t launch_grad_band(const DevBand &bd, const float *resid, float *gacc, 
 // ids): one workgroup each, beside launch_grad_band(..., skip_hot = true) of
 // the same band (dlr_kernels.hip k_band_hot; bitwise the same sums).
 hipError_t launch_band_hot(const DevBand &bd, const uint32_t *hw, int64_t nhot, const float *resid, float *gacc,
-                           hipStream_t s);
+                           hipStream_t s, uint32_t *err = nullptr, int fault = 0);
 // Long columns in row phases: piece partials part[slot], then the fixed
 // combine of each column's partials [cseg[l], cseg[l+1]) into graw[j].
 hipError_t launch_long_phase(const DevLPhase &lp, const uint32_t *cols, const uint32_t *cseg, int64_t ncols,

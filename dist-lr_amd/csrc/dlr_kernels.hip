@@ -89,6 +89,40 @@ __device__ __forceinline__ void lds_wait4(float &a, float &b, float &c, float &d
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
 }
 
+// Bounded waits of the in-launch hand-offs (dlr_kernels.h DevErr).  The
+// reference's worker never computes on data it has not received
+// (lr.cc:122, 131: kv_->Wait); a wait here that has seen no producer for
+// kSpinTicks of the 100 MHz real-time clock records its kind in the
+// context's error word -- the host then fails dlr_sync / the next step
+// with DLR_E_DEVICE instead of returning weights -- and marks the waiting
+// lane dead: its later waits in the launch return at once, so a launch
+// whose producer never comes drains after one timeout per wave, not one per
+// wait.  The clock is read every 64 polls from the 64th on: a wait whose
+// producer comes within 64 polls (nearly every wait of a healthy launch)
+// never reads it.
+constexpr uint64_t kSpinTicks = 25000000ull;  // 250 ms
+struct Spin {
+    uint32_t *err;  // the error words (host-mapped; null: none)
+    int kind;
+    bool dead = false;
+    uint64_t t0 = 0;
+    __device__ explicit Spin(uint32_t *e, int k) : err(e), kind(k) {}
+    // poll k (from 0) of a wait: false = stop polling (dead, or timed out)
+    __device__ __forceinline__ bool more(int k) {
+        if (dead) return false;
+        if ((k & 63) || k == 0) return true;
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        if (k == 64) {
+            t0 = t;
+            return true;
+        }
+        if (t - t0 < kSpinTicks) return true;
+        dead = true;
+        if (err) __hip_atomic_store(err + kind, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return false;
+    }
+};
+
 template <typename T>
 struct Vec4;
 template <>
@@ -1198,7 +1232,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every residual of the block stored
             // sub-counter k2 % 8 of the phase (each on a line of its own:
             // the adds and the polls spread over 8 lines)
-            if (lane == 0)
+            if (lane == 0 && !(p2.fault == kFaultMgPublish && k2 == 0))
                 __hip_atomic_fetch_add(
                     p2.cnt + (((p2.gen & 1) * 64 + (k2 * kPmRows) / R) * kMgSub + (k2 % kMgSub)) * 32, 1u,
                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1212,7 +1246,9 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
         if (DLR_MG_HOLD) lds_barrier();
     }
     // wave 0 waits until every block of phase p is published (the caller's
-    // barrier then holds the other waves' fills)
+    // barrier then holds the other waves' fills); a wait that runs out is
+    // reported (Spin)
+    Spin spin(MG ? p2.err : nullptr, kErrMgPublish);
     auto mg_wait = [&](int p) {
         if constexpr (MG) {
             if (wv == 0) {
@@ -1222,7 +1258,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
                     __builtin_amdgcn_make_buffer_rsrc(p2.cnt, 0, 0x7FFFFFFF, 0x00020000);
                 // lane s < 8 reads sub-counter s
                 const int off = (int)(((((p2.gen & 1) * 64 + p) * kMgSub + (lane & (kMgSub - 1))) * 32) * 4);
-                for (int k = 0; k < (1 << 20); ++k) {
+                for (int k = 0; spin.more(k); ++k) {
                     const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(crs, off, 0, 16);
                     uint32_t n = 0;
 #pragma unroll
@@ -1731,9 +1767,9 @@ __global__ __launch_bounds__(kWaves *kWave) void k_grad_band(DevBand bd, const R
         if (s0 + lane + (int64_t)k * kWave < sl) __builtin_nontemporal_store(acc[k], gacc + j[k]);
 }
 
-// Bounded polls: a hand-off whose producer never comes ends after kCtlSpin
-// polls (wrong sums instead of a hung GPU).
-constexpr int kCtlSpin = 1 << 22;
+// Bounded polls (Spin): a hand-off whose producer never comes ends after
+// kSpinTicks and is reported -- the host fails the step -- instead of
+// hanging the GPU.
 // LDS hand-off words between the waves of one half (no s_barrier: the two
 // halves run at their own pace).  A producer's data writes (or, for LDS-DMA,
 // its covering vmcnt wait) complete before the word is written; a consumer
@@ -1747,8 +1783,8 @@ __device__ __forceinline__ void ctl_write(uint32_t *p, uint32_t v) {
     asm volatile("s_waitcnt lgkmcnt(0)\n ds_write_b32 %0, %1\n s_waitcnt lgkmcnt(0)" ::"v"(lds_addr(p)), "v"(v)
                  : "memory");
 }
-__device__ __forceinline__ void ctl_wait_ge(const uint32_t *p, uint32_t v) {
-    for (int k = 0; k < kCtlSpin && (int32_t)(ctl_read(p) - v) < 0; ++k) __builtin_amdgcn_s_sleep(0);
+__device__ __forceinline__ void ctl_wait_ge(const uint32_t *p, uint32_t v, Spin &sp) {
+    for (int k = 0; (int32_t)(ctl_read(p) - v) < 0 && sp.more(k); ++k) __builtin_amdgcn_s_sleep(0);
 }
 // The per-stage / per-slot hand-offs: a plain ds_write (a wave's LDS
 // operations complete in order, so the data it stored before -- or the
@@ -1758,9 +1794,9 @@ __device__ __forceinline__ void ctl_wait_ge(const uint32_t *p, uint32_t v) {
 __device__ __forceinline__ void ctl_post(uint32_t *p, uint32_t v) {
     asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
 }
-__device__ __forceinline__ uint32_t ctl_poll(const uint32_t *p, uint32_t v) {
+__device__ __forceinline__ uint32_t ctl_poll(const uint32_t *p, uint32_t v, Spin &sp) {
     uint32_t x = ctl_read(p);
-    for (int k = 0; k < kCtlSpin && (int32_t)(x - v) < 0; ++k) {
+    for (int k = 0; (int32_t)(x - v) < 0 && sp.more(k); ++k) {
         __builtin_amdgcn_s_sleep(0);
         x = ctl_read(p);
     }
@@ -1780,9 +1816,9 @@ __device__ __forceinline__ uint32_t ctl_read_min(const uint32_t *p) {
     }
 }
 template <int N>
-__device__ __forceinline__ uint32_t ctl_poll_min(const uint32_t *p, uint32_t v) {
+__device__ __forceinline__ uint32_t ctl_poll_min(const uint32_t *p, uint32_t v, Spin &sp) {
     uint32_t x = ctl_read_min<N>(p);
-    for (int k = 0; k < kCtlSpin && (int32_t)(x - v) < 0; ++k) {
+    for (int k = 0; (int32_t)(x - v) < 0 && sp.more(k); ++k) {
         __builtin_amdgcn_s_sleep(0);
         x = ctl_read_min<N>(p);
     }
@@ -1814,12 +1850,13 @@ constexpr size_t kHotLds = 150 * 1024;  // requested: the workgroup holds its CU
 template <typename RowT, bool UNIT>
 __global__ __launch_bounds__(256) void k_band_hot(DevBand bd, const uint32_t *__restrict__ hw,
                                                   const RowT *__restrict__ brow, const float *__restrict__ resid,
-                                                  float *__restrict__ gacc) {
+                                                  float *__restrict__ gacc, uint32_t *err, int fault) {
     extern __shared__ __attribute__((aligned(16))) float hsm[];
     float *ring = hsm;                                                    // [kHotRing][kHotChunk]
     uint32_t *ctl = reinterpret_cast<uint32_t *>(hsm + kHotRing * kHotChunk);  // helper 1, helper 2, chain
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    Spin spin(err, kErrHotLds);
     if (threadIdx.x < 4) ctl[threadIdx.x] = 0u;
     __syncthreads();
     const uint32_t wid = hw[blockIdx.x];
@@ -1850,7 +1887,7 @@ __global__ __launch_bounds__(256) void k_band_hot(DevBand bd, const uint32_t *__
         const int64_t nfull = n / kHotChunk;
         v4f da[8], db[8];
         if (nfull > 0) {
-            pk = ctl_poll_min<2>(ctl, 1u);
+            pk = ctl_poll_min<2>(ctl, 1u, spin);
             rd(da, ring);
         }
         for (int64_t c = 0; c < nfull; ++c) {
@@ -1865,14 +1902,14 @@ __global__ __launch_bounds__(256) void k_band_hot(DevBand bd, const uint32_t *__
             rd(db, q + kHotChunk - 32);
             add(da);
             const bool more = c + 1 < nfull;
-            if (more && (int32_t)(pk - ((uint32_t)c + 2)) < 0) pk = ctl_poll_min<2>(ctl, (uint32_t)c + 2);
+            if (more && (int32_t)(pk - ((uint32_t)c + 2)) < 0) pk = ctl_poll_min<2>(ctl, (uint32_t)c + 2, spin);
             rd(da, more ? ring + ((c + 1) % kHotRing) * kHotChunk : q);  // (after the last: a re-read, unused)
             add(db);
             if (lane == 0) ctl_post(ctl + 2, (uint32_t)c + 1);
         }
         if (nfull < nch) {
             const int64_t c = nfull;
-            if ((int32_t)(pk - ((uint32_t)c + 1)) < 0) pk = ctl_poll_min<2>(ctl, (uint32_t)c + 1);
+            if ((int32_t)(pk - ((uint32_t)c + 1)) < 0) pk = ctl_poll_min<2>(ctl, (uint32_t)c + 1, spin);
             const float *q = ring + (c % kHotRing) * kHotChunk;
             const int cnt = (int)(n - c * kHotChunk);
             for (int k = 0; k < cnt; ++k) acc = acc + q[k];
@@ -1916,11 +1953,11 @@ __global__ __launch_bounds__(256) void k_band_hot(DevBand bd, const uint32_t *__
                 g[d % GA][1] = resid[rw[(d + GA) % RA][1]];
                 load_rows(c + RA, d);
                 if (c >= kHotRing && (int32_t)(ck - (uint32_t)(c - kHotRing + 1)) < 0)
-                    ck = ctl_poll(ctl + 2, (uint32_t)(c - kHotRing + 1));
+                    ck = ctl_poll(ctl + 2, (uint32_t)(c - kHotRing + 1), spin);
                 float *q = ring + (c % kHotRing) * kHotChunk;
                 q[hl] = p0;
                 q[128 + hl] = p1;
-                if (lane == 0) ctl_post(mine, (uint32_t)c + 1);
+                if (lane == 0 && fault != kFaultHotRing) ctl_post(mine, (uint32_t)c + 1);
             }
         }
     }
@@ -2938,9 +2975,11 @@ __global__ __launch_bounds__(256) void k_dense_combine(const float *__restrict__
 // chain epilogue, after its last slot: by then every unit -- every read of
 // w -- is done.  Counters and the queue are monotonic over launches
 // (sy.seq), so nothing is reset between steps.  Every wait is bounded
-// (kRefSpin polls): a launch whose producers never come runs to the end with
-// wrong sums instead of hanging the GPU.  X is read once from HBM (the
-// margins) and once from the Infinity Cache (the chains).
+// (Spin): a launch whose producers never come drains and reports the wait
+// that ran out (DevErr) instead of hanging the GPU, and the host fails the
+// step.  The grid never exceeds what is resident at once (dense_ref_ok).
+// X is read once from HBM (the margins) and once from the Infinity Cache
+// (the chains).
 constexpr int kRefCols = 16;      // columns per chain half
 constexpr int kRefSlot = 256;     // batch rows per chain slot
 constexpr int kRefUnit = 64;      // batch rows per margin unit (one lane each) = rows of a tile
@@ -2952,7 +2991,6 @@ constexpr int kRefPad = kRefSlot + 4;
 constexpr int kRefHD = 6;         // chain slots whose rows a helper has in flight
 constexpr int kRefThreads = 512;
 constexpr uint32_t kRefNone = 0xFFFFFFFFu;
-constexpr int kRefSpin = kCtlSpin;
 // LDS (floats): chain products [2][16][kRefPad], residuals [2][256], the
 // margin ring [7][64 x 64 + 256 (the stage's 64 weights, in a 1 KiB area)],
 // then 16 words of hand-off counters / unit ids
@@ -3085,6 +3123,7 @@ __device__ __forceinline__ void ref_chain_half(const DevDense &dd, int64_t first
         cg = ((k >> 1) << 4) | ((blockIdx.x & 7) << 1) | (k & 1);
     }
     const int64_t c0 = (int64_t)cg * kRefCols;
+    Spin spin(sy.err, kErrRefLds);
     // helpers: lane hl in [0, 128); its load v (0..7) is chunk v >> 1 of
     // the stripe for slot row r = 128 (v & 1) + hl -- a wave reads 64
     // consecutive rows of one chunk (1 KiB of a tile)
@@ -3141,7 +3180,7 @@ __device__ __forceinline__ void ref_chain_half(const DevDense &dd, int64_t first
         v4f da[8], db[8];
         {
             DLR_TACC_BEGIN();
-            hk = ctl_poll_min<2>(ctl + kCtlH0, 1u);
+            hk = ctl_poll_min<2>(ctl + kCtlH0, 1u, spin);
             DLR_TACC_LAP(t_cw);
         }
         rd(da, sp_of(0));
@@ -3160,7 +3199,7 @@ __device__ __forceinline__ void ref_chain_half(const DevDense &dd, int64_t first
             const bool more = t + 1 < nslot;
             if (more && (int32_t)(hk - ((uint32_t)t + 2)) < 0) {
                 DLR_TACC_LAP(t_ca);
-                hk = ctl_poll_min<2>(ctl + kCtlH0, (uint32_t)t + 2);
+                hk = ctl_poll_min<2>(ctl + kCtlH0, (uint32_t)t + 2, spin);
                 DLR_TACC_LAP(t_cw);
             }
             rd(da, more ? sp_of(t + 1) : sp);  // (after the last slot: a re-read, unused)
@@ -3207,9 +3246,9 @@ __device__ __forceinline__ void ref_chain_half(const DevDense &dd, int64_t first
                 const int64_t t = t0 + d;
                 if (t < nslot) {
                     DLR_TACC_BEGIN();
-                    if ((int32_t)(rk - ((uint32_t)t + 1)) < 0) rk = ctl_poll(ctl + kCtlR, (uint32_t)t + 1);
+                    if ((int32_t)(rk - ((uint32_t)t + 1)) < 0) rk = ctl_poll(ctl + kCtlR, (uint32_t)t + 1, spin);
                     DLR_TACC_LAP(t_hr);
-                    if (t >= 2 && (int32_t)(ck - ((uint32_t)t - 1)) < 0) ck = ctl_poll(ctl + kCtlChain, (uint32_t)t - 1);
+                    if (t >= 2 && (int32_t)(ck - ((uint32_t)t - 1)) < 0) ck = ctl_poll(ctl + kCtlChain, (uint32_t)t - 1, spin);
                     DLR_TACC_LAP(t_hc);
                     transform(t, x[d]);
                     if (lane == 0) ctl_post(mine, (uint32_t)t + 1);
@@ -3246,13 +3285,14 @@ __device__ __forceinline__ void ref_chain_half(const DevDense &dd, int64_t first
         if (lane == 0) __builtin_amdgcn_raw_buffer_store_b32(qbase + (uint32_t)lim, lrs, 0, 0, 16);
     };
     int64_t ready = -1;
+    Spin gspin(sy.err, kErrRefSlot);
     DLR_TACC_DECL(t_rp);
     DLR_TACC_DECL(t_rh);
     auto poll_from = [&](int64_t t0) {
         const uint32_t want0 = slot_target(t0);
-        for (int k = 0; k < kRefSpin; ++k) {
+        for (int k = 0;; ++k) {
             const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(crs, (int)(t0 * 4), 0, 16);
-            if (v >= want0) break;
+            if (v >= want0 || !gspin.more(k)) break;
             __builtin_amdgcn_s_sleep(32);
         }
         const int64_t sl = min<int64_t>(t0 + lane, nslot - 1);
@@ -3277,7 +3317,7 @@ __device__ __forceinline__ void ref_chain_half(const DevDense &dd, int64_t first
     uint32_t hk = 0;  // slots both helpers are known to have stored
     auto r_store = [&](int64_t t, const v4f &rv) {
         DLR_TACC_BEGIN();
-        if (t >= 2 && (int32_t)(hk - ((uint32_t)t - 1)) < 0) hk = ctl_poll_min<2>(ctl + kCtlH0, (uint32_t)t - 1);
+        if (t >= 2 && (int32_t)(hk - ((uint32_t)t - 1)) < 0) hk = ctl_poll_min<2>(ctl + kCtlH0, (uint32_t)t - 1, spin);
         DLR_TACC_LAP(t_rh);
         *reinterpret_cast<v4f *>(s_r + (t & 1) * kRefSlot + 4 * lane) = rv;
         if (lane == 0) ctl_post(ctl + kCtlR, (uint32_t)t + 1);
@@ -3314,6 +3354,7 @@ __device__ __forceinline__ void ref_margin_half(const DevDense &dd, int64_t firs
     uint32_t *s_unit = ctl + kCtlUnit;  // [4]
     const int spu = (int)(D / kRefStage);  // stages per unit (>= 8)
     const uint32_t base = ref_base(sy, nunits);
+    Spin spin(sy.err, kErrRefLds);
     if (mw < 3) {
         // loaders: stage g of this half's unit sequence into ring[g % 7]:
         // chunk q of the unit's 64 rows per LDS-DMA instruction (1 KiB; lane
@@ -3328,9 +3369,9 @@ __device__ __forceinline__ void ref_margin_half(const DevDense &dd, int64_t firs
         uint32_t uc = kRefNone;
         auto issue = [&](int k, int sg, int ri, int g) {
             if (g >= kRefRing && (int32_t)(compk - (uint32_t)(g - kRefRing + 1)) < 0)
-                compk = ctl_poll(ctl + kCtlComp, (uint32_t)(g - kRefRing + 1));
+                compk = ctl_poll(ctl + kCtlComp, (uint32_t)(g - kRefRing + 1), spin);
             if (k != kc) {
-                ctl_wait_ge(ctl + kCtlIds, (uint32_t)k + 1);
+                ctl_wait_ge(ctl + kCtlIds, (uint32_t)k + 1, spin);
                 uc = ctl_read(s_unit + (k & 3));
                 kc = k;
             }
@@ -3369,7 +3410,7 @@ __device__ __forceinline__ void ref_margin_half(const DevDense &dd, int64_t firs
         DLR_TACC_DECL(t_land);
         for (int g = 0, k = 0, sg = 0;; ++g) {
             if (sg == 0) {  // a new unit: stop at the end of the sequence
-                ctl_wait_ge(ctl + kCtlIds, (uint32_t)k + 1);
+                ctl_wait_ge(ctl + kCtlIds, (uint32_t)k + 1, spin);
                 if (ctl_read(s_unit + (k & 3)) == kRefNone) break;
             }
             DLR_TACC_BEGIN();
@@ -3404,6 +3445,7 @@ __device__ __forceinline__ void ref_margin_half(const DevDense &dd, int64_t firs
     // that waits for the result at once) leaves it alone: the result is
     // used only at the end of the unit.
     bool claiming = true;
+    Spin lspin(sy.err, kErrRefLimit);
     int vz;
     asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
     auto claim_issue = [&]() -> uint32_t {
@@ -3441,9 +3483,9 @@ __device__ __forceinline__ void ref_margin_half(const DevDense &dd, int64_t firs
             // within `lead` slots of it (every unit this half still holds is
             // later: nothing a chain waits for is held here)
             if (sy.lead > 0 && lane == 0)
-                for (int s = 0; s < kRefSpin / 64; ++s) {
+                for (int s = 0;; ++s) {
                     const uint32_t lim = __builtin_amdgcn_raw_buffer_load_b32(lrs, 0, 0, 16);
-                    if ((int32_t)(lim - (base + u)) > 0) break;
+                    if ((int32_t)(lim - (base + u)) > 0 || !lspin.more(s)) break;
                     __builtin_amdgcn_s_sleep(16);
                 }
             DLR_STAMP64M(22 + k, lane == 0 && k < 20);
@@ -3455,7 +3497,7 @@ __device__ __forceinline__ void ref_margin_half(const DevDense &dd, int64_t firs
         }
         // stage g landed: every loader's pieces of it
         DLR_TACC_BEGIN();
-        if ((int32_t)(lk - ((uint32_t)g + 1)) < 0) lk = ctl_poll_min<3>(ctl + kCtlL0, (uint32_t)g + 1);
+        if ((int32_t)(lk - ((uint32_t)g + 1)) < 0) lk = ctl_poll_min<3>(ctl + kCtlL0, (uint32_t)g + 1, spin);
         DLR_TACC_LAP(t_wait);
         if (!(DLR_ABL & 64)) {
             // the stage's 64 columns in order, 4 sets of 16: set S's adds
@@ -3483,8 +3525,9 @@ __device__ __forceinline__ void ref_margin_half(const DevDense &dd, int64_t firs
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every residual of the unit stored
             if (lane == 0) {
-                __hip_atomic_fetch_add(sy.slot_cnt + (u / (kRefSlot / kRefUnit)), 1u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
+                if (!(sy.fault == kFaultRefPublish && u == 0))
+                    __hip_atomic_fetch_add(sy.slot_cnt + (u / (kRefSlot / kRefUnit)), 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
                 // the next-but-one unit, before the stage count that lets the
                 // loaders reach it
                 ctl_write(s_unit + ((k + 2) & 3), have_pend ? claim_finish(pend) : kRefNone);
@@ -3862,10 +3905,72 @@ hipError_t launch_pm_margin(const DevPm &pm, const DevBatch &bt, const float *p,
     return hipGetLastError();
 }
 
+namespace {
+// The one-launch step's kernel for a fill (a workgroup of every grid
+// size it may take must fit beside the others: they wait for each other).
+const void *grad_lds_mg_fn(int fill) {
+    switch (fill) {
+        case 1: return reinterpret_cast<const void *>(&k_grad_lds<1, true, false, true, true>);
+        case 2: return reinterpret_cast<const void *>(&k_grad_lds<2, true, false, true, true>);
+        case 4: return reinterpret_cast<const void *>(&k_grad_lds<4, true, false, true, true>);
+        case 8: return reinterpret_cast<const void *>(&k_grad_lds<8, true, false, true, true>);
+        default: return nullptr;
+    }
+}
+size_t grad_lds_pm_lds(int fill) {
+    return std::max((size_t)fill * 4096 * 4 + (size_t)kGradWaves * kBlkPad * 4, (size_t)(kPmSlice + kPmMaxBlocks) * 4);
+}
+
+// CUs of the current device (cached per device; 0 if the runtime cannot say)
+int device_cus() {
+    static int ncu[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (!ncu[dev] && hipDeviceGetAttribute(&ncu[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        ncu[dev] = 0;
+    }
+    return ncu[dev];
+}
+
+// The MG launch's workgroups: one per slice, or (DLR_MG_EVEN) more when
+// that evens the blocks out over the CUs (C2: 1,024 blocks on 256
+// workgroups, 4 each, not 245 with up to 5); the extra workgroups only
+// sum blocks.
+int64_t grad_lds_mg_grid(int64_t nblk, int64_t grid) {
+    const int64_t even = (nblk + 3) / 4;
+    if (DLR_MG_EVEN && even > grid && even <= device_cus()) return even;
+    return grid;
+}
+}  // namespace
+
+int resident_grid(const void *fn, int threads, size_t lds) {
+    if (!fn) return 0;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return per_cu * device_cus();
+}
+
+// Whether batch b's pass 2 may run in its gradient's launch: the shape
+// fits, and every workgroup of the launch is resident at once -- each one
+// waits for blocks summed by the others, so one that is not resident
+// would leave the resident ones waiting (D = 2^21 at B =
+// 65,536 has 512 slices on 256 CUs; such batches take k_pm_margin).
 bool grad_lds_mg_ok(const DevPm &cur, int64_t D, int64_t B, int phases) {
     const int64_t grid = (D + kPmSlice - 1) / kPmSlice;
-    return D > 0 && cur.groups <= 8 && cur.nblk == (B + kPmRows - 1) / kPmRows &&
-           cur.nblk <= grid * grad_lds_fill(B) && phases >= 1 && phases <= 64;
+    const int fill = grad_lds_fill(B);
+    if (!(D > 0 && cur.groups <= 8 && cur.nblk == (B + kPmRows - 1) / kPmRows && cur.nblk <= grid * fill &&
+          phases >= 1 && phases <= 64))
+        return false;
+    static int cap[64][9] = {};  // per device and fill (cached: the check runs every step)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || fill < 1 || fill > 8) return false;
+    int &c = cap[dev][fill];
+    if (c == 0) c = resident_grid(grad_lds_mg_fn(fill), kGradWaves * kWave, grad_lds_pm_lds(fill));
+    return c > 0 && grad_lds_mg_grid(cur.nblk, grid) <= c;
 }
 
 hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const float *resid, float *w, float lr,
@@ -3877,26 +3982,13 @@ hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const flo
     if ((int64_t)grid != next.S || next.nblk > kPmMaxBlocks) return hipErrorInvalidValue;
     if (mg && (!grad_lds_mg_ok(mg->pm, D, B, pc.phases) || mg->bt.rows != B || !mg->cnt || !mg->resid))
         return hipErrorInvalidValue;
-    // MG: up to one workgroup per CU (every workgroup must be resident: the
-    // phases wait for every block), past the slices when that evens the
-    // blocks out (C2: 1,024 blocks on 256 workgroups, 4 each, not 245 with
-    // up to 5); the extra workgroups only sum blocks
-    unsigned mgrid = grid;
-    if (mg) {
-        static int ncu[64] = {};
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidValue;
-        if (!ncu[dev] && hipDeviceGetAttribute(&ncu[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return hipErrorInvalidValue;
-        const int64_t even = (mg->pm.nblk + 3) / 4;
-        if (DLR_MG_EVEN && even > (int64_t)grid && even <= ncu[dev]) mgrid = (unsigned)even;
-    }
+    // MG: every workgroup resident at once (grad_lds_mg_ok checked it)
+    const unsigned mgrid = mg ? (unsigned)grad_lds_mg_grid(mg->pm.nblk, grid) : grid;
     const dim3 blk(kGradWaves * kWave);
     const float Bf = (float)B;
     const double Bd = (double)B;
     const int fill = grad_lds_fill(B);
-    const size_t lds = std::max((size_t)fill * 4096 * 4 + (size_t)kGradWaves * kBlkPad * 4,
-                                (size_t)(kPmSlice + kPmMaxBlocks) * 4);
+    const size_t lds = grad_lds_pm_lds(fill);
 #define DLR_GLP(F)                                                                                            \
     case F:                                                                                                   \
         if (mg)                                                                                               \
@@ -4075,11 +4167,11 @@ hipError_t launch_grad_band(const DevBand &bd, const float *resid, float *gacc, 
 }
 
 hipError_t launch_band_hot(const DevBand &bd, const uint32_t *hw, int64_t nhot, const float *resid, float *gacc,
-                           hipStream_t s) {
+                           hipStream_t s, uint32_t *err, int fault) {
     if (nhot <= 0) return hipSuccess;
 #define DLR_BH(RT, U)                                                                                                \
     hipLaunchKernelGGL((k_band_hot<RT, U>), dim3((unsigned)nhot), dim3(256), kHotLds, s, bd, hw,                       \
-                       static_cast<const RT *>(bd.row), resid, gacc)
+                       static_cast<const RT *>(bd.row), resid, gacc, err, fault)
     if (bd.row16 && bd.val == nullptr)
         DLR_BH(uint16_t, true);
     else if (bd.row16)
@@ -4166,13 +4258,28 @@ hipError_t launch_dense_combine(const float *part, int64_t D, int64_t B, float *
     return hipGetLastError();
 }
 
+// K6r's workgroups hand off to each other (chain slots wait for margin
+// units, margin units for the chains' limit): the launch is at most what
+// is resident at once -- D / 16 chain halves, and the margin halves capped
+// to that capacity (dense_ref_cap, queried per device: one 512-thread
+// workgroup with kRefLds per CU).
+static int dense_ref_cap() {
+    static int cap[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (cap[dev] == 0) {
+        const void *fn = reinterpret_cast<const void *>(&k_dense_ref<true, true>);
+        cap[dev] = std::min(256, resident_grid(fn, kRefThreads, kRefLds));
+    }
+    return cap[dev];
+}
 bool dense_ref_ok(int64_t D, int64_t N, int64_t B) {
-    return D % kRefStage == 0 && D >= 512 && D / kRefCols <= 256 && B <= N && B < ((int64_t)1 << 31);
+    return D % kRefStage == 0 && D >= 512 && D / kRefCols <= dense_ref_cap() && B <= N && B < ((int64_t)1 << 31);
 }
 int64_t dense_ref_resid(int64_t B) { return (B + kRefSlot - 1) / kRefSlot * kRefSlot + 4; }
 int64_t dense_ref_sync_words(int64_t B) { return (B + kRefSlot - 1) / kRefSlot + 96; }
 int dense_ref_grid(int64_t D, int64_t B) {
-    return (int)std::max<int64_t>(D / kRefCols, std::min<int64_t>(256, (B + kRefUnit - 1) / kRefUnit));
+    return (int)std::max<int64_t>(D / kRefCols, std::min<int64_t>(dense_ref_cap(), (B + kRefUnit - 1) / kRefUnit));
 }
 
 hipError_t launch_dense_ref(const DevDense &dd, int64_t first, int64_t B, float *w, float *gout, float *resid,
@@ -4180,7 +4287,7 @@ hipError_t launch_dense_ref(const DevDense &dd, int64_t first, int64_t B, float 
     if (B <= 0) return hipSuccess;
     if (!dense_ref_ok(dd.D, dd.N, B) || first < 0 || first >= dd.N) return hipErrorInvalidValue;
     DevRefSync sy = sy_in;
-    sy.mgrid = (int)std::min<int64_t>(256, (B + kRefUnit - 1) / kRefUnit);
+    sy.mgrid = (int)std::min<int64_t>(dense_ref_cap(), (B + kRefUnit - 1) / kRefUnit);
     const unsigned grid = (unsigned)std::max<int64_t>(dd.D / kRefCols, sy.mgrid);
     const float Bf = (float)B;
     const double Bd = (double)B;

@@ -29,6 +29,9 @@ RESIDENCY_AUTO, RESIDENCY_DEVICE, RESIDENCY_STREAM = 0, 1, 2
 STAGE_MARGIN, STAGE_GRADIENT, STAGE_UPDATE = 0, 1, 2
 TRANSPORT_NONE, TRANSPORT_RCCL, TRANSPORT_LOOPBACK = 0, 1, 2
 ORDER_REFERENCE, ORDER_FAST = 0, 1
+E_DEVICE = -8  # an in-launch hand-off never came (dlr_sync)
+# test-only producer faults (dlr_set_fault)
+FAULT_NONE, FAULT_MG_PUBLISH, FAULT_REF_PUBLISH, FAULT_HOT_RING = 0, 1, 2, 3
 
 # Exported symbols, in include/distlr_amd.h order (tests check the .so
 # exports every one of them).
@@ -46,6 +49,7 @@ SYMBOLS = [
     "dlr_load_test_dense", "dlr_set_residency", "dlr_train_residency", "dlr_set_summation_order",
     "dlr_summation_order",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
+    "dlr_set_fault",
     "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_train_band_rows", "dlr_train_relabeled", "dlr_train_unit_values", "dlr_train_product_margin", "dlr_train_row_rounds",
     "dlr_set_exchange_overlap", "dlr_exchange_overlap", "dlr_set_exchange_pieces", "dlr_exchange_pieces",
     "dlr_memory_info", "dlr_stream_bytes",
@@ -156,6 +160,7 @@ _sig("dlr_worker_gradient", C.c_int, P, i64, C.c_float, P, i64)
 _sig("dlr_server_apply", C.c_int, P, P, C.c_int, i64, C.c_float, C.c_int)
 _sig("dlr_predict", C.c_int, P, C.POINTER(i64), C.POINTER(i64), C.POINTER(C.c_double))
 _sig("dlr_sync", C.c_int, P)
+_sig("dlr_set_fault", C.c_int, P, C.c_int)
 _sig("dlr_timing", C.c_int, P, C.c_int)
 _sig("dlr_kernel_time", C.c_int, P, C.c_int, C.POINTER(C.c_double), C.POINTER(i64))
 _sig("dlr_stage_time", C.c_int, P, C.c_int, i64, i64, C.c_float, C.c_float, C.POINTER(C.c_double))
@@ -550,6 +555,11 @@ class Engine:
 
     def sync(self) -> None:
         self._c(lib.dlr_sync(self._h))
+
+    def set_fault(self, fault: int) -> None:
+        """TEST ONLY: withhold one in-launch producer (FAULT_*) in the next
+        steps; they must then raise DLRError(E_DEVICE) (dlr_set_fault)."""
+        self._c(lib.dlr_set_fault(self._h, fault))
 
     def timing(self, enable: bool) -> None:
         self._c(lib.dlr_timing(self._h, 1 if enable else 0))

@@ -220,18 +220,20 @@ void LR::Train(DataIter &iter, int /*num_iter*/, int batch_size) {
     // what is left of the round): batches of bs rows from row k on, wrapping
     // to row 0, ceil((n - k) / bs) of them, as NextBatch would hand them out;
     // trained from the shard rotated by k rows.
+    // The cache is keyed on the caller's shard (kept alive in train_src) and
+    // the rotation, never on a rotated copy's address.
     const int64_t k = iter.offset();
-    int64_t nb_run = -1;  // -1: every batch of the loaded plan
-    if (k != 0) {
-        sh = rotated_shard(*sh, k);
-        nb_run = (n - k + bs - 1) / bs;
-    }
+    const int64_t nb_run = k != 0 ? (n - k + bs - 1) / bs : -1;  // -1: every batch of the loaded plan
     dlr_ctx *ctx = kv_->ctx();
-    if (kv_->train_shard != sh.get() || kv_->train_batch != batch_size) {
+    if (kv_->train_shard != sh.get() || kv_->train_rot != k || kv_->train_batch != batch_size) {
+        std::shared_ptr<Shard> load = k != 0 ? rotated_shard(*sh, k) : sh;
         int64_t nb = 0;
-        check(dlr_load_train(ctx, sh->get(), batch_size, &nb), ctx, "dlr_load_train");
+        kv_->train_shard = nullptr;  // nothing valid is resident if the load fails
+        check(dlr_load_train(ctx, load->get(), batch_size, &nb), ctx, "dlr_load_train");
         kv_->train_shard = sh.get();
-        kv_->train_keep = sh;
+        kv_->train_rot = k;
+        kv_->train_keep = load;
+        kv_->train_src = sh;
         kv_->train_batch = batch_size;
         kv_->train_batches = nb;
     }

@@ -79,12 +79,16 @@ class KVWorker {
     float learning_rate() const { return learning_rate_; }
     int mode() const;  // DLR_MODE_* from sync_mode
     // Device residency cache: the shard currently resident for training
-    // (with its batch size) and for testing.
+    // (the caller's shard, the row it starts from -- LR::Train loads a
+    // partially consumed DataIter's shard rotated by that many rows -- and
+    // the batch size) and for testing.  train_keep holds what was loaded,
+    // train_src the caller's shard (so its address is not reused while cached).
     const Shard *train_shard = nullptr;
+    int64_t train_rot = 0;
     int64_t train_batch = 0;
     int64_t train_batches = 0;
     const Shard *test_shard = nullptr;
-    std::shared_ptr<Shard> train_keep, test_keep;
+    std::shared_ptr<Shard> train_keep, train_src, test_keep;
 
    private:
     KVWorker(dlr_ctx *ctx, int rank, int world, float learning_rate, bool sync_mode);  // adopts ctx

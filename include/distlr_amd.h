@@ -34,6 +34,7 @@ extern "C" {
 #define DLR_E_RCCL (-5)     /* RCCL error                               */
 #define DLR_E_NOMEM (-6)    /* host or device allocation failed         */
 #define DLR_E_STATE (-7)    /* call out of order (e.g. no data loaded)  */
+#define DLR_E_DEVICE (-8)   /* an in-launch hand-off never came (below) */
 
 /* Server update semantics (main.cc:41-96, KVStoreDistServer::DataHandle). */
 #define DLR_MODE_SYNC_MEAN 0  /* intended sync merge: w -= fl32(lr*sum_r g_r)/W, sum in rank order */
@@ -312,8 +313,28 @@ int dlr_server_apply(dlr_ctx *ctx, const float *grads, int num_workers, int64_t 
  * Blocks until done. */
 int dlr_predict(dlr_ctx *ctx, int64_t *correct, int64_t *n_rows, double *logloss);
 
-/* Waits for all work on the context's stream. */
+/* Waits for all work on the context's stream.
+ *
+ * In-launch hand-offs.  Some kernels hand data between workgroups of one
+ * launch (the one-launch C2 step: rows summed by one CU, their residuals
+ * used by all; K6r: margins -> column chains) or between the waves of one
+ * workgroup.  Like the reference's worker, which waits until its pulled data
+ * is there (lr.cc:122, 131), a consumer never proceeds on data whose
+ * producer has not published it -- but a wait is bounded (250 ms), so a
+ * producer that never comes cannot hang the GPU: the wait records what it
+ * waited for, and dlr_sync, dlr_get_weights, dlr_predict,
+ * dlr_worker_gradient, dlr_stage_time and every later dlr_train_step return
+ * DLR_E_DEVICE (dlr_last_error names the hand-off) until the next
+ * dlr_load_train*.  Launches whose workgroups wait for each other are never
+ * larger than what the device holds at once (they fall back to separate
+ * launches), so a healthy run never sees it. */
 int dlr_sync(dlr_ctx *ctx);
+
+/* TEST ONLY: withhold one producer of the next steps' in-launch hand-offs
+ * (0 = none; 1 = the one-launch step's margin block 0 never publishes; 2 =
+ * K6r's margin unit 0 never publishes; 3 = k_band_hot's product waves never
+ * post) -- the steps must then fail with DLR_E_DEVICE. */
+int dlr_set_fault(dlr_ctx *ctx, int fault);
 
 /* Per-kernel timing with HIP events on the context's stream.  enable=1
  * starts recording (clears totals); dlr_kernel_time returns the summed
@@ -383,7 +404,9 @@ int dlr_train_unit_values(dlr_ctx *ctx);
  * 2 and pass 2 inside the step's own gradient launch (one rank, LDS-phase
  * gradient, rows of <= 64 entries: the launch sums the batch's rows first and
  * hands the residuals to the gradient's phases through device-scope counters;
- * DLR_PM_MG=0 keeps it a launch of its own).  The
+ * DLR_PM_MG=0 keeps it a launch of its own; a shard whose launch would have
+ * more workgroups than the device holds at once -- they wait for each other
+ * -- gets 2).  The
  * product margin (LDS-layout batches, >= 128 column slices of 4,096; resident
  * shards) forms every product fl32(w_j * x_ij) by column slice from LDS-staged
  * weights, then sums each row's products in column order from LDS: bitwise

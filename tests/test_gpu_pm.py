@@ -71,9 +71,15 @@ def test_pm_batch_sizes_and_wraps(pm_on, B, value_mode):
     # divide N, wrap at the epoch end, or wrap twice (B > N)
     D = 30000
     ds = dlr.Dataset.generate(1000, D, 20, value_mode=value_mode, seed=3, stream=1)
-    # the margin in the gradient's launch (3) needs the LDS-phase gradient:
-    # row-round batches (small B) keep pass 2 a launch of its own (2)
-    assert _mode_of(ds, D, B) == (2 if pm_on == 3 and _rounds_of(ds, D, B) else pm_on)
+    # the margin in the gradient's launch (3) needs the LDS-phase gradient
+    # (row-round batches, small B, keep pass 2 a launch of its own: 2) and
+    # every 64-row block summed by a wave of the launch: blocks <= slices x
+    # the waves that fill the residuals (B = 2,500 > N: 40 blocks, 8 slices
+    # x 1 -> 2)
+    Beff = 1000 if B < 0 else B
+    fill = 1 if Beff <= 4096 else 2 if Beff <= 8192 else 4 if Beff <= 16384 else 8
+    fits = (Beff + 63) // 64 <= (D + 4095) // 4096 * fill
+    assert _mode_of(ds, D, B) == (2 if pm_on == 3 and (_rounds_of(ds, D, B) or not fits) else pm_on)
     eng = run_engine([ds], D, 3, B, 0.1)
     orc = oracle.run_worker([oracle_shard(ds, D)], D, 3, B, 0.1)
     compare_runs(eng, orc)
