@@ -113,13 +113,19 @@ def parse_args():
     ap.add_argument("--nnz", type=int, default=None)
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--lr", type=float, default=0.2)
-    ap.add_argument("--xpieces", type=int, default=4,
-                    help="N > 1: pieces of the overlapped all-gather (dlr_set_exchange_pieces)")
+    ap.add_argument("--xpieces", type=int, default=0,
+                    help="N > 1: pieces of the overlapped all-gather (dlr_set_exchange_pieces; 0 = auto, "
+                         "one per 4 MiB of a rank's key range, 1 to 4)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=["mean", "last", "async"], default="mean",
                     help="server update rule (main.cc:57-84): sync mean (default), sync last push, async")
     ap.add_argument("--spawn", action="store_true", help="use the process launcher even at --gpus 1")
+    ap.add_argument("--loopback-ranks", type=int, default=0,
+                    help="W > 1: an N > 1 exchange cost estimate on ONE GPU -- W ranks of the loopback "
+                         "transport (dlr_create_group, one thread each) run the world-W step; prints the "
+                         "exchange/merge microseconds per step with and without the overlap (not a "
+                         "throughput line)")
     ap.add_argument("--launcher-check", action="store_true",
                     help="ranks rendezvous over gloo and rank 0 prints the ranks it saw, no GPU work (CPU tests)")
     ap.add_argument("--dump-weights", default=None,
@@ -351,9 +357,128 @@ def launch(n: int) -> int:
 
 def main():
     args = parse_args()
+    if args.loopback_ranks > 1:
+        if args.gpus != 1 or "WORLD_SIZE" in os.environ:
+            sys.exit("--loopback-ranks runs W ranks on one GPU: --gpus 1, no launcher")
+        run_loopback(args)
+        return
     if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.spawn):
         sys.exit(launch(args.gpus))
     run_rank(args)
+
+
+def run_loopback(args):
+    """The world-W step on ONE GPU through the loopback transport (DESIGN.md
+    8): W contexts on device 0, one host thread each, the exchange's
+    collectives as device-to-device copies ordered by events.  What it
+    measures: the exchange's own work per step -- the key-range all-to-all
+    and all-gather as HBM copies (W - 1 peer blocks each way), the
+    rank-ordered merge, the next batch's pass 1 regrouped around the pieces
+    -- and how much of it the overlap hides.  What it cannot measure: xGMI
+    and RCCL latency (no multi-GPU box in this pool).  The W ranks share the
+    GPU, so ms_per_step is W ranks' compute."""
+    global dlr, np
+    import threading
+    import numpy as np  # noqa: F811
+    try:
+        import torch  # noqa: F401  -- the library binds to torch's HIP runtime
+    except Exception:  # pragma: no cover
+        pass
+    import distlr_amd as dlr  # noqa: F811
+    W, D, B = args.loopback_ranks, args.features, args.batch
+    t0 = time.perf_counter()
+    shards = [make_shard(args, args.rows, r + 1) for r in range(W)]
+    log(f"loopback: {W} shards of {args.rows} x {D} generated in {time.perf_counter() - t0:.1f}s")
+    engines = dlr.Engine.create_group(D, W, 0)
+    w0 = dlr.init_weight(D)
+    res = [None] * W
+    errors = [None] * W
+    bar = threading.Barrier(W)
+
+    def rank_main(r):
+        eng = engines[r]
+        try:
+            eng.set_exchange_pieces(args.xpieces)
+            eng.set_weights(w0)
+            nb = eng.load_train_dense(shards[r], B) if args.kind == "dense" else eng.load_train(shards[r], B)
+            shards[r].free()
+            k = 0
+
+            def steps(n, instrumented):
+                nonlocal k
+                eng.timing(instrumented)
+                bar.wait()
+                eng.sync()
+                bar.wait()
+                ta = time.perf_counter()
+                for _ in range(n):
+                    eng.train_step(k % nb, args.lr, 1.0, dlr.MODE_SYNC_MEAN)
+                    k += 1
+                eng.sync()
+                el = time.perf_counter() - ta
+                out = {name: eng.kernel_time(i) for name, i in
+                       [("exchange", dlr.TIMER_EXCHANGE), ("merge", dlr.TIMER_UPDATE), ("margin", dlr.TIMER_MARGIN),
+                        ("grad_update", dlr.TIMER_GRAD)]} if instrumented else {}
+                bar.wait()
+                return el, out
+
+            def per_step(t):
+                ms, n = t
+                return round(ms / max(1, n) * 1000.0, 3)
+
+            steps(args.warmup, False)
+            el_on, _ = steps(args.steps, False)
+            _, kt_on = steps(args.steps, True)
+            overlap, pieces = eng.exchange_overlap(), eng.exchange_pieces()
+            off = None
+            if overlap:
+                eng.set_exchange_overlap(False)  # collective: every rank calls it here
+                el_off, _ = steps(args.steps, False)
+                _, kt_off = steps(args.steps, True)
+                eng.set_exchange_overlap(True)
+                off = {"ms_per_step": round(el_off / args.steps * 1000.0, 5),
+                       "exchange_us_per_step": per_step(kt_off["exchange"]),
+                       "margin_us_per_step": per_step(kt_off["margin"])}
+            res[r] = {"ms_per_step": round(el_on / args.steps * 1000.0, 5), "overlap": bool(overlap),
+                      "pieces": pieces, "exchange_us_per_step": per_step(kt_on["exchange"]),
+                      "merge_us_per_step": per_step(kt_on["merge"]), "margin_us_per_step": per_step(kt_on["margin"]),
+                      "gradient_us_per_step": per_step(kt_on["grad_update"]), "without_overlap": off,
+                      "weights_sha1": hashlib.sha1(eng.get_weights().tobytes()).hexdigest()}
+        except BaseException as e:  # noqa: BLE001 -- reported below
+            errors[r] = e
+            eng.comm_abort(f"rank {r}: {e}")
+            try:
+                bar.abort()
+            except Exception:
+                pass
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(W)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for e in engines:
+        e.close()
+    for r, e in enumerate(errors):
+        if e is not None:
+            raise RuntimeError(f"loopback rank {r} failed") from e
+    r0 = res[0]
+    line = {
+        "metric": "exchange cost estimate (loopback transport, W ranks on one GPU)",
+        "ranks": W, "config": {"name": args.config, "rows_per_rank": args.rows, "num_feature_dim": D,
+                               "nnz_per_row": args.nnz, "batch_size": B},
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step_all_ranks": r0["ms_per_step"],
+        "exchange_us_per_step": r0["exchange_us_per_step"], "merge_us_per_step": r0["merge_us_per_step"],
+        "margin_us_per_step": r0["margin_us_per_step"], "gradient_us_per_step": r0["gradient_us_per_step"],
+        "overlap": r0["overlap"], "pieces": r0["pieces"], "without_overlap": r0["without_overlap"],
+        "per_rank_exchange_us": [x["exchange_us_per_step"] for x in res],
+        "ranks_agree": len({x["weights_sha1"] for x in res}) == 1,
+        "note": "the W ranks share one GPU (their compute is serialised on it); the collectives are "
+                "event-ordered device copies, so xGMI/RCCL latency is NOT in these numbers: the exchange's "
+                "own work (copies, rank-ordered merge, pass-1 regrouping) and what the overlap hides",
+    }
+    print(json.dumps(line), flush=True)
 
 
 def run_rank(args):
@@ -477,15 +602,18 @@ def run_rank(args):
             el = float(t.item())
         return el
 
-    # Pass 1 (the throughput): no per-kernel events in the launch stream.
-    el = timed(args.warmup, False)
-    # Pass 2: the same K steps with a HIP-event pair around every launch on
-    # the engine's stream -> the step breakdown (exchange included, N>1).
-    el_instr = timed(args.warmup + args.steps, True)
+    # Pass 1: K steps with a HIP-event pair around every launch on the
+    # engine's stream -> the step breakdown (exchange included, N>1).
+    # Pass 2 (the throughput, `value`): the next K steps, no per-kernel
+    # events in the launch stream.  The instrumented pass runs first so that
+    # the throughput pass does not start on a GPU whose clocks are still
+    # ramping from the idle host-side setup ("Short timed
+    # regions"); both are K real steps bracketed the same way.
+    el_instr = timed(args.warmup, True)
     kt = {name: eng.kernel_time(i) for name, i in
           [("margin", dlr.TIMER_MARGIN), ("grad_update", dlr.TIMER_GRAD), ("merge", dlr.TIMER_UPDATE),
            ("exchange", dlr.TIMER_EXCHANGE), ("step", dlr.TIMER_STEP)]}
-    eng.timing(False)
+    el = timed(args.warmup + args.steps, False)   # (timing(False) clears the event totals: read above)
     # Every rank holds the replicated weights after the same 2K (+W) steps:
     # their checksums must agree (and, with --dump-weights, the tests compare
     # them with the oracle's W-worker run).

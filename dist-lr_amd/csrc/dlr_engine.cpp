@@ -128,7 +128,8 @@ struct TrainShard {
     uint32_t *xslices = nullptr;
     std::vector<int64_t> xgofs;
     int64_t xsub = 0;  // words per piece of a rank's key range
-    int xpieces = 4;   // pieces (dlr_set_exchange_pieces at load, agreed over the ranks)
+    int xpieces = 1;   // pieces (dlr_set_exchange_pieces at load, agreed over the ranks)
+    bool xauto = true; // the piece count was left to auto_pieces
     // touched-column layout (huge D, small batches): per batch the touched
     // columns tcols[tcoff[b] .. +tncols[b]), segment pointers in cptr at
     // tpoff[b] (tncols[b]+1 entries), entries at coff[b] in crow/cval
@@ -272,8 +273,9 @@ struct dlr_ctx {
     hipStream_t xstream = nullptr;
     hipEvent_t ev_xmerged = nullptr;
     hipEvent_t ev_xpiece[kXPiecesMax] = {};
-    // pieces of the next loaded shard's overlapped all-gather
-    int xpieces = 4;
+    // pieces of the next loaded shard's overlapped all-gather (0: auto,
+    // auto_pieces)
+    int xpieces = 0;
     // product margin: the batch whose products pm_p holds, formed from the
     // CURRENT weights by the last step's fused gradient (-1: none; every
     // entry point that changes w or the shard resets it)
@@ -640,7 +642,13 @@ int coll_agree_pieced(dlr_ctx *c) {
     TrainShard &t = c->train;
     t.xpieced = false;
     if (!c->comm) return DLR_OK;
-    int64_t v = (t.pm && c->xoverlap && !t.sparse_stream) ? -1 : 0;  // max(-x) = -min(x)
+    // auto with one piece: no overlap -- pass 1 of this rank's own range is
+    // all it would hide (1/W of pass 1, under a microsecond at C2) and it
+    // costs a second pass-1 launch and a cross-stream wait (the loopback
+    // estimate, profiles/r05_loopback_c2_w*.json: 0.151 vs 0.122 ms per
+    // step at W = 2); the plain all-gather and the next margin's pass 1
+    const bool want = t.pm && c->xoverlap && !t.sparse_stream && !(t.xauto && t.xpieces == 1);
+    int64_t v = want ? -1 : 0;  // max(-x) = -min(x)
     int rc = coll_max_i64(c, &v);
     if (rc) return rc;
     t.xpieced = v == -1;
@@ -2151,6 +2159,21 @@ int build_overlap_groups(dlr_ctx *c) {
     return upload(c, &t.xslices, all.data(), all.size());
 }
 
+// The default piece count of the overlapped all-gather from the key range
+// one rank owns (the same on every rank: D and W only).  Each piece is a
+// collective with its own latency -- grouped RCCL sends and receives to
+// every peer, tens of microseconds -- so a piece must carry enough of the
+// range to be bandwidth-bound: one piece per 4 MiB of the range, 1 to 4.
+// C2 (D = 1M: 4 MB of weights, <= 2 MB a rank at W >= 2) gets ONE piece,
+// and then (coll_agree_pieced) no overlap at all: the plain in-place
+// ncclAllGather, not W - 1 sends and receives per piece against a 28 us
+// step.  An explicit dlr_set_exchange_pieces(1) keeps
+// the overlap with one ncclAllGather (exchange_overlapped).
+static int auto_pieces(int64_t chunk) {
+    const int64_t bytes = chunk * 4;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(4, bytes / ((int64_t)4 << 20)));
+}
+
 // world > 1, product margin: the all-gather of the merged weights in pieces
 // on the exchange stream, the next batch's pass 1 slice group by slice group
 // on the engine stream as their weights land (the exchange
@@ -2172,6 +2195,16 @@ int exchange_overlapped(dlr_ctx *c, int64_t b) {
         return dlr::launch_pm_products(pm, c->w, c->D, t.pm_p, c->stream, t.xslices + t.xgofs[(size_t)grp], n);
     };
     HIPC(c, pass1(0));  // inside this rank's own key range: ready now
+    if (t.xpieces == 1) {
+        // one piece: the plain in-place all-gather (one collective), then
+        // pass 1 of every other slice
+        COMMC(c, all_gather(c->w + (int64_t)c->rank * c->chunk, c->w, (size_t)c->chunk, c->xstream, e_));
+        HIPC(c, hipEventRecord(c->ev_xpiece[0], c->xstream));
+        HIPC(c, hipStreamWaitEvent(c->stream, c->ev_xpiece[0], 0));
+        HIPC(c, pass1(1));
+        c->pm_ready = nx;
+        return DLR_OK;
+    }
     for (int k = 0; k < t.xpieces; ++k) {
         const int64_t off = k * t.xsub, cnt = std::max<int64_t>(0, std::min(t.xsub, c->chunk - off));
         COMMC(c, all_gather_part(c->w, (size_t)c->chunk, (size_t)off, (size_t)cnt, c->xstream, e_));
@@ -2205,7 +2238,8 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         if (int rc_ = wait_stream(c, c->xstream, __func__)) return rc_;
     free_train(c);
     TrainShard &t = c->train;
-    t.xpieces = c->xpieces;
+    t.xpieces = c->xpieces ? c->xpieces : auto_pieces(c->chunk);
+    t.xauto = c->xpieces == 0;
     t.n_rows = ds->n_rows;
     t.nnz = (int64_t)ds->col.size();
     t.B = batch_size < 0 ? ds->n_rows : batch_size;
@@ -3412,8 +3446,8 @@ int dlr_exchange_overlap(dlr_ctx *c) {
 }
 
 int dlr_set_exchange_pieces(dlr_ctx *c, int pieces) {
-    if (!c || pieces < 1 || pieces > kXPiecesMax)
-        return fail(c, DLR_E_ARG, "dlr_set_exchange_pieces: pieces must be in [1, 16]");
+    if (!c || pieces < 0 || pieces > kXPiecesMax)
+        return fail(c, DLR_E_ARG, "dlr_set_exchange_pieces: pieces must be 0 (auto) or in [1, 16]");
     c->xpieces = pieces;  // the next load's (the ranks agree there)
     return DLR_OK;
 }

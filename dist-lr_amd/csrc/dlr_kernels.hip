@@ -1248,22 +1248,40 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     // wave 0 waits until every block of phase p is published (the caller's
     // barrier then holds the other waves' fills); a wait that runs out is
     // reported (Spin)
+    // The same poll reads the NEXT phase's counters too (lanes 8..15): the
+    // blocks of both phases are summed at the launch's start, so phase 1 is
+    // nearly always complete when phase 0 is, and its own poll -- a round
+    // trip queued behind the phase-1 windows and the pass-1 list loads --
+    // is skipped (mg_done: the phases known complete).
     Spin spin(MG ? p2.err : nullptr, kErrMgPublish);
+    int mg_done = 0;
     auto mg_wait = [&](int p) {
         if constexpr (MG) {
-            if (wv == 0) {
+            if (wv == 0 && p >= mg_done) {
                 constexpr int64_t bpp = R / kPmRows;
-                const uint32_t want = (uint32_t)(min<int64_t>(p2.pm.nblk, (p + 1) * bpp) - p * bpp);
+                auto want_of = [&](int q) {
+                    return (uint32_t)(min<int64_t>(p2.pm.nblk, (q + 1) * bpp) - q * bpp);
+                };
+                const bool two = p + 1 < P;
+                const uint32_t want = want_of(p), want1 = two ? want_of(p + 1) : 0u;
                 const __amdgpu_buffer_rsrc_t crs =
                     __builtin_amdgcn_make_buffer_rsrc(p2.cnt, 0, 0x7FFFFFFF, 0x00020000);
-                // lane s < 8 reads sub-counter s
-                const int off = (int)(((((p2.gen & 1) * 64 + p) * kMgSub + (lane & (kMgSub - 1))) * 32) * 4);
+                // lane s < 8 reads sub-counter s of phase p, lane 8 + s that
+                // of phase p + 1 (phase p again when p is the last)
+                const int q = p + ((lane >> 3) & 1 & (int)two);
+                const int off = (int)(((((p2.gen & 1) * 64 + q) * kMgSub + (lane & (kMgSub - 1))) * 32) * 4);
                 for (int k = 0; spin.more(k); ++k) {
                     const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(crs, off, 0, 16);
-                    uint32_t n = 0;
+                    uint32_t n = 0, n1 = 0;
 #pragma unroll
-                    for (int i = 0; i < kMgSub; ++i) n += __builtin_amdgcn_readlane(v, i);
-                    if (n >= want) break;
+                    for (int i = 0; i < kMgSub; ++i) {
+                        n += __builtin_amdgcn_readlane(v, i);
+                        n1 += __builtin_amdgcn_readlane(v, kMgSub + i);
+                    }
+                    if (n >= want) {
+                        mg_done = two && n1 >= want1 ? p + 2 : p + 1;
+                        break;
+                    }
                     __builtin_amdgcn_s_sleep(DLR_MG_SLEEP);
                 }
             }

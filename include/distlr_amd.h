@@ -425,8 +425,8 @@ int dlr_train_row_rounds(dlr_ctx *ctx);
 
 /* World > 1 with the product margin: the exchange overlapped with the next
  * batch's margin (BASELINE north_star).  The in-place all-gather of the
- * merged weights (lr.cc:122's Pull) runs in pieces (4 unless
- * dlr_set_exchange_pieces) on a second stream --
+ * merged weights (lr.cc:122's Pull) runs in pieces (dlr_set_exchange_pieces)
+ * on a second stream --
  * RCCL grouped send/recv of each rank's piece, or device copies on the
  * loopback group -- and the next batch's pass 1 forms each 4,096-column
  * slice as soon as every weight in it has landed (the slices of this rank's
@@ -442,8 +442,13 @@ int dlr_train_row_rounds(dlr_ctx *ctx);
 int dlr_set_exchange_overlap(dlr_ctx *ctx, int on);
 int dlr_exchange_overlap(dlr_ctx *ctx);
 
-/* Pieces of that all-gather, 1 .. 16 (default 4): more pieces start the
- * next margin's slices earlier, each piece costs a collective's latency.
+/* Pieces of that all-gather, 1 .. 16, or 0 (default) = auto: one piece per
+ * 4 MiB of the key range a rank owns, 1 to 4 -- and when that is one piece
+ * (C2 at any W), no overlap: the plain all-gather, then the next margin's
+ * pass 1 (one own-range slice group is all one piece could hide).  More
+ * pieces start the next margin's slices earlier, each piece costs a
+ * collective's latency; an explicit 1 is one in-place all-gather with the
+ * own-range pass 1 beside it.
  * A load-time setting: it applies to the next dlr_load_train, where the
  * ranks must agree on it (DLR_E_ARG otherwise).  dlr_exchange_pieces: the
  * loaded shard's piece count, 0 when its steps do not piece the gather. */

@@ -182,7 +182,8 @@ def test_pm_exchange_overlap_on_off(monkeypatch, W):
             seen.append((eng.train_product_margin(), eng.exchange_overlap()))
         return f
 
-    got = {on: run_group(shards, D, 2, 250, 0.2, setup=setup(on)) for on in (True, False)}
+    got = {on: run_group(shards, D, 2, 250, 0.2, setup=setup(on), preload=lambda eng, r: eng.set_exchange_pieces(4))
+           for on in (True, False)}
     assert (1, True) in seen and (1, False) in seen
     orc = oracle.run_worker([oracle_shard(s, D) for s in shards], D, 2, 250, 0.2)
     assert_same_weights(got[True].w, orc.w, "overlapped exchange")
@@ -218,7 +219,7 @@ def test_pm_exchange_pieces(monkeypatch, pieces, loop):
 @pytest.mark.parametrize("loop", ["async", "sync"])
 def test_pm_exchange_form_agreed_over_ranks(monkeypatch, loop):
     # one rank asks for the plain all-gather before loading, the others for
-    # the pieced one (the default): the ranks agree at load on the plain
+    # the pieced one (4 pieces): the ranks agree at load on the plain
     # form (the two forms are different collective sequences),
     # every rank reports it, and the weights are the oracle's
     monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
@@ -229,6 +230,7 @@ def test_pm_exchange_form_agreed_over_ranks(monkeypatch, loop):
     seen = []
 
     def pre(eng, r):
+        eng.set_exchange_pieces(4)
         if r == 1:
             eng.set_exchange_overlap(False)
 
@@ -250,11 +252,29 @@ def test_pm_exchange_pieces_must_agree(monkeypatch):
         run_group(shards, D, 1, 100, 0.2, preload=lambda eng, r: eng.set_exchange_pieces(2 + r))
     eng = dlr.Engine(D)
     try:
-        for bad in (0, 17):
+        for bad in (-1, 17):
             with pytest.raises(dlr.DLRError):
                 eng.set_exchange_pieces(bad)
+        eng.set_exchange_pieces(0)  # auto (the default)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("W", [2, 8])
+def test_pm_exchange_auto_pieces_is_one_gather(monkeypatch, W):
+    # the default piece count is one per 4 MiB of a rank's key range: a
+    # C2-sized D (<= 4 MB of weights) gets ONE piece, i.e. no overlap -- the
+    # plain in-place all-gather, not W - 1 sends and receives per piece --
+    # bitwise the oracle
+    monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
+    monkeypatch.setenv("DLR_PM", "1")
+    D = 300_000
+    shards = [dlr.Dataset.generate(900, D, 12, value_mode=1, seed=41, stream=r + 1) for r in range(W)]
+    seen = []
+    got = run_group(shards, D, 2, 200, 0.2, setup=lambda eng: seen.append((eng.exchange_overlap(), eng.exchange_pieces())))
+    assert seen == [(0, 0)] * W
+    orc = oracle.run_worker([oracle_shard(s, D) for s in shards], D, 2, 200, 0.2)
+    compare_runs(got, orc)
 
 
 def test_pm_overlap_through_rccl_one_rank(monkeypatch):
