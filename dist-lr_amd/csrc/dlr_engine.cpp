@@ -11,6 +11,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <numeric>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -189,6 +190,18 @@ struct TrainShard {
         int64_t hw = 0, nhot = 0;            // the band's hot waves (k_band_hot): bhw[hw .. hw + nhot)
     };
     int64_t max_hot = 0;  // the most hot waves of a band (CUs the pipelined margin leaves them)
+    // hot-column product stream (band mode, REFERENCE; dlr_kernels.h
+    // DevHotOut / DevHotChain): per batch b, its hot columns hs_cols[hsco[b]
+    // .. + hs_nh[b]), their (start, count) per band hs_seg[hsso[b] ..], the
+    // per-row hot entry lists hs_off[hsoo[b] ..] (B_b + 1, absolute into
+    // hs_dest / hs_val); one stream buffer and per-band flags for the shard
+    bool hs = false;
+    std::vector<int64_t> hs_nh, hsco, hsso, hsoo;
+    uint32_t *hs_cols = nullptr, *hs_off = nullptr, *hs_dest = nullptr, *hs_flag = nullptr;
+    uint2 *hs_seg = nullptr;
+    float *hs_val = nullptr, *hs_buf = nullptr;
+    uint32_t hs_seq = 0;
+    int64_t hs_bytes = 0;
     int band_shift = 0;
     bool band_longrun = false;  // band mode without the long-column split: runs of 10^5 entries in a band
     // margin with the hot (lowest, frequency-ordered) weights in LDS
@@ -365,8 +378,9 @@ int check_device(dlr_ctx *c, const char *who) {
         "a chain slot's margin units were never published (k_dense_ref)",
         "the column chains' limit never reached a margin unit (k_dense_ref)",
         "a hand-off between the waves of a workgroup never came (k_dense_ref)",
-        "a hand-off between the waves of a workgroup never came (k_band_hot)",
-        "unknown", "unknown", "unknown"};
+        "a hand-off between the waves of a workgroup never came (k_band_hot / k_hot_chain)",
+        "a band's hot-column products were never published (k_hot_chain)",
+        "unknown", "unknown"};
     std::string msg;
     for (int k = 0; k < dlr::kErrWords; ++k) {
         if (__atomic_load_n(c->h_err + k, __ATOMIC_ACQUIRE) == 0u) continue;
@@ -453,7 +467,8 @@ void free_train(dlr_ctx *c) {
                     (void *)t.gval, (void *)t.gscratch, (void *)t.tcols,
                     (void *)t.lcols, (void *)t.lcseg, (void *)t.lsptr, t.lrow, (void *)t.lval, (void *)t.lpart, (void *)t.lsched,
                     (void *)t.dX, (void *)t.dpart, (void *)t.wsched, (void *)t.bcols, (void *)t.bptr,
-                    (void *)t.bws, (void *)t.bhw, t.brow, (void *)t.bval, (void *)t.gacc, (void *)t.lpdesc, (void *)t.lpptr,
+                    (void *)t.bws, (void *)t.bhw, (void *)t.hs_cols, (void *)t.hs_off, (void *)t.hs_dest,
+                    (void *)t.hs_flag, (void *)t.hs_seg, (void *)t.hs_val, (void *)t.hs_buf, t.brow, (void *)t.bval, (void *)t.gacc, (void *)t.lpdesc, (void *)t.lpptr,
                     (void *)t.lpslot, (void *)t.lpws, (void *)t.lprow, (void *)t.lpval, (void *)t.pm_lbeg,
                     (void *)t.pm_list, (void *)t.pm_pofs, (void *)t.pm_rg, (void *)t.pm_qoff, (void *)t.pm_val,
                     (void *)t.pm_p, (void *)t.pm_qs, (void *)t.xslices, (void *)t.rt_gq, (void *)t.rt_val,
@@ -1021,6 +1036,138 @@ void build_bands(const std::vector<uint32_t> &cptr, const std::vector<RowT> &cro
         }
         out.bfirst[(size_t)b + 1] = (int64_t)out.bands.size();
     }
+}
+
+// The hot-column product stream (TrainShard::hs) of every batch, from the
+// classic copy (each column's entries in batch-row order): a column with >=
+// hot_min entries in the batch is HOT (the same ones build_bands marks);
+// its stream holds its products band by band, each band's segment starting
+// at a multiple of kHotChunkF floats (no chunk -- no cache line -- holds two
+// bands); row i's list gets one (stream slot, value) per hot entry.  Off
+// (DLR_HOT_STREAM=0, no hot column, or more than kHsMaxCols in a batch: the
+// per-band k_band_hot launches instead).
+constexpr int64_t kHsMaxCols = 64;
+bool hot_stream_wanted() {
+    const char *e = getenv("DLR_HOT_STREAM");
+    return !(e && strcmp(e, "0") == 0);
+}
+// The smallest threshold >= hot_min that leaves at most kHsMaxCols hot
+// columns in every batch (one k_hot_chain workgroup -- one CU -- each).
+int64_t hot_stream_threshold(const std::vector<uint32_t> &cptr, int64_t nb, int64_t D, int64_t hot_min) {
+    int64_t thr = hot_min;
+    for (int64_t b = 0; b < nb; ++b) {
+        const uint32_t *cp = cptr.data() + (size_t)b * (size_t)(D + 1);
+        std::vector<int64_t> big;
+        for (int64_t j = 0; j < D; ++j) {
+            const int64_t n = (int64_t)(cp[j + 1] & 0x7FFFFFFFu) - (int64_t)(cp[j] & 0x7FFFFFFFu);
+            if (n >= hot_min) big.push_back(n);
+        }
+        if ((int64_t)big.size() > kHsMaxCols) {
+            std::nth_element(big.begin(), big.begin() + kHsMaxCols, big.end(), std::greater<int64_t>());
+            thr = std::max(thr, big[(size_t)kHsMaxCols] + 1);  // the (kHsMaxCols+1)-th largest is not hot
+        }
+    }
+    return thr;
+}
+template <typename RowT>
+int build_hot_stream(dlr_ctx *c, const std::vector<uint32_t> &cptr, const std::vector<RowT> &crow,
+                     const std::vector<float> &cval, int64_t hot_min, int shift) {
+    TrainShard &t = c->train;
+    if (!hot_stream_wanted()) return DLR_OK;
+    const int64_t nb = (int64_t)t.plan.size(), D = c->D;
+    std::vector<std::vector<uint32_t>> hot((size_t)nb);
+    int64_t any = 0;
+    for (int64_t b = 0; b < nb; ++b) {
+        const uint32_t *cp = cptr.data() + (size_t)b * (size_t)(D + 1);
+        for (int64_t j = 0; j < D; ++j)
+            if ((int64_t)(cp[j + 1] & 0x7FFFFFFFu) - (int64_t)(cp[j] & 0x7FFFFFFFu) >= hot_min && !(cp[j] & 0x80000000u))
+                hot[(size_t)b].push_back((uint32_t)j);
+        if ((int64_t)hot[(size_t)b].size() > kHsMaxCols) return DLR_OK;
+        any += (int64_t)hot[(size_t)b].size();
+    }
+    if (any == 0) return DLR_OK;
+    std::vector<uint32_t> cols, off, dest;
+    std::vector<float> val;
+    std::vector<uint2> seg;
+    t.hs_nh.assign((size_t)nb, 0);
+    t.hsco.assign((size_t)nb + 1, 0);
+    t.hsso.assign((size_t)nb + 1, 0);
+    t.hsoo.assign((size_t)nb + 1, 0);
+    int64_t buf_need = 0, max_bands = 1;
+    for (int64_t b = 0; b < nb; ++b) {
+        const uint32_t *cp = cptr.data() + (size_t)b * (size_t)(D + 1);
+        const RowT *rr = crow.data() + t.coff[(size_t)b];
+        const float *vv = t.unit ? nullptr : cval.data() + t.coff[(size_t)b];
+        const int64_t rows = t.plan[(size_t)b].rows;
+        const int64_t nbands = (rows + ((int64_t)1 << shift) - 1) >> shift;
+        max_bands = std::max(max_bands, nbands);
+        const std::vector<uint32_t> &H = hot[(size_t)b];
+        const int64_t nh = (int64_t)H.size();
+        t.hs_nh[(size_t)b] = nh;
+        // segments: per (column, band) count, then padded starts
+        std::vector<uint2> sg((size_t)(nh * nbands), uint2{0, 0});
+        for (int64_t h = 0; h < nh; ++h) {
+            const uint32_t j = H[(size_t)h];
+            for (uint32_t q = cp[j] & 0x7FFFFFFFu; q < (cp[j + 1] & 0x7FFFFFFFu); ++q)
+                ++sg[(size_t)(h * nbands + ((int64_t)rr[q] >> shift))].y;
+        }
+        int64_t at = 0;
+        for (uint2 &x : sg) {
+            x.x = (uint32_t)at;
+            at += (x.y + dlr::kHotChunkF - 1) / dlr::kHotChunkF * dlr::kHotChunkF;
+        }
+        if (at >= ((int64_t)1 << 32)) return fail(c, DLR_E_ARG, "dlr_load_train: hot-column stream too large");
+        buf_need = std::max(buf_need, at);
+        // per-row lists: counts, offsets, then (slot, value) per hot entry
+        std::vector<uint32_t> cnt((size_t)rows + 1, 0);
+        for (int64_t h = 0; h < nh; ++h) {
+            const uint32_t j = H[(size_t)h];
+            for (uint32_t q = cp[j] & 0x7FFFFFFFu; q < (cp[j + 1] & 0x7FFFFFFFu); ++q) ++cnt[(size_t)rr[q] + 1];
+        }
+        const size_t o0 = off.size(), d0 = dest.size();
+        if (d0 + (size_t)std::accumulate(cnt.begin(), cnt.end(), (uint64_t)0) >= ((size_t)1 << 32))
+            return fail(c, DLR_E_ARG, "dlr_load_train: too many hot entries");
+        off.resize(o0 + (size_t)rows + 1);
+        uint32_t run = (uint32_t)d0;
+        for (int64_t i = 0; i <= rows; ++i) {
+            run += cnt[(size_t)i];
+            off[o0 + (size_t)i] = run;  // (cnt[0] == 0: off[o0] = d0)
+        }
+        dest.resize(off[o0 + (size_t)rows]);
+        if (!t.unit) val.resize(dest.size());
+        std::vector<uint32_t> fillp(off.begin() + (int64_t)o0, off.end() - 1);
+        for (int64_t h = 0; h < nh; ++h) {
+            const uint32_t j = H[(size_t)h];
+            std::vector<uint32_t> rank((size_t)nbands, 0);
+            for (uint32_t q = cp[j] & 0x7FFFFFFFu; q < (cp[j + 1] & 0x7FFFFFFFu); ++q) {
+                const int64_t i = (int64_t)rr[q], sb = i >> shift;
+                const uint32_t slot = sg[(size_t)(h * nbands + sb)].x + rank[(size_t)sb]++;
+                const uint32_t k = fillp[(size_t)i]++;
+                dest[k] = slot;
+                if (!t.unit) val[k] = vv[q];
+            }
+        }
+        t.hsco[(size_t)b + 1] = t.hsco[(size_t)b] + nh;
+        t.hsso[(size_t)b + 1] = t.hsso[(size_t)b] + nh * nbands;
+        t.hsoo[(size_t)b] = (int64_t)o0;
+        t.hsoo[(size_t)b + 1] = (int64_t)off.size();
+        cols.insert(cols.end(), H.begin(), H.end());
+        seg.insert(seg.end(), sg.begin(), sg.end());
+    }
+    int r;
+    if ((r = upload(c, &t.hs_cols, cols.data(), cols.size()))) return r;
+    if ((r = upload(c, &t.hs_seg, seg.data(), seg.size()))) return r;
+    if ((r = upload(c, &t.hs_off, off.data(), off.size()))) return r;
+    if ((r = upload(c, &t.hs_dest, dest.data(), dest.size(), 1))) return r;
+    if (!t.unit && (r = upload(c, &t.hs_val, val.data(), val.size(), 1))) return r;
+    if ((r = dev_alloc(c, (void **)&t.hs_buf, (size_t)(buf_need + dlr::kHotChunkF) * 4))) return r;
+    std::vector<uint32_t> zero((size_t)max_bands, 0);
+    if ((r = upload(c, &t.hs_flag, zero.data(), zero.size()))) return r;
+    t.hs_seq = 0;
+    t.hs = true;
+    t.hs_bytes = (int64_t)((cols.size() + off.size() + dest.size() + val.size()) * 4 + seg.size() * 8 +
+                           (buf_need + dlr::kHotChunkF) * 4);
+    return DLR_OK;
 }
 
 // Long columns of every batch regrouped in row phases of kLPhase rows
@@ -1896,6 +2043,11 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
         if (e != hipSuccess) return e;
     }
     const bool hot = t.bhw != nullptr;
+    // the hot columns' chains: ONE k_hot_chain launch over every band (the
+    // hot-column product stream: the margins write the products, a flag per
+    // band publishes them), or k_band_hot per band
+    const bool hs = hot && t.hs;
+    const int64_t nh = hs ? t.hs_nh[bb] : 0;
     // with hot chains beside it, the persistent margin leaves their CUs (and
     // DLR_BAND_CUS more to the other columns' band kernel, whose workgroups
     // cannot share a CU with the margin's: A/B, measured no better at 32,
@@ -1904,7 +2056,7 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
         const char *e = getenv("DLR_BAND_CUS");
         return e ? atoi(e) : 0;
     }();
-    const int margin_reserve = hot ? (int)t.max_hot + band_cus : 0;
+    const int margin_reserve = hs ? (int)nh + band_cus : hot ? (int)t.max_hot + band_cus : 0;
     if (hot && !c->hstream) {
         e = hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_hdone, hipEventDisableTiming);
@@ -1925,6 +2077,14 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
     if (e == hipSuccess) e = hipEventRecord(c->ev_bstart, c->stream);
     if (e == hipSuccess) e = hipStreamWaitEvent(c->gstream, c->ev_bstart, 0);
     if (e == hipSuccess && hot) e = hipStreamWaitEvent(c->hstream, c->ev_bstart, 0);
+    dlr::DevHotOut ho{};
+    if (hs) {
+        ++t.hs_seq;
+        const dlr::DevHotChain hc{t.hs_cols + t.hsco[bb], t.hs_seg + t.hsso[bb], t.hs_buf, t.hs_flag, nh, nbands,
+                                  t.hs_seq, c->d_err, c->fault};
+        if (e == hipSuccess) e = dlr::launch_hot_chain(hc, t.gacc, c->hstream);
+        ho = dlr::DevHotOut{t.hs_off + t.hsoo[bb], t.hs_dest, t.hs_val, t.hs_buf};
+    }
     for (int64_t k = 0; e == hipSuccess && k < nbands; ++k) {
         const int64_t r0 = k * BR, r1 = std::min(all.rows, r0 + BR);
         dlr::DevBatch sub = all;
@@ -1932,8 +2092,11 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
         sub.label = all.label + r0;
         sub.rows = r1 - r0;
         sub.nnz = all.rows > 0 ? all.nnz * sub.rows / all.rows : 0;  // the margin's rows-per-wave heuristic
-        e = t.margin_hot ? dlr::launch_margin_hot(sub, c->w, c->D, c->resid + r0, c->stream, margin_reserve)
+        dlr::DevHotOut hk = ho;
+        if (hk.off) hk.off += r0;  // the band's rows
+        e = t.margin_hot ? dlr::launch_margin_hot(sub, c->w, c->D, c->resid + r0, c->stream, margin_reserve, hk)
                          : dlr::launch_margin_residual(sub, c->w, c->resid + r0, c->stream);
+        if (e == hipSuccess && hs) e = dlr::launch_flag_store(t.hs_flag + k, t.hs_seq, c->stream);
         if (e == hipSuccess) e = hipEventRecord(c->ev_band[(size_t)k], c->stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(c->gstream, c->ev_band[(size_t)k], 0);
         const TrainShard::Band &bd = t.bands[(size_t)(t.bfirst[bb] + k)];
@@ -1942,8 +2105,8 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
         if (e == hipSuccess) e = dlr::launch_grad_band(dv, c->resid, t.gacc, c->gstream, t.band_longrun, hot);
         // the hot pairs: their chains continue band after band on their own
         // stream, beside the next band's margin and the other columns
-        if (e == hipSuccess && hot) e = hipStreamWaitEvent(c->hstream, c->ev_band[(size_t)k], 0);
-        if (e == hipSuccess && hot) e = dlr::launch_band_hot(dv, t.bhw + bd.hw, bd.nhot, c->resid, t.gacc, c->hstream, c->d_err, c->fault);
+        if (e == hipSuccess && hot && !hs) e = hipStreamWaitEvent(c->hstream, c->ev_band[(size_t)k], 0);
+        if (e == hipSuccess && hot && !hs) e = dlr::launch_band_hot(dv, t.bhw + bd.hw, bd.nhot, c->resid, t.gacc, c->hstream, c->d_err, c->fault);
     }
     if (e == hipSuccess) e = hipEventRecord(c->ev_bdone, c->gstream);
     if (e == hipSuccess && hot) e = hipEventRecord(c->ev_hdone, c->hstream);
@@ -2800,7 +2963,12 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             // (DLR_BAND_HOT: entries in the batch that make a column hot;
             // 0 = none)
             const char *bh = getenv("DLR_BAND_HOT");
-            const int64_t hot_min = long_min == 0 ? (bh ? atoll(bh) : (int64_t)1 << 17) : 0;
+            int64_t hot_min = long_min == 0 ? (bh ? atoll(bh) : (int64_t)1 << 17) : 0;
+            // with the hot-column product stream: at most kHsMaxCols hot
+            // columns a batch (the hottest; the others' chains run in
+            // k_grad_band, band by band)
+            if (hot_min > 0 && t.margin_hot && hot_stream_wanted())
+                hot_min = hot_stream_threshold(cptr, nb, D, hot_min);
             build_bands(cptr, crow, cval, t.coff, nb, D, t.B, shift, t.unit, nthreads, hot_min, bb);
             t.band_shift = shift;
             t.band_longrun = long_min == 0;
@@ -2811,6 +2979,8 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             if ((r = upload(c, &t.bws, bb.ws.data(), bb.ws.size()))) return r;
             if (!bb.hw.empty() && (r = upload(c, &t.bhw, bb.hw.data(), bb.hw.size()))) return r;
             for (const TrainShard::Band &x : t.bands) t.max_hot = std::max(t.max_hot, x.nhot);
+            if (hot_min > 0 && t.margin_hot && (r = build_hot_stream(c, cptr, crow, cval, hot_min, shift))) return r;
+            csc_bytes += t.hs_bytes;
             if ((r = upload(c, (RowT **)&t.brow, bb.row.data(), bb.row.size(), kPad))) return r;
             if (!t.unit && (r = upload(c, &t.bval, bb.val.data(), bb.val.size(), kPad))) return r;
             if ((r = dev_alloc(c, (void **)&t.gacc, (size_t)D * 4))) return r;
@@ -3415,6 +3585,15 @@ int dlr_train_row_rounds(dlr_ctx *c) {
     if (!c) return DLR_E_ARG;
     if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_row_rounds: no training shard loaded");
     return c->train.pcsc && c->train.rt ? c->train.rt_rounds : 0;
+}
+
+int dlr_train_hot_columns(dlr_ctx *c) {
+    if (!c) return DLR_E_ARG;
+    if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_hot_columns: no training shard loaded");
+    const TrainShard &t = c->train;
+    int64_t n = 0;
+    for (int64_t x : t.hs_nh) n = std::max(n, x);
+    return t.hs ? (int)n : 0;
 }
 
 int dlr_train_band_rows(dlr_ctx *c) {

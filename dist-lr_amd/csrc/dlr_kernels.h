@@ -125,7 +125,8 @@ enum DevErr {
     kErrRefSlot = 1,    // k_dense_ref: a chain slot's margin units were never published
     kErrRefLimit = 2,   // k_dense_ref: the chains' limit never reached a margin unit
     kErrRefLds = 3,     // k_dense_ref: a hand-off between the waves of a workgroup
-    kErrHotLds = 4,     // k_band_hot: a hand-off between the waves of a workgroup
+    kErrHotLds = 4,     // k_band_hot / k_hot_chain: a hand-off between the waves of a workgroup
+    kErrHotFlag = 5,    // k_hot_chain: a band's hot products were never published
     kErrWords = 8
 };
 // Test-only fault injection (dlr_set_fault): a producer that never comes.
@@ -133,7 +134,7 @@ enum DevFault {
     kFaultNone = 0,
     kFaultMgPublish = 1,   // k_grad_lds MG: margin block 0 never adds to its counter
     kFaultRefPublish = 2,  // k_dense_ref: margin unit 0 never adds to its slot's counter
-    kFaultHotRing = 3      // k_band_hot: the product waves never post a chunk
+    kFaultHotRing = 3      // k_band_hot / k_hot_chain: the product / loader waves never post a chunk
 };
 
 // The largest grid of `threads`-thread workgroups with `lds` bytes of
@@ -250,12 +251,51 @@ struct RankSizes {
 };
 
 hipError_t launch_margin_residual(const DevBatch &bt, const float *w, float *resid, hipStream_t s);
+// HOT-COLUMN PRODUCT STREAM (REFERENCE order, band mode; dlr_kernels.hip
+// "Hot-column product stream").  The margin kernel, right after row i's
+// residual r_i, writes fl32(r_i * x_ij) of each of the row's entries in a
+// HOT column j (one with a chain of ~10^6 adds) to that column's stream in
+// buf: entries t in [off[i], off[i+1]) of dest/val (val null: unit values)
+// go to buf[dest[t]].  A column's stream holds its products in batch-row
+// order, band by band, each band's segment starting at a multiple of
+// kHotChunk floats.  off/dest/val indexed from the margin's first row (the
+// caller offsets off like row_ptr).
+struct DevHotOut {
+    const uint32_t *off = nullptr;  // null: no hot products
+    const uint32_t *dest = nullptr;
+    const float *val = nullptr;
+    float *buf = nullptr;
+};
+// The margin kernel of a band publishes the band's hot products: after it,
+// flag[band] = seq (agent scope).
+hipError_t launch_flag_store(uint32_t *flag, uint32_t seq, hipStream_t s);
+// The hot columns' chains of one batch, ONE launch for every band (a
+// workgroup per hot column, persistent over the step): the column's
+// products streamed from buf in order, band s once flag[s] >= seq; chain
+// sum from +0 in batch-row order; the sum stored to gacc[cols[h]].  seg:
+// per (column h, band s) the segment's (start, count) in buf, h-major.
+struct DevHotChain {
+    const uint32_t *cols;
+    const uint2 *seg;
+    const float *buf;
+    const uint32_t *flag;
+    int64_t nh, nbands;
+    uint32_t seq;
+    uint32_t *err;
+    int fault;
+};
+constexpr int kHotChunkF = 256;  // floats of one stream chunk (a band segment starts at a multiple)
+hipError_t launch_hot_chain(const DevHotChain &hc, float *gacc, hipStream_t s);
 // The same margins with w[0, kMarginHot) staged in LDS (frequency-ordered
-// shards; needs D >= kMarginHot).
+// shards; needs D >= kMarginHot); ho: the hot columns' products too.
 constexpr int kMarginHot = 8192;
 constexpr int kMarginHotWaves = 8;
 hipError_t launch_margin_hot(const DevBatch &bt, const float *w, int64_t D, float *resid, hipStream_t s,
-                             int reserve = 0);
+                             int reserve, const DevHotOut &ho);
+inline hipError_t launch_margin_hot(const DevBatch &bt, const float *w, int64_t D, float *resid, hipStream_t s,
+                                    int reserve = 0) {
+    return launch_margin_hot(bt, w, D, resid, s, reserve, DevHotOut{});
+}
 int predict_grid(int64_t rows);
 hipError_t launch_predict(const DevBatch &bt, const float *w, unsigned long long *correct, double *ll_part,
                           double *ll_out, hipStream_t s);

@@ -523,9 +523,12 @@ __global__ __launch_bounds__(kWaves *kWave) void k_margin_residual(DevBatch bt, 
 // gathers read LDS and only the tail's go to L2.  Persistent workgroups
 // (two per CU) loop over blocks of NW*SEG rows; otherwise k_margin_residual
 // (same products, same in-order sums: bitwise the same margins).
+// ho.off != null: after row i's residual, its hot columns' products
+// fl32(r_i * x_ij) go to their product streams (DevHotOut) -- the same
+// products k_band_hot forms from the residuals, in the same rounding.
 template <int HOT, int NW, int SEG, bool UNIT>
 __global__ __launch_bounds__(NW *kWave) void k_margin_hot(DevBatch bt, const float *__restrict__ w,
-                                                          float *__restrict__ resid) {
+                                                          float *__restrict__ resid, DevHotOut ho) {
     __shared__ __attribute__((aligned(16))) float s_w[HOT];
     __shared__ float s_p[NW][kWin];
     const int lane = threadIdx.x & (kWave - 1);
@@ -549,7 +552,14 @@ __global__ __launch_bounds__(NW *kWave) void k_margin_hot(DevBatch bt, const flo
         const int64_t a = valid ? bt.row_ptr[my] : e1, b = valid ? bt.row_ptr[my + 1] : e1;
         const float z = ordered_segment_dot<int32_t, UNIT, HOT>(e0, e1, a, b, lane, bt.col, bt.val, w, s_p[wv],
                                                                  0.0f, s_w);
-        if (valid) resid[my] = sigmoid_ref(z) - y;
+        if (valid) {
+            const float r = sigmoid_ref(z) - y;
+            resid[my] = r;
+            if (ho.off) {
+                const uint32_t t1 = ho.off[my + 1];
+                for (uint32_t t = ho.off[my]; t < t1; ++t) ho.buf[ho.dest[t]] = UNIT ? r : r * ho.val[t];
+            }
+        }
     }
 }
 
@@ -1979,6 +1989,127 @@ __global__ __launch_bounds__(256) void k_band_hot(DevBand bd, const uint32_t *__
             }
         }
     }
+}
+
+// Hot-column product stream (REFERENCE order, band mode; DevHotOut /
+// DevHotChain).  k_band_hot forms a hot column's products from residuals
+// it gathers band by band -- random L2 reads on the chain's critical path,
+// slowest beside the next band's margin -- and is launched once per band, so
+// its chain restarts at every band.  Here the margin kernel writes each hot
+// product as it computes the row's residual (k_margin_hot, ho), into the
+// column's stream in batch-row order, and after each band's margin a flag
+// publishes the band (launch_flag_store).  ONE launch per step then runs
+// every hot column's chain over all bands: wave 1 streams the column's
+// products into a 32-chunk LDS ring by LDS-DMA (a band's chunks once its flag
+// is up; sc1 loads, and no band segment shares a chunk -- or a cache line --
+// with the next, so no line is read before its band is published), and wave
+// 0 adds them in order from +0, 32 per LDS wait, the next 32 in flight.  The
+// same products added in the same order: bitwise k_band_hot's (and the
+// oracle's) sums; the chain never waits on a gather.
+constexpr int kHcRing = 32;  // chunks of kHotChunkF floats in the ring
+constexpr int kHcLA = 8;     // chunks a loader keeps in flight
+static_assert(kHotChunkF == kHotChunk, "one chunk size for both hot kernels");
+__global__ __launch_bounds__(1) void k_flag_store(uint32_t *flag, uint32_t seq) {
+    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(128) void k_hot_chain(DevHotChain hc, float *__restrict__ gacc) {
+    extern __shared__ __attribute__((aligned(16))) float hsm[];
+    float *ring = hsm;                                                     // [kHcRing][kHotChunkF]
+    uint32_t *ctl = reinterpret_cast<uint32_t *>(hsm + kHcRing * kHotChunkF);  // [0] landed, [1] consumed
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    if (threadIdx.x < 4) ctl[threadIdx.x] = 0u;
+    __syncthreads();
+    const int64_t h = blockIdx.x;
+    const uint2 *seg = hc.seg + h * hc.nbands;
+    Spin spin(hc.err, kErrHotLds);
+    if (wv == 1) {
+        // the loader: chunk g of the column's stream (bands in order) into
+        // ring slot g % kHcRing; landed chunks are posted in order
+        Spin fspin(hc.err, kErrHotFlag);
+        const __amdgpu_buffer_rsrc_t frs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(hc.flag), 0, 0x7FFFFFFF, 0x00020000);
+        uint32_t g = 0, landed = 0, ck = 0;  // chunks issued, posted landed, known consumed
+        for (int64_t s = 0; s < hc.nbands; ++s) {
+            const uint2 sg = seg[s];
+            const uint32_t nch = (sg.y + kHotChunkF - 1) / kHotChunkF;
+            if (nch == 0) continue;
+            for (int k = 0;; ++k) {  // the band's products are published
+                const uint32_t f = __builtin_amdgcn_raw_buffer_load_b32(frs, (int)(s * 4), 0, 16);
+                if ((int32_t)(__builtin_amdgcn_readfirstlane(f) - hc.seq) >= 0 || !fspin.more(k)) break;
+                __builtin_amdgcn_s_sleep(8);
+            }
+            for (uint32_t c = 0; c < nch; ++c, ++g) {
+                if (g >= (uint32_t)kHcRing && (int32_t)(ck - (g - kHcRing + 1)) < 0)
+                    ck = ctl_poll(ctl + 1, g - kHcRing + 1, spin);  // the slot's last chunk was added
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(hc.buf + sg.x + (size_t)c * kHotChunkF + 4 * lane),
+                    (__attribute__((address_space(3))) void *)(ring + (g % kHcRing) * kHotChunkF), 16, 0, 16);
+                if (g + 1 - landed > (uint32_t)kHcLA) {
+                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // = kHcLA: chunk g - 8 has landed
+                    landed = g + 1 - kHcLA;
+                    if (lane == 0 && hc.fault != kFaultHotRing) ctl_post(ctl, landed);
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the band's chunks (before the next flag poll)
+            landed = g;
+            if (lane == 0 && hc.fault != kFaultHotRing) ctl_post(ctl, landed);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives its wave
+        return;
+    }
+    if (wv != 0) return;
+    // the chain: the column's products in stream order from +0
+    float acc = 0.0f;
+    uint32_t pk = 0, g = 0;  // chunks known landed, chunks added
+    auto rd = [&](v4f(&d)[8], const float *q) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) d[u] = *reinterpret_cast<const v4f *>(q + 4 * u);
+    };
+    auto add = [&](const v4f(&d)[8]) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            acc = acc + d[u].x;
+            acc = acc + d[u].y;
+            acc = acc + d[u].z;
+            acc = acc + d[u].w;
+        }
+    };
+    v4f da[8], db[8];
+    for (int64_t s = 0; s < hc.nbands; ++s) {
+        const uint2 sg = seg[s];
+        const uint32_t nfull = sg.y / kHotChunkF, rem = sg.y % kHotChunkF;
+        if (nfull > 0) {
+            if ((int32_t)(pk - (g + 1)) < 0) pk = ctl_poll(ctl, g + 1, spin);
+            rd(da, ring + (g % kHcRing) * kHotChunkF);
+        }
+        for (uint32_t c = 0; c < nfull; ++c, ++g) {
+            const float *q = ring + (g % kHcRing) * kHotChunkF;
+#pragma unroll 1
+            for (int k = 0; k < kHotChunkF - 64; k += 64) {
+                rd(db, q + k + 32);
+                add(da);
+                rd(da, q + k + 64);
+                add(db);
+            }
+            rd(db, q + kHotChunkF - 32);
+            add(da);
+            const bool more = c + 1 < nfull;
+            if (more && (int32_t)(pk - (g + 2)) < 0) pk = ctl_poll(ctl, g + 2, spin);
+            rd(da, more ? ring + ((g + 1) % kHcRing) * kHotChunkF : q);  // (after the last: a re-read, unused)
+            add(db);
+            if (lane == 0) ctl_post(ctl + 1, g + 1);
+        }
+        if (rem > 0) {
+            if ((int32_t)(pk - (g + 1)) < 0) pk = ctl_poll(ctl, g + 1, spin);
+            const float *q = ring + (g % kHcRing) * kHotChunkF;
+            for (uint32_t k = 0; k < rem; ++k) acc = acc + q[k];
+            if (lane == 0) ctl_post(ctl + 1, g + 1);
+            ++g;
+        }
+    }
+    if (lane == 0) gacc[hc.cols[h]] = acc;
 }
 
 // Long columns in ROW PHASES (band mode).  The chunked long path gathers
@@ -3722,17 +3853,18 @@ hipError_t launch_margin_residual(const DevBatch &bt, const float *w, float *res
 }
 
 template <int HOT, int NW>
-hipError_t launch_mh(const DevBatch &bt, const float *w, float *resid, unsigned cap, hipStream_t s) {
+hipError_t launch_mh(const DevBatch &bt, const float *w, float *resid, unsigned cap, hipStream_t s,
+                     const DevHotOut &ho) {
     const bool unit = bt.val == nullptr;
 #define DLR_MH(SEG)                                                                                            \
     case SEG: {                                                                                                \
         const unsigned grid = std::min<unsigned>(grid_for(bt.rows, NW * SEG), cap);                            \
         if (unit)                                                                                              \
             hipLaunchKernelGGL((k_margin_hot<HOT, NW, SEG, true>), dim3(grid), dim3(NW * kWave), 0, s, bt, w,   \
-                               resid);                                                                         \
+                               resid, ho);                                                                     \
         else                                                                                                   \
             hipLaunchKernelGGL((k_margin_hot<HOT, NW, SEG, false>), dim3(grid), dim3(NW * kWave), 0, s, bt, w,  \
-                               resid);                                                                         \
+                               resid, ho);                                                                     \
         break;                                                                                                 \
     }
     switch (margin_seg(bt)) {
@@ -3747,7 +3879,7 @@ hipError_t launch_mh(const DevBatch &bt, const float *w, float *resid, unsigned 
 }
 
 hipError_t launch_margin_hot(const DevBatch &bt, const float *w, int64_t D, float *resid, hipStream_t s,
-                             int reserve) {
+                             int reserve, const DevHotOut &ho) {
     if (bt.rows <= 0) return hipSuccess;
     static const int ncu_all = [] {
         int dev = 0, n = 0;
@@ -3774,13 +3906,13 @@ hipError_t launch_margin_hot(const DevBatch &bt, const float *w, int64_t D, floa
     // -- measured slower: 1.90 vs 1.76 ms, profiles/r02_c3_margin_ab.txt)
     // 24,576 x 16 (LDS: exactly 160 KiB) since the rare-column order: C3
     // margin 1.579 vs 1.601 ms for 16,384 x 16 (profiles/r03j_bench_c3_*.json)
-    if (shape == 0 && D >= 24576) return launch_mh<24576, 16>(bt, w, resid, (unsigned)ncu, s);
-    if ((shape == 0 || shape == 6) && D >= 16384) return launch_mh<16384, 16>(bt, w, resid, (unsigned)ncu, s);
-    if (shape == 2 && D >= 16384) return launch_mh<16384, 8>(bt, w, resid, (unsigned)ncu, s);
-    if (shape == 3 && D >= 24576) return launch_mh<24576, 8>(bt, w, resid, (unsigned)ncu, s);
-    if (shape == 4 && D >= 24576) return launch_mh<24576, 16>(bt, w, resid, (unsigned)ncu, s);
-    if (shape == 5 && D >= 20480) return launch_mh<20480, 16>(bt, w, resid, (unsigned)ncu, s);
-    return launch_mh<kMarginHot, kMarginHotWaves>(bt, w, resid, (unsigned)ncu * 2, s);
+    if (shape == 0 && D >= 24576) return launch_mh<24576, 16>(bt, w, resid, (unsigned)ncu, s, ho);
+    if ((shape == 0 || shape == 6) && D >= 16384) return launch_mh<16384, 16>(bt, w, resid, (unsigned)ncu, s, ho);
+    if (shape == 2 && D >= 16384) return launch_mh<16384, 8>(bt, w, resid, (unsigned)ncu, s, ho);
+    if (shape == 3 && D >= 24576) return launch_mh<24576, 8>(bt, w, resid, (unsigned)ncu, s, ho);
+    if (shape == 4 && D >= 24576) return launch_mh<24576, 16>(bt, w, resid, (unsigned)ncu, s, ho);
+    if (shape == 5 && D >= 20480) return launch_mh<20480, 16>(bt, w, resid, (unsigned)ncu, s, ho);
+    return launch_mh<kMarginHot, kMarginHotWaves>(bt, w, resid, (unsigned)ncu * 2, s, ho);
 }
 
 int predict_grid(int64_t rows) { return rows <= 0 ? 0 : (int)grid_for(rows, kWaves * kWave); }
@@ -4199,6 +4331,19 @@ hipError_t launch_band_hot(const DevBand &bd, const uint32_t *hw, int64_t nhot, 
     else
         DLR_BH(uint32_t, false);
 #undef DLR_BH
+    return hipGetLastError();
+}
+
+hipError_t launch_flag_store(uint32_t *flag, uint32_t seq, hipStream_t s) {
+    hipLaunchKernelGGL(k_flag_store, dim3(1), dim3(1), 0, s, flag, seq);
+    return hipGetLastError();
+}
+
+hipError_t launch_hot_chain(const DevHotChain &hc, float *gacc, hipStream_t s) {
+    if (hc.nh <= 0) return hipSuccess;
+    // 150 KB of LDS requested (the ring needs 32 KB): the workgroup holds its
+    // CU alone, so nothing shares the chain's SIMD (as k_band_hot)
+    hipLaunchKernelGGL(k_hot_chain, dim3((unsigned)hc.nh), dim3(128), kHotLds, s, hc, gacc);
     return hipGetLastError();
 }
 

@@ -50,7 +50,7 @@ SYMBOLS = [
     "dlr_summation_order",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
     "dlr_set_fault",
-    "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_train_band_rows", "dlr_train_relabeled", "dlr_train_unit_values", "dlr_train_product_margin", "dlr_train_row_rounds",
+    "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_train_band_rows", "dlr_train_relabeled", "dlr_train_unit_values", "dlr_train_product_margin", "dlr_train_hot_columns", "dlr_train_row_rounds",
     "dlr_set_exchange_overlap", "dlr_exchange_overlap", "dlr_set_exchange_pieces", "dlr_exchange_pieces",
     "dlr_memory_info", "dlr_stream_bytes",
 ]
@@ -169,6 +169,7 @@ _sig("dlr_train_band_rows", C.c_int, P)
 _sig("dlr_train_relabeled", C.c_int, P)
 _sig("dlr_train_unit_values", C.c_int, P)
 _sig("dlr_train_product_margin", C.c_int, P)
+_sig("dlr_train_hot_columns", C.c_int, P)
 _sig("dlr_train_row_rounds", C.c_int, P)
 _sig("dlr_set_exchange_overlap", C.c_int, P, C.c_int)
 _sig("dlr_exchange_overlap", C.c_int, P)
@@ -603,6 +604,14 @@ class Engine:
         rc = lib.dlr_train_unit_values(self._h)
         self._c(min(rc, 0))
         return rc == 1
+
+    def train_hot_columns(self) -> int:
+        """Hot columns whose chains run from the product stream (one
+        k_hot_chain launch per step), 0 = per-band k_band_hot or none
+        (dlr_train_hot_columns)."""
+        rc = lib.dlr_train_hot_columns(self._h)
+        self._c(min(rc, 0))
+        return rc
 
     def train_product_margin(self) -> int:
         """0: gather margin; 1: product margin with a separate pass 1; 2:

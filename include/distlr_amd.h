@@ -415,6 +415,17 @@ int dlr_train_unit_values(dlr_ctx *ctx);
  * Sigmoid_ dot product for these shards (same arithmetic). */
 int dlr_train_product_margin(dlr_ctx *ctx);
 
+/* Band mode, REFERENCE order: the hot columns (>= DLR_BAND_HOT entries in a
+ * batch, default 2^17: C3's Zipf heads) whose chains run from the HOT-COLUMN
+ * PRODUCT STREAM -- the margin kernel writes each hot product fl32(r_i *
+ * x_ij) as it computes r_i, and ONE launch per step adds every hot column's
+ * products in batch-row order over all bands (k_hot_chain) -- returns the
+ * most hot columns of a batch; 0 when the hot chains run per band from
+ * gathered residuals (k_band_hot: DLR_HOT_STREAM=0, more than 64 hot
+ * columns, or no LDS hot-weight margin) or there are none.  Same products,
+ * same order: lr.cc:35-39's sums either way. */
+int dlr_train_hot_columns(dlr_ctx *ctx);
+
 /* The gradient kernel of a product-margin shard: the number of 8,192-row
  * rounds of the ROW-ROUND gradient (k_grad_rt: the batch read in pass 1's
  * row-major order, products transposed into column order in LDS; default

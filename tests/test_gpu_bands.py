@@ -336,3 +336,83 @@ def test_long_phase_order_bitwise(monkeypatch, piece):
     short = counts <= BAND_LONG_COLUMN
     assert_same_weights(got[short], g_orc[short], "short-column gradient")
 
+
+
+def _hot_stream_run(ds, D, steps, hot, stream, band_rows="8192"):
+    import os as _os
+    env = {"DLR_BAND_ROWS": band_rows, "DLR_BAND_HOT": hot, "DLR_HOT_STREAM": stream, "DLR_GRAD_KERNEL": "classic"}
+    old = {k: _os.environ.get(k) for k in env}
+    _os.environ.update(env)
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(dlr.init_weight(D))
+        eng.load_train(ds, -1)
+        nh = eng.train_hot_columns()
+        for _ in range(steps):
+            eng.train_step(0, 0.2, 1.0)
+        return eng.get_weights(), nh
+    finally:
+        eng.close()
+        for k, v in old.items():
+            if v is None:
+                _os.environ.pop(k, None)
+            else:
+                _os.environ[k] = v
+
+
+@pytest.mark.parametrize("hot", ["2000", "6000"])
+def test_hot_stream_bitwise(hot):
+    # the hot columns' chains from the product stream (the margin writes
+    # fl32(r_i * x_ij) of each hot entry, ONE k_hot_chain launch adds every
+    # hot column over all bands, band s once its flag is up): bitwise the
+    # per-band k_band_hot chains (DLR_HOT_STREAM=0) and the oracle
+    D = 1 << 24
+    ds = _c3_shards(1, rows=80_000)[0]
+    got, nh = _hot_stream_run(ds, D, 3, hot, "1")
+    assert 0 < nh <= 64, nh
+    ref, nh0 = _hot_stream_run(ds, D, 3, hot, "0")
+    assert nh0 == 0
+    assert_same_weights(got, ref, "hot stream vs k_band_hot")
+    rp, col, val, lab = ds.csr()
+    w = dlr.init_weight(D)
+    for _ in range(3):
+        g = oracle.grad_csr((rp, col, val), lab, np.arange(len(lab)), w)
+        oracle.server_update(w, [g], 0.2)
+    assert_same_weights(got, w, "hot stream vs oracle")
+
+
+def test_hot_stream_valued_and_ragged_bands():
+    # fp32 values (the products r * x in the margin) and a last band of a
+    # few rows; bands of 4,096 rows so columns hold segments in many bands
+    D = 1 << 20
+    rng = np.random.default_rng(5)
+    n = 30_001
+    hot_cols = np.array([3, 17, 40000], dtype=np.int64)
+    rows, cols = [], []
+    for i in range(n):
+        c = set(rng.choice(D, 12, replace=False).tolist())
+        for h in hot_cols:
+            if rng.random() < 0.3:
+                c.add(int(h))
+        c = sorted(c)
+        rows.append(len(c))
+        cols.extend(c)
+    rp = np.concatenate([[0], np.cumsum(rows)]).astype(np.int64)
+    col = np.asarray(cols, dtype=np.int32)
+    val = rng.integers(1, 10001, size=len(col)).astype(np.float32) / np.float32(10000)
+    lab = rng.integers(0, 2, size=n).astype(np.int32)
+    ds = dlr.Dataset.from_csr(rp, col, val, lab, D)
+    import os as _os
+    _os.environ["DLR_MARGIN_HOT"] = "1"
+    try:
+        got, nh = _hot_stream_run(ds, D, 2, "5000", "1", band_rows="4096")
+        ref, _ = _hot_stream_run(ds, D, 2, "5000", "0", band_rows="4096")
+    finally:
+        _os.environ.pop("DLR_MARGIN_HOT", None)
+    assert nh == 3, nh
+    assert_same_weights(got, ref, "hot stream vs k_band_hot (valued)")
+    w = dlr.init_weight(D)
+    for _ in range(2):
+        g = oracle.grad_csr((rp, col, val), lab, np.arange(n), w)
+        oracle.server_update(w, [g], 0.2)
+    assert_same_weights(got, w, "hot stream vs oracle (valued)")

@@ -135,6 +135,26 @@ def test_band_hot_withheld_ring_raises(monkeypatch):
         eng.close()
 
 
+def test_hot_stream_withheld_ring_raises(monkeypatch):
+    # k_hot_chain (the hot columns' chains over every band from the product
+    # stream): its loader never posts a chunk -> the chain's wait runs out
+    monkeypatch.setenv("DLR_BAND_ROWS", "8192")
+    monkeypatch.setenv("DLR_BAND_HOT", "2000")
+    D = 1 << 24
+    ds = dlr.Dataset.generate_hashed(80_000, D, 39, seed=10, stream=1)
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(dlr.init_weight(D))
+        eng.load_train(ds, -1)
+        assert eng.train_hot_columns() > 0
+        eng.set_fault(dlr.FAULT_HOT_RING)
+        eng.train_step(0, 0.2, 1.0)
+        msg = _expect_device_error(eng.sync)
+        assert "k_hot_chain" in msg
+    finally:
+        eng.close()
+
+
 def test_set_fault_rejects_unknown():
     eng = dlr.Engine(16)
     try:
