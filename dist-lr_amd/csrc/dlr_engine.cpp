@@ -156,6 +156,7 @@ struct TrainShard {
     uint32_t *dref_sync = nullptr;
     uint32_t dref_seq = 0;
     int dref_lead = 0;
+    uint32_t dref_pace = 0;  // ticks of 10 ns
     // streamed dense shard (DLR_RESIDENCY_STREAM): X stays in the caller's
     // host memory (registered, pinned in place); each batch's rows and labels
     // are staged into one of two device slots on the copy stream
@@ -1044,15 +1045,24 @@ void build_bands(const std::vector<uint32_t> &cptr, const std::vector<RowT> &cro
 // its stream holds its products band by band, each band's segment starting
 // at a multiple of kHotChunkF floats (no chunk -- no cache line -- holds two
 // bands); row i's list gets one (stream slot, value) per hot entry.  Off
-// (DLR_HOT_STREAM=0, no hot column, or more than kHsMaxCols in a batch: the
+// (DLR_HOT_STREAM=0, no hot column, or more than hs_max_cols() in a batch: the
 // per-band k_band_hot launches instead).
-constexpr int64_t kHsMaxCols = 64;
+// (the hot stream's chains: kHcCols per CU.  C3 has 39 columns of ~1.55M
+// entries, 39 of ~724K, 273 more of >= 2^17: at most 40 / 78 / 128 / 256
+// of them in the stream, 5.70 / 5.71 / 5.72 / 6.53 ms per step -- the
+// margin's hot-product writes grow with them, the band kernels' chains
+// shrink; profiles/r05_c3_hot_stream_max.txt)
+static int64_t hs_max_cols() {
+    const char *e = getenv("DLR_HOT_STREAM_MAX");
+    return e ? std::max<int64_t>(1, atoll(e)) : 64;
+}
+
 bool hot_stream_wanted() {
     const char *e = getenv("DLR_HOT_STREAM");
     return !(e && strcmp(e, "0") == 0);
 }
-// The smallest threshold >= hot_min that leaves at most kHsMaxCols hot
-// columns in every batch (one k_hot_chain workgroup -- one CU -- each).
+// The smallest threshold >= hot_min that leaves at most hs_max_cols() hot
+// columns in every batch (dlr::hot_chain_grid: kHcCols chains per CU).
 int64_t hot_stream_threshold(const std::vector<uint32_t> &cptr, int64_t nb, int64_t D, int64_t hot_min) {
     int64_t thr = hot_min;
     for (int64_t b = 0; b < nb; ++b) {
@@ -1062,9 +1072,9 @@ int64_t hot_stream_threshold(const std::vector<uint32_t> &cptr, int64_t nb, int6
             const int64_t n = (int64_t)(cp[j + 1] & 0x7FFFFFFFu) - (int64_t)(cp[j] & 0x7FFFFFFFu);
             if (n >= hot_min) big.push_back(n);
         }
-        if ((int64_t)big.size() > kHsMaxCols) {
-            std::nth_element(big.begin(), big.begin() + kHsMaxCols, big.end(), std::greater<int64_t>());
-            thr = std::max(thr, big[(size_t)kHsMaxCols] + 1);  // the (kHsMaxCols+1)-th largest is not hot
+        if ((int64_t)big.size() > hs_max_cols()) {
+            std::nth_element(big.begin(), big.begin() + hs_max_cols(), big.end(), std::greater<int64_t>());
+            thr = std::max(thr, big[(size_t)hs_max_cols()] + 1);  // the (hs_max_cols()+1)-th largest is not hot
         }
     }
     return thr;
@@ -1082,7 +1092,7 @@ int build_hot_stream(dlr_ctx *c, const std::vector<uint32_t> &cptr, const std::v
         for (int64_t j = 0; j < D; ++j)
             if ((int64_t)(cp[j + 1] & 0x7FFFFFFFu) - (int64_t)(cp[j] & 0x7FFFFFFFu) >= hot_min && !(cp[j] & 0x80000000u))
                 hot[(size_t)b].push_back((uint32_t)j);
-        if ((int64_t)hot[(size_t)b].size() > kHsMaxCols) return DLR_OK;
+        if ((int64_t)hot[(size_t)b].size() > hs_max_cols()) return DLR_OK;
         any += (int64_t)hot[(size_t)b].size();
     }
     if (any == 0) return DLR_OK;
@@ -1946,7 +1956,7 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
         if (e == hipSuccess && t.dref) {
             const int64_t nw = dlr::dense_ref_sync_words(B);
             const dlr::DevRefSync sy{t.dref_sync, t.dref_sync + nw - 64, t.dref_sync + nw - 32, t.dref_seq,
-                                     t.dref_lead, 0, c->d_err, c->fault};
+                                     t.dref_lead, 0, c->d_err, c->fault, t.dref_pace};
             e = dlr::launch_dense_ref(dd, first, B, c->w, gout, c->resid, sy, lr, C, fused, c->stream);
             if (e == hipSuccess) ++c->train.dref_seq;
         } else if (e == hipSuccess)
@@ -2056,7 +2066,7 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
         const char *e = getenv("DLR_BAND_CUS");
         return e ? atoi(e) : 0;
     }();
-    const int margin_reserve = hs ? (int)nh + band_cus : hot ? (int)t.max_hot + band_cus : 0;
+    const int margin_reserve = hs ? dlr::hot_chain_grid(nh) + band_cus : hot ? (int)t.max_hot + band_cus : 0;
     if (hot && !c->hstream) {
         e = hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_hdone, hipEventDisableTiming);
@@ -2964,7 +2974,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             // 0 = none)
             const char *bh = getenv("DLR_BAND_HOT");
             int64_t hot_min = long_min == 0 ? (bh ? atoll(bh) : (int64_t)1 << 17) : 0;
-            // with the hot-column product stream: at most kHsMaxCols hot
+            // with the hot-column product stream: at most hs_max_cols() hot
             // columns a batch (the hottest; the others' chains run in
             // k_grad_band, band by band)
             if (hot_min > 0 && t.margin_hot && hot_stream_wanted())
@@ -3146,6 +3156,10 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
         // (DLR_DENSE_REF_LEAD: A/B; 0 = no limit)
         const char *dl = getenv("DLR_DENSE_REF_LEAD");
         t.dref_lead = dl ? atoi(dl) : 64;
+        // the first units' start pace in ns per unit (k_dense_ref, DevRefSync
+        // pace; DLR_DENSE_REF_PACE: A/B, 0 = all at once)
+        const char *dp = getenv("DLR_DENSE_REF_PACE");
+        t.dref_pace = (uint32_t)((dp ? atoi(dp) : 0) / 10);
     }
     t.fast = t.dblocked;
     // Residency: device-resident unless asked to stream, or (auto) the rows

@@ -240,6 +240,9 @@ struct DevRefSync {
     int mgrid;        // margin workgroups (set by launch_dense_ref)
     uint32_t *err = nullptr;  // DevErr words
     int fault = 0;            // kFaultRefPublish (tests)
+    // the launch's first units start paced: unit u's stream not before
+    // u x pace ticks (100 MHz) after its workgroup's start (0: all at once)
+    uint32_t pace = 0;
 };
 
 // Batch size of every rank (the L2 term of rank r's push is
@@ -286,6 +289,7 @@ struct DevHotChain {
 };
 constexpr int kHotChunkF = 256;  // floats of one stream chunk (a band segment starts at a multiple)
 hipError_t launch_hot_chain(const DevHotChain &hc, float *gacc, hipStream_t s);
+int hot_chain_grid(int64_t nh);  // workgroups (= CUs) of that launch
 // The same margins with w[0, kMarginHot) staged in LDS (frequency-ordered
 // shards; needs D >= kMarginHot); ho: the hot columns' products too.
 constexpr int kMarginHot = 8192;

@@ -2006,25 +2006,32 @@ __global__ __launch_bounds__(256) void k_band_hot(DevBand bd, const uint32_t *__
 // 0 adds them in order from +0, 32 per LDS wait, the next 32 in flight.  The
 // same products added in the same order: bitwise k_band_hot's (and the
 // oracle's) sums; the chain never waits on a gather.
-constexpr int kHcRing = 32;  // chunks of kHotChunkF floats in the ring
+constexpr int kHcRing = 32;  // chunks of kHotChunkF floats in a ring
 constexpr int kHcLA = 8;     // chunks a loader keeps in flight
+// hot columns per workgroup: chain waves 0..kHcCols-1 (one per SIMD), their
+// loaders waves kHcCols..2*kHcCols-1 (a loader's few instructions share its
+// chain's SIMD); a ring each.  One workgroup per CU (kHotLds).
+constexpr int kHcCols = 4;
+static_assert(kHcCols * (kHcRing * kHotChunkF * 4 + 16) <= (int)kHotLds, "the rings fit the workgroup's LDS");
 static_assert(kHotChunkF == kHotChunk, "one chunk size for both hot kernels");
 __global__ __launch_bounds__(1) void k_flag_store(uint32_t *flag, uint32_t seq) {
     __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(128) void k_hot_chain(DevHotChain hc, float *__restrict__ gacc) {
+__global__ __launch_bounds__(2 * kHcCols * kWave) void k_hot_chain(DevHotChain hc, float *__restrict__ gacc) {
     extern __shared__ __attribute__((aligned(16))) float hsm[];
-    float *ring = hsm;                                                     // [kHcRing][kHotChunkF]
-    uint32_t *ctl = reinterpret_cast<uint32_t *>(hsm + kHcRing * kHotChunkF);  // [0] landed, [1] consumed
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    if (threadIdx.x < 4) ctl[threadIdx.x] = 0u;
+    const int pr = wv % kHcCols;  // this wave's (chain, loader) pair
+    float *ring = hsm + pr * kHcRing * kHotChunkF;  // [kHcRing][kHotChunkF]
+    uint32_t *ctl = reinterpret_cast<uint32_t *>(hsm + kHcCols * kHcRing * kHotChunkF) + 4 * pr;  // landed, consumed
+    if (threadIdx.x < 4 * kHcCols) reinterpret_cast<uint32_t *>(hsm + kHcCols * kHcRing * kHotChunkF)[threadIdx.x] = 0u;
     __syncthreads();
-    const int64_t h = blockIdx.x;
+    const int64_t h = (int64_t)blockIdx.x * kHcCols + pr;
+    if (h >= hc.nh) return;  // wave-uniform (no barrier after this point)
     const uint2 *seg = hc.seg + h * hc.nbands;
     Spin spin(hc.err, kErrHotLds);
-    if (wv == 1) {
+    if (wv >= kHcCols) {
         // the loader: chunk g of the column's stream (bands in order) into
         // ring slot g % kHcRing; landed chunks are posted in order
         Spin fspin(hc.err, kErrHotFlag);
@@ -2059,7 +2066,6 @@ __global__ __launch_bounds__(128) void k_hot_chain(DevHotChain hc, float *__rest
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives its wave
         return;
     }
-    if (wv != 0) return;
     // the chain: the column's products in stream order from +0
     float acc = 0.0f;
     uint32_t pk = 0, g = 0;  // chunks known landed, chunks added
@@ -3512,6 +3518,7 @@ __device__ __forceinline__ void ref_margin_half(const DevDense &dd, int64_t firs
         // landed; stage g + 6 goes into the slot stage g - 1 used, once the
         // compute is past it.
         const int lw = mw;                    // loader 0..2: chunks lw, lw + 3, ...
+        const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
         const int npieces = lw == 2 ? 5 : 6;  // of the 16 + 1 (6 + 5 + 5, and loader 1 the weights)
         uint32_t compk = 0;  // stages the compute is known to be past
         int kc = -1;         // the unit whose id uc is
@@ -3523,6 +3530,15 @@ __device__ __forceinline__ void ref_margin_half(const DevDense &dd, int64_t firs
                 ctl_wait_ge(ctl + kCtlIds, (uint32_t)k + 1, spin);
                 uc = ctl_read(s_unit + (k & 3));
                 kc = k;
+                // the first units of the launch start paced, unit u at u x
+                // pace: the first slots' rows are not streamed 1/256th of
+                // HBM at a time beside every other CU's first unit (they
+                // would all land ~50 us in, and the column chains wait for
+                // slot 0 that long); later units start as earlier ones end
+                if (k == 0 && sy.pace > 0 && uc != kRefNone) {
+                    const uint64_t until = t_start + (uint64_t)uc * sy.pace;
+                    while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(4);
+                }
             }
             const uint32_t u = uc;
             const int64_t i = min((int64_t)(u == kRefNone ? 0 : u) * kRefUnit + lane, B - 1);
@@ -4339,11 +4355,14 @@ hipError_t launch_flag_store(uint32_t *flag, uint32_t seq, hipStream_t s) {
     return hipGetLastError();
 }
 
+int hot_chain_grid(int64_t nh) { return (int)((nh + kHcCols - 1) / kHcCols); }
+
 hipError_t launch_hot_chain(const DevHotChain &hc, float *gacc, hipStream_t s) {
     if (hc.nh <= 0) return hipSuccess;
     // 150 KB of LDS requested (the ring needs 32 KB): the workgroup holds its
     // CU alone, so nothing shares the chain's SIMD (as k_band_hot)
-    hipLaunchKernelGGL(k_hot_chain, dim3((unsigned)hc.nh), dim3(128), kHotLds, s, hc, gacc);
+    hipLaunchKernelGGL(k_hot_chain, dim3((unsigned)hot_chain_grid(hc.nh)), dim3(2 * kHcCols * kWave), kHotLds, s, hc,
+                       gacc);
     return hipGetLastError();
 }
 

@@ -369,7 +369,7 @@ def test_hot_stream_bitwise(hot):
     D = 1 << 24
     ds = _c3_shards(1, rows=80_000)[0]
     got, nh = _hot_stream_run(ds, D, 3, hot, "1")
-    assert 0 < nh <= 64, nh
+    assert 0 < nh <= 128, nh
     ref, nh0 = _hot_stream_run(ds, D, 3, hot, "0")
     assert nh0 == 0
     assert_same_weights(got, ref, "hot stream vs k_band_hot")
