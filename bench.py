@@ -118,6 +118,9 @@ def parse_args():
                          "one per 4 MiB of a rank's key range, 1 to 4)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stage-pass", action="store_true",
+                    help="skip the per-stage roofline pass (PMC runs: every kernel then belongs to a whole step; "
+                         "the roofline uses the step time)")
     ap.add_argument("--mode", choices=["mean", "last", "async"], default="mean",
                     help="server update rule (main.cc:57-84): sync mean (default), sync last push, async")
     ap.add_argument("--spawn", action="store_true", help="use the process launcher even at --gpus 1")
@@ -651,10 +654,10 @@ def run_rank(args):
     # (A streamed shard is bound by the batch copies instead: no stage pass.)
     k0 = args.warmup + (4 if overlap else 2) * args.steps
     stage_us = {}
-    if not streamed:
+    if not streamed and not args.no_stage_pass:
         stage_us = {"margin": eng.stage_time(dlr.STAGE_MARGIN, k0 % nb, args.steps, args.lr) * 1000.0,
                     "gradient": eng.stage_time(dlr.STAGE_GRADIENT, k0 % nb, args.steps, args.lr) * 1000.0}
-    if layout == "touched":
+    if layout == "touched" and not args.no_stage_pass:
         stage_us["update"] = eng.stage_time(dlr.STAGE_UPDATE, k0 % nb, args.steps, args.lr) * 1000.0
     B_eff = B if B > 0 else args.rows                 # B = -1: the full shard per step
     samples = world * args.steps * B_eff
@@ -667,8 +670,9 @@ def run_rank(args):
     # itself; the roofline then uses the step's own time
     stage_sum_us = sum(stage_us.values()) + (avg_us["merge"] if world > 1 and layout != "touched" else 0.0)
     step_us = el / args.steps * 1e6
-    kern_us = min(stage_sum_us, step_us) if stage_sum_us > 0 else 0.0
-    time_basis = "step time (stages overlap)" if stage_sum_us > step_us else "sum of the stage averages"
+    kern_us = min(stage_sum_us, step_us) if stage_sum_us > 0 else step_us
+    time_basis = ("step time (no stage pass)" if stage_sum_us <= 0 else
+                  "step time (stages overlap)" if stage_sum_us > step_us else "sum of the stage averages")
     unit = args.kind != "dense" and eng.train_unit_values()
     step_bytes = alg_bytes_per_step(B_eff, nnz_avg, D, args.kind == "dense", unit)
     achieved = step_bytes / (kern_us * 1e-6) / 1e9 if kern_us > 0 else 0.0

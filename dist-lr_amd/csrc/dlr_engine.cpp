@@ -156,7 +156,6 @@ struct TrainShard {
     uint32_t *dref_sync = nullptr;
     uint32_t dref_seq = 0;
     int dref_lead = 0;
-    uint32_t dref_pace = 0;  // ticks of 10 ns
     // streamed dense shard (DLR_RESIDENCY_STREAM): X stays in the caller's
     // host memory (registered, pinned in place); each batch's rows and labels
     // are staged into one of two device slots on the copy stream
@@ -199,7 +198,7 @@ struct TrainShard {
     bool hs = false;
     std::vector<int64_t> hs_nh, hsco, hsso, hsoo;
     uint32_t *hs_cols = nullptr, *hs_off = nullptr, *hs_dest = nullptr, *hs_flag = nullptr;
-    uint2 *hs_seg = nullptr;
+    uint2 *hs_seg = nullptr, *hs_state = nullptr;
     float *hs_val = nullptr, *hs_buf = nullptr;
     uint32_t hs_seq = 0;
     int64_t hs_bytes = 0;
@@ -469,7 +468,7 @@ void free_train(dlr_ctx *c) {
                     (void *)t.lcols, (void *)t.lcseg, (void *)t.lsptr, t.lrow, (void *)t.lval, (void *)t.lpart, (void *)t.lsched,
                     (void *)t.dX, (void *)t.dpart, (void *)t.wsched, (void *)t.bcols, (void *)t.bptr,
                     (void *)t.bws, (void *)t.bhw, (void *)t.hs_cols, (void *)t.hs_off, (void *)t.hs_dest,
-                    (void *)t.hs_flag, (void *)t.hs_seg, (void *)t.hs_val, (void *)t.hs_buf, t.brow, (void *)t.bval, (void *)t.gacc, (void *)t.lpdesc, (void *)t.lpptr,
+                    (void *)t.hs_flag, (void *)t.hs_seg, (void *)t.hs_state, (void *)t.hs_val, (void *)t.hs_buf, t.brow, (void *)t.bval, (void *)t.gacc, (void *)t.lpdesc, (void *)t.lpptr,
                     (void *)t.lpslot, (void *)t.lpws, (void *)t.lprow, (void *)t.lpval, (void *)t.pm_lbeg,
                     (void *)t.pm_list, (void *)t.pm_pofs, (void *)t.pm_rg, (void *)t.pm_qoff, (void *)t.pm_val,
                     (void *)t.pm_p, (void *)t.pm_qs, (void *)t.xslices, (void *)t.rt_gq, (void *)t.rt_val,
@@ -1052,6 +1051,10 @@ void build_bands(const std::vector<uint32_t> &cptr, const std::vector<RowT> &cro
 // of them in the stream, 5.70 / 5.71 / 5.72 / 6.53 ms per step -- the
 // margin's hot-product writes grow with them, the band kernels' chains
 // shrink; profiles/r05_c3_hot_stream_max.txt)
+// A band flag not seen for this long ends the first k_hot_chain launch (the
+// resume launch finishes the chains): far above the ~0.1-0.3 ms between
+// flags when the margins run beside it, far below the 250 ms error bound
+constexpr uint32_t kHsGiveUpTicks = 2000000;  // 20 ms at 100 MHz
 static int64_t hs_max_cols() {
     const char *e = getenv("DLR_HOT_STREAM_MAX");
     return e ? std::max<int64_t>(1, atoll(e)) : 64;
@@ -1173,6 +1176,9 @@ int build_hot_stream(dlr_ctx *c, const std::vector<uint32_t> &cptr, const std::v
     if ((r = dev_alloc(c, (void **)&t.hs_buf, (size_t)(buf_need + dlr::kHotChunkF) * 4))) return r;
     std::vector<uint32_t> zero((size_t)max_bands, 0);
     if ((r = upload(c, &t.hs_flag, zero.data(), zero.size()))) return r;
+    int64_t nh_max = 1;
+    for (int64_t x : t.hs_nh) nh_max = std::max(nh_max, x);
+    if ((r = dev_alloc(c, (void **)&t.hs_state, (size_t)nh_max * 8))) return r;
     t.hs_seq = 0;
     t.hs = true;
     t.hs_bytes = (int64_t)((cols.size() + off.size() + dest.size() + val.size()) * 4 + seg.size() * 8 +
@@ -1956,7 +1962,7 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
         if (e == hipSuccess && t.dref) {
             const int64_t nw = dlr::dense_ref_sync_words(B);
             const dlr::DevRefSync sy{t.dref_sync, t.dref_sync + nw - 64, t.dref_sync + nw - 32, t.dref_seq,
-                                     t.dref_lead, 0, c->d_err, c->fault, t.dref_pace};
+                                     t.dref_lead, 0, c->d_err, c->fault};
             e = dlr::launch_dense_ref(dd, first, B, c->w, gout, c->resid, sy, lr, C, fused, c->stream);
             if (e == hipSuccess) ++c->train.dref_seq;
         } else if (e == hipSuccess)
@@ -2088,10 +2094,11 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
     if (e == hipSuccess) e = hipStreamWaitEvent(c->gstream, c->ev_bstart, 0);
     if (e == hipSuccess && hot) e = hipStreamWaitEvent(c->hstream, c->ev_bstart, 0);
     dlr::DevHotOut ho{};
+    dlr::DevHotChain hc{};
     if (hs) {
         ++t.hs_seq;
-        const dlr::DevHotChain hc{t.hs_cols + t.hsco[bb], t.hs_seg + t.hsso[bb], t.hs_buf, t.hs_flag, nh, nbands,
-                                  t.hs_seq, c->d_err, c->fault};
+        hc = dlr::DevHotChain{t.hs_cols + t.hsco[bb], t.hs_seg + t.hsso[bb], t.hs_buf, t.hs_flag, nh, nbands,
+                              t.hs_seq, c->d_err, c->fault, t.hs_state, 0, kHsGiveUpTicks};
         if (e == hipSuccess) e = dlr::launch_hot_chain(hc, t.gacc, c->hstream);
         ho = dlr::DevHotOut{t.hs_off + t.hsoo[bb], t.hs_dest, t.hs_val, t.hs_buf};
     }
@@ -2125,6 +2132,13 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
     if (e == hipSuccess) e = launch_long_columns(c, b, B, gout, lr, C, fused);
     if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_bdone, 0);
     if (e == hipSuccess && hot) e = hipStreamWaitEvent(c->stream, c->ev_hdone, 0);
+    // the hot chains the first launch could not finish (it gives up on a
+    // flag when the margins cannot run beside it; DevHotChain): after every
+    // margin and that launch -- nothing to do in a concurrent run
+    if (e == hipSuccess && hs) {
+        hc.resume = 1;
+        e = dlr::launch_hot_chain(hc, t.gacc, c->stream);
+    }
     if (e == hipSuccess) e = dlr::launch_band_finalize(t.gacc, c->w, gout, c->D, B, lr, C, fused, c->stream);
     return e;
 }
@@ -3156,10 +3170,6 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
         // (DLR_DENSE_REF_LEAD: A/B; 0 = no limit)
         const char *dl = getenv("DLR_DENSE_REF_LEAD");
         t.dref_lead = dl ? atoi(dl) : 64;
-        // the first units' start pace in ns per unit (k_dense_ref, DevRefSync
-        // pace; DLR_DENSE_REF_PACE: A/B, 0 = all at once)
-        const char *dp = getenv("DLR_DENSE_REF_PACE");
-        t.dref_pace = (uint32_t)((dp ? atoi(dp) : 0) / 10);
     }
     t.fast = t.dblocked;
     // Residency: device-resident unless asked to stream, or (auto) the rows

@@ -126,7 +126,7 @@ enum DevErr {
     kErrRefLimit = 2,   // k_dense_ref: the chains' limit never reached a margin unit
     kErrRefLds = 3,     // k_dense_ref: a hand-off between the waves of a workgroup
     kErrHotLds = 4,     // k_band_hot / k_hot_chain: a hand-off between the waves of a workgroup
-    kErrHotFlag = 5,    // k_hot_chain: a band's hot products were never published
+    kErrHotFlag = 5,    // k_hot_chain (resume launch): a band's hot products were never published
     kErrWords = 8
 };
 // Test-only fault injection (dlr_set_fault): a producer that never comes.
@@ -240,9 +240,6 @@ struct DevRefSync {
     int mgrid;        // margin workgroups (set by launch_dense_ref)
     uint32_t *err = nullptr;  // DevErr words
     int fault = 0;            // kFaultRefPublish (tests)
-    // the launch's first units start paced: unit u's stream not before
-    // u x pace ticks (100 MHz) after its workgroup's start (0: all at once)
-    uint32_t pace = 0;
 };
 
 // Batch size of every rank (the L2 term of rank r's push is
@@ -277,6 +274,12 @@ hipError_t launch_flag_store(uint32_t *flag, uint32_t seq, hipStream_t s);
 // products streamed from buf in order, band s once flag[s] >= seq; chain
 // sum from +0 in batch-row order; the sum stored to gacc[cols[h]].  seg:
 // per (column h, band s) the segment's (start, count) in buf, h-major.
+// The flags need the margins to run BESIDE this launch.  Where kernels are
+// serialised instead (e.g. under counter collection) a flag that does not
+// come within `giveup` ticks (100 MHz) ends the launch: each column's first
+// band not added and its sum so far go to state[h], and a RESUME launch
+// (resume = 1), queued after the last margin, adds the rest -- the same
+// chain, so the same bits.  The first launch always writes state.
 struct DevHotChain {
     const uint32_t *cols;
     const uint2 *seg;
@@ -286,6 +289,9 @@ struct DevHotChain {
     uint32_t seq;
     uint32_t *err;
     int fault;
+    uint2 *state;  // nh: (first band not added, the sum's bits)
+    int resume;
+    uint32_t giveup;
 };
 constexpr int kHotChunkF = 256;  // floats of one stream chunk (a band segment starts at a multiple)
 hipError_t launch_hot_chain(const DevHotChain &hc, float *gacc, hipStream_t s);

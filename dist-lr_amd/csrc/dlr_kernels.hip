@@ -2024,29 +2024,63 @@ __global__ __launch_bounds__(2 * kHcCols * kWave) void k_hot_chain(DevHotChain h
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int pr = wv % kHcCols;  // this wave's (chain, loader) pair
     float *ring = hsm + pr * kHcRing * kHotChunkF;  // [kHcRing][kHotChunkF]
-    uint32_t *ctl = reinterpret_cast<uint32_t *>(hsm + kHcCols * kHcRing * kHotChunkF) + 4 * pr;  // landed, consumed
+    // per pair: [0] chunks landed, [1] chunks added, [2] bands whose flag the
+    // loader has seen (bit 31: it gave up at that band)
+    uint32_t *ctl = reinterpret_cast<uint32_t *>(hsm + kHcCols * kHcRing * kHotChunkF) + 4 * pr;
     if (threadIdx.x < 4 * kHcCols) reinterpret_cast<uint32_t *>(hsm + kHcCols * kHcRing * kHotChunkF)[threadIdx.x] = 0u;
     __syncthreads();
     const int64_t h = (int64_t)blockIdx.x * kHcCols + pr;
     if (h >= hc.nh) return;  // wave-uniform (no barrier after this point)
     const uint2 *seg = hc.seg + h * hc.nbands;
+    // the resume launch continues where the first one stopped (state[h]:
+    // the first band not added, the chain's sum so far); nothing if it ended
+    int64_t s0 = 0;
+    float acc0 = 0.0f;
+    if (hc.resume) {
+        const uint2 st = hc.state[h];
+        s0 = st.x;
+        acc0 = __uint_as_float(st.y);
+        if (s0 >= hc.nbands) return;
+    }
     Spin spin(hc.err, kErrHotLds);
     if (wv >= kHcCols) {
         // the loader: chunk g of the column's stream (bands in order) into
         // ring slot g % kHcRing; landed chunks are posted in order
-        Spin fspin(hc.err, kErrHotFlag);
         const __amdgpu_buffer_rsrc_t frs =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(hc.flag), 0, 0x7FFFFFFF, 0x00020000);
         uint32_t g = 0, landed = 0, ck = 0;  // chunks issued, posted landed, known consumed
-        for (int64_t s = 0; s < hc.nbands; ++s) {
+        for (int64_t s = s0; s < hc.nbands; ++s) {
             const uint2 sg = seg[s];
             const uint32_t nch = (sg.y + kHotChunkF - 1) / kHotChunkF;
-            if (nch == 0) continue;
-            for (int k = 0;; ++k) {  // the band's products are published
-                const uint32_t f = __builtin_amdgcn_raw_buffer_load_b32(frs, (int)(s * 4), 0, 16);
-                if ((int32_t)(__builtin_amdgcn_readfirstlane(f) - hc.seq) >= 0 || !fspin.more(k)) break;
-                __builtin_amdgcn_s_sleep(8);
+            if (nch > 0) {
+                // the band's products are published -- or, after kGiveUp
+                // without them (the margins cannot run beside this launch:
+                // kernels serialised, e.g. under counter collection), the
+                // rest is left to the resume launch, which the engine queues
+                // after the last margin
+                bool up = false;
+                uint64_t t0 = 0;
+                for (int k = 0;; ++k) {
+                    const uint32_t f = __builtin_amdgcn_raw_buffer_load_b32(frs, (int)(s * 4), 0, 16);
+                    if ((int32_t)(__builtin_amdgcn_readfirstlane(f) - hc.seq) >= 0) {
+                        up = true;
+                        break;
+                    }
+                    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+                    if (k == 0) t0 = t;
+                    if (t - t0 > hc.giveup) break;
+                    __builtin_amdgcn_s_sleep(8);
+                }
+                if (!up) {
+                    // (the resume launch runs after every margin: a flag it
+                    // does not see is an error)
+                    if (hc.resume && hc.err && lane == 0)
+                        __hip_atomic_store(hc.err + kErrHotFlag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (lane == 0) ctl_post(ctl + 2, 0x80000000u | (uint32_t)(s - s0));
+                    break;
+                }
             }
+            if (lane == 0) ctl_post(ctl + 2, (uint32_t)(s - s0 + 1));
             for (uint32_t c = 0; c < nch; ++c, ++g) {
                 if (g >= (uint32_t)kHcRing && (int32_t)(ck - (g - kHcRing + 1)) < 0)
                     ck = ctl_poll(ctl + 1, g - kHcRing + 1, spin);  // the slot's last chunk was added
@@ -2066,9 +2100,10 @@ __global__ __launch_bounds__(2 * kHcCols * kWave) void k_hot_chain(DevHotChain h
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives its wave
         return;
     }
-    // the chain: the column's products in stream order from +0
-    float acc = 0.0f;
-    uint32_t pk = 0, g = 0;  // chunks known landed, chunks added
+    // the chain: the column's products in stream order, from +0 (or the
+    // first launch's sum)
+    float acc = acc0;
+    uint32_t pk = 0, g = 0, bk = 0;  // chunks known landed, chunks added, loader's band word
     auto rd = [&](v4f(&d)[8], const float *q) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) d[u] = *reinterpret_cast<const v4f *>(q + 4 * u);
@@ -2083,7 +2118,18 @@ __global__ __launch_bounds__(2 * kHcCols * kWave) void k_hot_chain(DevHotChain h
         }
     };
     v4f da[8], db[8];
-    for (int64_t s = 0; s < hc.nbands; ++s) {
+    int64_t s = s0;
+    for (; s < hc.nbands; ++s) {
+        // the loader is past band s's flag, or gave up before it
+        const uint32_t want = (uint32_t)(s - s0 + 1);
+        if ((bk & 0x7FFFFFFFu) < want && !(bk & 0x80000000u)) {
+            bk = ctl_read(ctl + 2);
+            for (int k = 0; (bk & 0x7FFFFFFFu) < want && !(bk & 0x80000000u) && spin.more(k); ++k) {
+                __builtin_amdgcn_s_sleep(1);
+                bk = ctl_read(ctl + 2);
+            }
+        }
+        if ((bk & 0x7FFFFFFFu) < want) break;  // gave up here: the resume launch adds the rest
         const uint2 sg = seg[s];
         const uint32_t nfull = sg.y / kHotChunkF, rem = sg.y % kHotChunkF;
         if (nfull > 0) {
@@ -2115,7 +2161,10 @@ __global__ __launch_bounds__(2 * kHcCols * kWave) void k_hot_chain(DevHotChain h
             ++g;
         }
     }
-    if (lane == 0) gacc[hc.cols[h]] = acc;
+    if (lane == 0) {
+        if (s >= hc.nbands) gacc[hc.cols[h]] = acc;
+        if (!hc.resume) hc.state[h] = make_uint2((uint32_t)s, __float_as_uint(acc));
+    }
 }
 
 // Long columns in ROW PHASES (band mode).  The chunked long path gathers
@@ -3518,7 +3567,6 @@ __device__ __forceinline__ void ref_margin_half(const DevDense &dd, int64_t firs
         // landed; stage g + 6 goes into the slot stage g - 1 used, once the
         // compute is past it.
         const int lw = mw;                    // loader 0..2: chunks lw, lw + 3, ...
-        const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
         const int npieces = lw == 2 ? 5 : 6;  // of the 16 + 1 (6 + 5 + 5, and loader 1 the weights)
         uint32_t compk = 0;  // stages the compute is known to be past
         int kc = -1;         // the unit whose id uc is
@@ -3530,15 +3578,6 @@ __device__ __forceinline__ void ref_margin_half(const DevDense &dd, int64_t firs
                 ctl_wait_ge(ctl + kCtlIds, (uint32_t)k + 1, spin);
                 uc = ctl_read(s_unit + (k & 3));
                 kc = k;
-                // the first units of the launch start paced, unit u at u x
-                // pace: the first slots' rows are not streamed 1/256th of
-                // HBM at a time beside every other CU's first unit (they
-                // would all land ~50 us in, and the column chains wait for
-                // slot 0 that long); later units start as earlier ones end
-                if (k == 0 && sy.pace > 0 && uc != kRefNone) {
-                    const uint64_t until = t_start + (uint64_t)uc * sy.pace;
-                    while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(4);
-                }
             }
             const uint32_t u = uc;
             const int64_t i = min((int64_t)(u == kRefNone ? 0 : u) * kRefUnit + lane, B - 1);

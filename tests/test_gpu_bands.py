@@ -416,3 +416,31 @@ def test_hot_stream_valued_and_ragged_bands():
         g = oracle.grad_csr((rp, col, val), lab, np.arange(n), w)
         oracle.server_update(w, [g], 0.2)
     assert_same_weights(got, w, "hot stream vs oracle (valued)")
+
+
+def test_hot_stream_serialised_kernels_resume(tmp_path):
+    # the hot chains' first launch needs the margins to run beside it (their
+    # flags); with every kernel serialised (AMD_SERIALIZE_KERNEL=3, as under
+    # counter collection) it gives up on band 0's flag and the resume launch
+    # -- queued after the last margin -- adds every band: the same bits
+    import subprocess
+    import sys
+    D = 1 << 24
+    ds = _c3_shards(1, rows=80_000)[0]
+    got, nh = _hot_stream_run(ds, D, 2, "2000", "1")
+    assert nh > 0
+    out = tmp_path / "w.npy"
+    code = (
+        "import sys, numpy as np\n"
+        "sys.path.insert(0, %r); sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+        "import test_gpu_bands as t, distlr_amd as dlr\n"
+        "ds = t._c3_shards(1, rows=80_000)[0]\n"
+        "w, nh = t._hot_stream_run(ds, 1 << 24, 2, '2000', '1')\n"
+        "assert nh > 0\n"
+        "np.save(%r, w)\n"
+    ) % (os.path.dirname(os.path.abspath(__file__)), os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "dist-lr_amd"), os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "oracle"), str(out))
+    env = dict(os.environ, AMD_SERIALIZE_KERNEL="3")
+    subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=240)
+    assert_same_weights(np.load(out), got, "serialised kernels (resume launch) vs concurrent")

@@ -287,3 +287,20 @@ def test_sparse_layouts_two_ranks_valued(monkeypatch, layout, B):
     got = run_group(shards, D, 2, B, 0.1, mode=dlr.MODE_SYNC_MEAN)
     orc = oracle.run_worker([_csr(s) for s in shards], D, 2, B, 0.1)
     compare_runs(got, orc)
+
+
+def test_rank_failing_mid_load_releases_its_peers(monkeypatch):
+    # a rank that fails AFTER the load agreement (here: DLR_PM=1
+    # and its rows are too long for the product margin) must not leave its
+    # peer blocked in the load's later collectives: it aborts the group
+    # (run_group's error path), and the peer's load fails with the reason
+    monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
+    monkeypatch.setenv("DLR_PM", "1")
+    import time
+    D = 300_000
+    ok = dlr.Dataset.generate(1200, D, 18, value_mode=1, seed=13, stream=1)
+    too_long = dlr.Dataset.generate(1200, D, 200, value_mode=1, seed=13, stream=2)  # > 128 entries a row
+    t0 = time.perf_counter()
+    with pytest.raises(dlr.DLRError):
+        run_group([ok, too_long], D, 1, 300, 0.2)
+    assert time.perf_counter() - t0 < 120, "the peer waited for the loopback timeout"

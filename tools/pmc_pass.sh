@@ -17,7 +17,8 @@ for pass in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
       "$R/tools/kbench/kbench" 65536 1000000 50 40 calib > "$R/$PD/calib_$tag.log" 2>&1 || exit 1
   echo "== pass $tag (bench)"
   timeout -s KILL 400 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d "$R/$PD/bench_$tag" -o run -- \
-      python3 "$R/bench.py" ${CONFIG:+--config $CONFIG} --steps $STEPS --warmup ${WARMUP:-5} --no-cpu-baseline > "$R/$PD/bench_$tag.json" \
+      python3 "$R/bench.py" ${CONFIG:+--config $CONFIG} --steps $STEPS --warmup ${WARMUP:-5} --no-cpu-baseline \
+      ${NO_STAGES:+--no-stage-pass} > "$R/$PD/bench_$tag.json" \
       2> "$R/$PD/bench_$tag.err" || exit 1
 done
 echo "pmc passes done"
