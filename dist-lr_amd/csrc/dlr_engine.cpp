@@ -101,6 +101,13 @@ struct TrainShard {
     // batch's pass 2 (DevP2): pm_cnt its hand-off counters, pm_gen the
     // launches so far.
     bool pm = false, pm_fused = false, pm_mg = false;
+    // band mode (classic layout, batches of >= 2^21 rows: C2 at B = -1): the
+    // margin as the product margin over WINDOWS of kPmWinRows rows (pass 1 +
+    // pass 2 per window; the weights do not change inside the step); the
+    // DevPm arrays are the windows', window w of batch b at index
+    // pmw_first[b] + w
+    bool pmw = false;
+    std::vector<int64_t> pmw_first;
     uint32_t *pm_cnt = nullptr;
     uint32_t pm_gen = 0;
     int64_t pmS = 0;
@@ -1055,6 +1062,9 @@ void build_bands(const std::vector<uint32_t> &cptr, const std::vector<RowT> &cro
 // resume launch finishes the chains): far above the ~0.1-0.3 ms between
 // flags when the margins run beside it, far below the 250 ms error bound
 constexpr uint32_t kHsGiveUpTicks = 2000000;  // 20 ms at 100 MHz
+// rows of a window of the band-mode product margin (TrainShard::pmw): the
+// product margin's 1,024 blocks of 64 rows
+constexpr int64_t kPmWinRows = (int64_t)dlr::kPmMaxBlocks * dlr::kPmRows;
 static int64_t hs_max_cols() {
     const char *e = getenv("DLR_HOT_STREAM_MAX");
     return e ? std::max<int64_t>(1, atoll(e)) : 64;
@@ -1872,6 +1882,28 @@ hipError_t dense_batch_done(dlr_ctx *c, int64_t b) {
     return e;
 }
 
+// The windowed product margin (TrainShard::pmw) of rows [r0, r1) of batch b
+// (r0 a multiple of kPmWinRows): per window, pass 1 from the current
+// weights, then pass 2 into resid.  Same products and order as every margin:
+// bitwise.
+hipError_t launch_pm_windows(dlr_ctx *c, int64_t b, int64_t r0, int64_t r1) {
+    const TrainShard &t = c->train;
+    const dlr::DevBatch all = batch_view(c, b);
+    r1 = std::min(r1, all.rows);
+    hipError_t e = hipSuccess;
+    for (int64_t wr0 = r0; e == hipSuccess && wr0 < r1; wr0 += kPmWinRows) {
+        const int64_t wi = t.pmw_first[(size_t)b] + wr0 / kPmWinRows;
+        dlr::DevBatch sub = all;
+        sub.row_ptr = all.row_ptr + wr0;
+        sub.label = all.label + wr0;
+        sub.rows = std::min(kPmWinRows, all.rows - wr0);
+        const dlr::DevPm pm = pm_view(c, wi);
+        e = dlr::launch_pm_products(pm, c->w, c->D, t.pm_p, c->stream);
+        if (e == hipSuccess) e = dlr::launch_pm_margin(pm, sub, t.pm_p, c->resid + wr0, c->stream);
+    }
+    return e;
+}
+
 // Whether batch b's pass 2 runs inside its fused gradient launch (one rank,
 // k_grad_lds MG): launch_margin then forms only the products, if missing.
 bool pm_mg_ok(const dlr_ctx *c, int64_t b) {
@@ -1907,6 +1939,7 @@ hipError_t launch_margin(dlr_ctx *c, int64_t b, bool rowsum_only = false, bool m
         return dlr::launch_pm_margin(pm_view(c, b), batch_view(c, b), t.pm_p, c->resid, c->stream);
     }
     if (t.margin_hot) return dlr::launch_margin_hot(batch_view(c, b), c->w, c->D, c->resid, c->stream);
+    if (t.pmw) return launch_pm_windows(c, b, 0, t.plan[(size_t)b].rows);
     return dlr::launch_margin_residual(batch_view(c, b), c->w, c->resid, c->stream);
 }
 
@@ -2112,6 +2145,7 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
         dlr::DevHotOut hk = ho;
         if (hk.off) hk.off += r0;  // the band's rows
         e = t.margin_hot ? dlr::launch_margin_hot(sub, c->w, c->D, c->resid + r0, c->stream, margin_reserve, hk)
+            : t.pmw      ? launch_pm_windows(c, b, r0, r1)
                          : dlr::launch_margin_residual(sub, c->w, c->resid + r0, c->stream);
         if (e == hipSuccess && hs) e = dlr::launch_flag_store(t.hs_flag + k, t.hs_seq, c->stream);
         if (e == hipSuccess) e = hipEventRecord(c->ev_band[(size_t)k], c->stream);
@@ -2141,6 +2175,142 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
     }
     if (e == hipSuccess) e = dlr::launch_band_finalize(t.gacc, c->w, gout, c->D, B, lr, C, fused, c->stream);
     return e;
+}
+
+// The product margin's arrays (DevPm, and the row-round gradient's DevRt
+// when allow_rt) for `spans` -- a shard's batches (their index is the
+// batch's), or the 65,536-row WINDOWS of band-mode batches (TrainShard::
+// pmw) -- uploaded back to back; built = false (nothing uploaded) when a
+// span does not fit them or they would not leave the residency headroom
+// (force: DLR_PM=1, that is an error).
+int build_pm(dlr_ctx *c, const CsrView &src, const std::vector<dlr::BatchSpan> &spans, bool allow_rt, bool force,
+             int nthreads, int64_t &resid_need, int64_t &csc_bytes, bool &built) {
+    TrainShard &t = c->train;
+    const int64_t ns = (int64_t)spans.size(), D = c->D;
+    const int64_t S = (D + dlr::kPmSlice - 1) / dlr::kPmSlice;
+    int rc;
+    built = false;
+    std::vector<PmBatch> pm((size_t)ns);
+    std::atomic<bool> ok{true};
+    // the row-round gradient: by default for batches of <= 2 rounds
+    // (C2 at B = 8,192: 7.5 vs 10.0 us for k_grad_lds); at 8 rounds
+    // (B = 65,536) k_grad_lds is faster.  DLR_GRAD_RT=1
+    // takes it for every batch that fits, =0 never.
+    const char *rte = getenv("DLR_GRAD_RT");
+    int64_t maxrows = 0;
+    for (const dlr::BatchSpan &sp : spans) maxrows = std::max(maxrows, sp.rows);
+    const int64_t rounds = (maxrows + dlr::kRtRows - 1) / dlr::kRtRows;
+    const bool want_rt = allow_rt && rounds <= dlr::kRtMaxRounds &&
+                         (rte ? strcmp(rte, "0") != 0 : rounds <= 2);
+    for_batches(ns, nthreads, [&](int64_t b) {
+        if (ok && !pm_batch(src, spans[(size_t)b], D, t.unit, want_rt, pm[(size_t)b])) ok = false;
+    });
+    bool rt_fits = want_rt;
+    if (ok) {
+        // only where it leaves the headroom the residency choice keeps
+        // (8 GiB): else the gather margin, which needs no extra arrays.
+        // The row-round arrays are optional (k_grad_lds needs none of
+        // them): they are counted separately and dropped if only they
+        // do not fit.
+        int64_t need = 0, need_rt = 0;
+        for (const PmBatch &q : pm) {
+            need += (int64_t)(q.list.size() * 4 + q.val.size() * 4 + q.pofs.size() * 4 + q.rg.size() * 8 +
+                              q.qs.size() * 2 + q.lbeg.size() * 4);
+            need_rt += (int64_t)(q.gq.size() * 4 + q.rval.size() * 4 + q.cend.size() * 2);
+        }
+        size_t fr = 0, tot = 0;
+        HIPC(c, hipMemGetInfo(&fr, &tot));
+        const double head = (double)((size_t)8 << 30);
+        if ((double)need + head > (double)fr) {
+            ok = false;
+            if (force)
+                return fail(c, DLR_E_NOMEM, "dlr_load_train: DLR_PM=1 but the product margin's arrays (" +
+                                                std::to_string((long long)(need >> 20)) + " MiB) do not fit");
+        }
+        rt_fits = rt_fits && (double)(need + need_rt) + head <= (double)fr;
+        if (!rt_fits)
+            for (PmBatch &q : pm) {
+                std::vector<uint32_t>().swap(q.gq);
+                std::vector<float>().swap(q.rval);
+                std::vector<uint16_t>().swap(q.cend);
+            }
+    }
+    if (ok) {
+        t.pmS = S;
+        t.pmo_list.assign((size_t)ns + 1, 0);
+        t.pmo_pofs.assign((size_t)ns + 1, 0);
+        t.pmo_rg.assign((size_t)ns + 1, 0);
+        t.pmo_qs.assign((size_t)ns + 1, 0);
+        int64_t pcap = 0, maxslice = 0;
+        for (int64_t b = 0; b < ns; ++b) {
+            const PmBatch &q = pm[(size_t)b];
+            t.pmo_list[(size_t)b + 1] = t.pmo_list[(size_t)b] + (int64_t)q.list.size() * 2;  // entries
+            t.pmo_pofs[(size_t)b + 1] = t.pmo_pofs[(size_t)b] + (int64_t)q.pofs.size();
+            t.pmo_rg[(size_t)b + 1] = t.pmo_rg[(size_t)b] + (int64_t)q.rg.size();
+            t.pmo_qs[(size_t)b + 1] = t.pmo_qs[(size_t)b] + (int64_t)q.qs.size();
+            pcap = std::max<int64_t>(pcap, q.rg.back());
+            maxslice = std::max(maxslice, q.maxslice);
+            t.pm_groups = std::max(t.pm_groups, q.groups);
+        }
+        t.pm_split = (int)std::min<int64_t>(16, std::max<int64_t>(1, (maxslice + 16383) / 16384));
+        if (const char *sp = getenv("DLR_PM_SPLIT"))  // A/B: pass-1 workgroups per slice (separate pass)
+            t.pm_split = std::max(t.pm_split, std::min(16, std::max(1, atoi(sp))));
+        // one device array per member: the batches' parts back to back
+        // (offsets off[b] / div elements), each batch's host part
+        // released once copied, so the host peak stays ~1x the layout
+        auto cat_upload = [&](auto member, auto **dst, const std::vector<int64_t> &off, int64_t div,
+                              size_t pad) -> int {
+            using V = std::remove_reference_t<decltype(pm[0].*member)>;
+            V v((size_t)(off.back() / div));
+            for (int64_t b = 0; b < ns; ++b) {
+                V &src = pm[(size_t)b].*member;
+                std::copy(src.begin(), src.end(), v.begin() + off[(size_t)b] / div);
+                V().swap(src);
+            }
+            return upload(c, dst, v.data(), v.size(), pad);
+        };
+        std::vector<int64_t> lboff((size_t)ns + 1);
+        for (int64_t b = 0; b <= ns; ++b) lboff[(size_t)b] = b * (S + 1);
+        const int64_t lbeg_n = lboff.back();
+        if ((rc = cat_upload(&PmBatch::lbeg, &t.pm_lbeg, lboff, 1, 0))) return rc;
+        if ((rc = cat_upload(&PmBatch::list, &t.pm_list, t.pmo_list, 2, 64))) return rc;  // 2 words / 4 entries
+        if (!t.unit && (rc = cat_upload(&PmBatch::val, &t.pm_val, t.pmo_list, 1, 64))) return rc;
+        if ((rc = cat_upload(&PmBatch::pofs, &t.pm_pofs, t.pmo_pofs, 1, 0))) return rc;
+        if ((rc = cat_upload(&PmBatch::rg, &t.pm_rg, t.pmo_rg, 1, 0))) return rc;
+        if ((rc = cat_upload(&PmBatch::qoff, &t.pm_qoff, t.pmo_rg, 1, 0))) return rc;
+        if ((rc = cat_upload(&PmBatch::qs, &t.pm_qs, t.pmo_qs, 1, 8))) return rc;
+        bool rt_all = rt_fits;
+        for (const PmBatch &q : pm) rt_all = rt_all && !q.gq.empty();
+        if (rt_all) {
+            std::vector<int64_t> ceoff((size_t)ns + 1);
+            t.rtoff.assign((size_t)ns + 1, 0);
+            t.rt_cap.assign((size_t)ns, 0);
+            for (int64_t b = 0; b < ns; ++b) {
+                t.rtoff[(size_t)b + 1] = t.rtoff[(size_t)b] + (int64_t)pm[(size_t)b].gq.size();
+                t.rt_cap[(size_t)b] = pm[(size_t)b].rtcap;
+            }
+            for (int64_t b = 0; b <= ns; ++b) ceoff[(size_t)b] = b * S * dlr::kPmSlice;
+            if ((rc = cat_upload(&PmBatch::gq, &t.rt_gq, t.rtoff, 1, 0))) return rc;
+            if (!t.unit && (rc = cat_upload(&PmBatch::rval, &t.rt_val, t.rtoff, 1, 0))) return rc;
+            if ((rc = cat_upload(&PmBatch::cend, &t.rt_cend, ceoff, 1, 0))) return rc;
+            t.rt = true;
+            t.rt_rounds = (int)rounds;
+            resid_need = std::max(resid_need, (int64_t)t.rt_rounds * dlr::kRtRows);
+            csc_bytes += (int64_t)(t.rtoff.back() * (t.unit ? 4 : 8) + ceoff.back() * 2);
+        } else {
+            for (PmBatch &q : pm) {  // release the unused row-round host arrays now
+                std::vector<uint32_t>().swap(q.gq);
+                std::vector<float>().swap(q.rval);
+                std::vector<uint16_t>().swap(q.cend);
+            }
+        }
+        if ((rc = dev_alloc(c, (void **)&t.pm_p, (size_t)(pcap + 64) * 4))) return rc;
+        HIPC(c, hipMemsetAsync(t.pm_p, 0, (size_t)(pcap + 64) * 4, c->stream));
+        csc_bytes += (int64_t)(lbeg_n * 4 + t.pmo_list.back() * (t.unit ? 2 : 6) +
+                               t.pmo_pofs.back() * 4 + t.pmo_rg.back() * 8 + t.pmo_qs.back() * 2 + pcap * 4);
+        built = true;
+    }
+    return DLR_OK;
 }
 
 }  // namespace
@@ -2659,122 +2829,10 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         const char *pme = getenv("DLR_PM");
         const int64_t S = (D + dlr::kPmSlice - 1) / dlr::kPmSlice;
         if (!t.sparse_stream && !(pme && strcmp(pme, "0") == 0) && ((pme && strcmp(pme, "1") == 0) || S >= 128)) {
-            std::vector<PmBatch> pm((size_t)nb);
-            std::atomic<bool> ok{true};
-            // the row-round gradient: by default for batches of <= 2 rounds
-            // (C2 at B = 8,192: 7.5 vs 10.0 us for k_grad_lds); at 8 rounds
-            // (B = 65,536) k_grad_lds is faster.  DLR_GRAD_RT=1
-            // takes it for every batch that fits, =0 never.
-            const char *rte = getenv("DLR_GRAD_RT");
-            const int64_t rounds = (t.B + dlr::kRtRows - 1) / dlr::kRtRows;
-            const bool want_rt = rounds <= dlr::kRtMaxRounds &&
-                                 (rte ? strcmp(rte, "0") != 0 : rounds <= 2);
-            for_batches(nb, nthreads, [&](int64_t b) {
-                if (ok && !pm_batch(src, t.plan[(size_t)b], D, t.unit, want_rt, pm[(size_t)b])) ok = false;
-            });
-            bool rt_fits = want_rt;
-            if (ok) {
-                // only where it leaves the headroom the residency choice keeps
-                // (8 GiB): else the gather margin, which needs no extra arrays.
-                // The row-round arrays are optional (k_grad_lds needs none of
-                // them): they are counted separately and dropped if only they
-                // do not fit.
-                int64_t need = 0, need_rt = 0;
-                for (const PmBatch &q : pm) {
-                    need += (int64_t)(q.list.size() * 4 + q.val.size() * 4 + q.pofs.size() * 4 + q.rg.size() * 8 +
-                                      q.qs.size() * 2 + q.lbeg.size() * 4);
-                    need_rt += (int64_t)(q.gq.size() * 4 + q.rval.size() * 4 + q.cend.size() * 2);
-                }
-                size_t fr = 0, tot = 0;
-                HIPC(c, hipMemGetInfo(&fr, &tot));
-                const double head = (double)((size_t)8 << 30);
-                if ((double)need + head > (double)fr) {
-                    ok = false;
-                    if (pme && strcmp(pme, "1") == 0)
-                        return fail(c, DLR_E_NOMEM, "dlr_load_train: DLR_PM=1 but the product margin's arrays (" +
-                                                        std::to_string((long long)(need >> 20)) + " MiB) do not fit");
-                }
-                rt_fits = rt_fits && (double)(need + need_rt) + head <= (double)fr;
-                if (!rt_fits)
-                    for (PmBatch &q : pm) {
-                        std::vector<uint32_t>().swap(q.gq);
-                        std::vector<float>().swap(q.rval);
-                        std::vector<uint16_t>().swap(q.cend);
-                    }
-            }
-            if (ok) {
-                t.pmS = S;
-                t.pmo_list.assign((size_t)nb + 1, 0);
-                t.pmo_pofs.assign((size_t)nb + 1, 0);
-                t.pmo_rg.assign((size_t)nb + 1, 0);
-                t.pmo_qs.assign((size_t)nb + 1, 0);
-                int64_t pcap = 0, maxslice = 0;
-                for (int64_t b = 0; b < nb; ++b) {
-                    const PmBatch &q = pm[(size_t)b];
-                    t.pmo_list[(size_t)b + 1] = t.pmo_list[(size_t)b] + (int64_t)q.list.size() * 2;  // entries
-                    t.pmo_pofs[(size_t)b + 1] = t.pmo_pofs[(size_t)b] + (int64_t)q.pofs.size();
-                    t.pmo_rg[(size_t)b + 1] = t.pmo_rg[(size_t)b] + (int64_t)q.rg.size();
-                    t.pmo_qs[(size_t)b + 1] = t.pmo_qs[(size_t)b] + (int64_t)q.qs.size();
-                    pcap = std::max<int64_t>(pcap, q.rg.back());
-                    maxslice = std::max(maxslice, q.maxslice);
-                    t.pm_groups = std::max(t.pm_groups, q.groups);
-                }
-                t.pm_split = (int)std::min<int64_t>(16, std::max<int64_t>(1, (maxslice + 16383) / 16384));
-                if (const char *sp = getenv("DLR_PM_SPLIT"))  // A/B: pass-1 workgroups per slice (separate pass)
-                    t.pm_split = std::max(t.pm_split, std::min(16, std::max(1, atoi(sp))));
-                // one device array per member: the batches' parts back to back
-                // (offsets off[b] / div elements), each batch's host part
-                // released once copied, so the host peak stays ~1x the layout
-                auto cat_upload = [&](auto member, auto **dst, const std::vector<int64_t> &off, int64_t div,
-                                      size_t pad) -> int {
-                    using V = std::remove_reference_t<decltype(pm[0].*member)>;
-                    V v((size_t)(off.back() / div));
-                    for (int64_t b = 0; b < nb; ++b) {
-                        V &src = pm[(size_t)b].*member;
-                        std::copy(src.begin(), src.end(), v.begin() + off[(size_t)b] / div);
-                        V().swap(src);
-                    }
-                    return upload(c, dst, v.data(), v.size(), pad);
-                };
-                std::vector<int64_t> lboff((size_t)nb + 1);
-                for (int64_t b = 0; b <= nb; ++b) lboff[(size_t)b] = b * (S + 1);
-                const int64_t lbeg_n = lboff.back();
-                if ((rc = cat_upload(&PmBatch::lbeg, &t.pm_lbeg, lboff, 1, 0))) return rc;
-                if ((rc = cat_upload(&PmBatch::list, &t.pm_list, t.pmo_list, 2, 64))) return rc;  // 2 words / 4 entries
-                if (!t.unit && (rc = cat_upload(&PmBatch::val, &t.pm_val, t.pmo_list, 1, 64))) return rc;
-                if ((rc = cat_upload(&PmBatch::pofs, &t.pm_pofs, t.pmo_pofs, 1, 0))) return rc;
-                if ((rc = cat_upload(&PmBatch::rg, &t.pm_rg, t.pmo_rg, 1, 0))) return rc;
-                if ((rc = cat_upload(&PmBatch::qoff, &t.pm_qoff, t.pmo_rg, 1, 0))) return rc;
-                if ((rc = cat_upload(&PmBatch::qs, &t.pm_qs, t.pmo_qs, 1, 8))) return rc;
-                bool rt_all = rt_fits;
-                for (const PmBatch &q : pm) rt_all = rt_all && !q.gq.empty();
-                if (rt_all) {
-                    std::vector<int64_t> ceoff((size_t)nb + 1);
-                    t.rtoff.assign((size_t)nb + 1, 0);
-                    t.rt_cap.assign((size_t)nb, 0);
-                    for (int64_t b = 0; b < nb; ++b) {
-                        t.rtoff[(size_t)b + 1] = t.rtoff[(size_t)b] + (int64_t)pm[(size_t)b].gq.size();
-                        t.rt_cap[(size_t)b] = pm[(size_t)b].rtcap;
-                    }
-                    for (int64_t b = 0; b <= nb; ++b) ceoff[(size_t)b] = b * S * dlr::kPmSlice;
-                    if ((rc = cat_upload(&PmBatch::gq, &t.rt_gq, t.rtoff, 1, 0))) return rc;
-                    if (!t.unit && (rc = cat_upload(&PmBatch::rval, &t.rt_val, t.rtoff, 1, 0))) return rc;
-                    if ((rc = cat_upload(&PmBatch::cend, &t.rt_cend, ceoff, 1, 0))) return rc;
-                    t.rt = true;
-                    t.rt_rounds = (int)((t.B + dlr::kRtRows - 1) / dlr::kRtRows);
-                    resid_need = std::max(resid_need, (int64_t)t.rt_rounds * dlr::kRtRows);
-                    csc_bytes += (int64_t)(t.rtoff.back() * (t.unit ? 4 : 8) + ceoff.back() * 2);
-                } else {
-                    for (PmBatch &q : pm) {  // release the unused row-round host arrays now
-                        std::vector<uint32_t>().swap(q.gq);
-                        std::vector<float>().swap(q.rval);
-                        std::vector<uint16_t>().swap(q.cend);
-                    }
-                }
-                if ((rc = dev_alloc(c, (void **)&t.pm_p, (size_t)(pcap + 64) * 4))) return rc;
-                HIPC(c, hipMemsetAsync(t.pm_p, 0, (size_t)(pcap + 64) * 4, c->stream));
-                csc_bytes += (int64_t)(lbeg_n * 4 + t.pmo_list.back() * (t.unit ? 2 : 6) +
-                                       t.pmo_pofs.back() * 4 + t.pmo_rg.back() * 8 + t.pmo_qs.back() * 2 + pcap * 4);
+            bool built = false;
+            if ((rc = build_pm(c, src, t.plan, true, pme && strcmp(pme, "1") == 0, nthreads, resid_need, csc_bytes, built)))
+                return rc;
+            if (built) {
                 t.pm = true;
                 const char *pf = getenv("DLR_PM_FUSED");
                 t.pm_fused = !c->comm && !(pf && strcmp(pf, "0") == 0);
@@ -3064,6 +3122,29 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         if (!band)
             csc_bytes += (int64_t)(cptr.size() * 4 + (total + kPad) * ((t.row16 ? 2 : 4) + (t.unit ? 0 : 4)));
         csc_bytes += lbytes;
+        // the windowed product margin (band mode, no hot-weight margin)
+        const char *pme = getenv("DLR_PM");
+        const int64_t S = (D + dlr::kPmSlice - 1) / dlr::kPmSlice;
+        if (band && !t.margin_hot && ((int64_t)1 << shift) % kPmWinRows == 0 && !(pme && strcmp(pme, "0") == 0) &&
+            ((pme && strcmp(pme, "1") == 0) || S >= 128)) {
+            std::vector<dlr::BatchSpan> spans;
+            t.pmw_first.assign((size_t)nb + 1, 0);
+            for (int64_t b = 0; b < nb; ++b) {
+                const dlr::BatchSpan &sp = t.plan[(size_t)b];
+                for (int64_t r0 = 0; r0 < sp.rows; r0 += kPmWinRows) {
+                    const int64_t f = (sp.first_row + r0) % t.n_rows, n = std::min(kPmWinRows, sp.rows - r0);
+                    spans.push_back(dlr::BatchSpan{f, n, f + n <= t.n_rows});
+                }
+                t.pmw_first[(size_t)b + 1] = (int64_t)spans.size();
+            }
+            bool built = false;
+            if ((rc = build_pm(c, src, spans, false, pme && strcmp(pme, "1") == 0, nthreads, resid_need, csc_bytes,
+                               built)))
+                return rc;
+            t.pmw = built;
+            if (!built && pme && strcmp(pme, "1") == 0)
+                return fail(c, DLR_E_ARG, "dlr_load_train: DLR_PM=1 but the batches' windows do not fit the product margin");
+        }
     }
     // Residual buffer (padded to whole LDS phases for the LDS kernel).
     if (c->resid_cap < resid_need) {
@@ -3602,7 +3683,7 @@ int dlr_train_unit_values(dlr_ctx *c) {
 int dlr_train_product_margin(dlr_ctx *c) {
     if (!c) return DLR_E_ARG;
     if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_product_margin: no training shard loaded");
-    return c->train.pm ? (c->train.pm_fused ? (c->train.pm_mg ? 3 : 2) : 1) : 0;
+    return c->train.pm ? (c->train.pm_fused ? (c->train.pm_mg ? 3 : 2) : 1) : c->train.pmw ? 1 : 0;
 }
 
 int dlr_train_row_rounds(dlr_ctx *c) {

@@ -412,7 +412,10 @@ int dlr_train_unit_values(dlr_ctx *ctx);
  * weights, then sums each row's products in column order from LDS: bitwise
  * the gather margin.  DLR_PM=0 turns it off, DLR_PM=1 on for any batches that
  * fit; DLR_PM_FUSED=0 keeps pass 1 separate.  Replaces lr.cc:108-114's
- * Sigmoid_ dot product for these shards (same arithmetic). */
+ * Sigmoid_ dot product for these shards (same arithmetic).  Band-mode
+ * batches (>= 2^21 rows, e.g. a full-shard batch) without the hot-weight
+ * margin run it over windows of 65,536 rows (pass 1 and pass 2 per window:
+ * reported as 1). */
 int dlr_train_product_margin(dlr_ctx *ctx);
 
 /* Band mode, REFERENCE order: the hot columns (>= DLR_BAND_HOT entries in a

@@ -122,8 +122,7 @@ def test_c3_eight_ranks_loopback(c3_w8, order):
         within_bar(got.w, orc.w, "W = 8, long-column phases")
 
 
-@pytest.mark.parametrize("W", [2, 4])
-@pytest.mark.parametrize("order", ["reference", "fast"])
+@pytest.mark.parametrize("order,W", [("reference", 2), ("reference", 4), ("fast", 2)])
 def test_dense_c4_shape_ranks(monkeypatch, W, order):
     # C4's shape (D = 4,096, B = 65,536; 3 batches per epoch, the last
     # wrapping) on W loopback ranks at the bench's lr 0.2.  Reference order

@@ -434,3 +434,41 @@ def test_pm_margin_in_gradient_launch(monkeypatch, B):
         g = oracle.grad_csr((rp, col, val), lab, oracle.batch_rows(n, B, b % nb), w)
         oracle.server_update(w, [g], 0.2)
     assert_same_weights(got[-1], w)
+
+
+@pytest.mark.parametrize("band_rows", ["262144"])
+def test_pm_windows_full_shard_batch(monkeypatch, band_rows):
+    # B = -1 over > 2^20 rows (band mode): the margin as
+    # the product margin over 65,536-row windows -- pass 1 and pass 2 per
+    # window, the weights fixed inside the step (dlr_train_product_margin 1)
+    # -- two steps, bitwise the gather margin (DLR_PM=0) and the oracle
+    monkeypatch.setenv("DLR_BAND_ROWS", band_rows)
+    D = 1 << 20
+    n = 1_100_000
+    ds = dlr.Dataset.generate(n, D, 50, value_mode=1, seed=8, stream=3)
+
+    def run(pm):
+        monkeypatch.setenv("DLR_PM", pm)
+        eng = dlr.Engine(D)
+        try:
+            eng.set_weights(dlr.init_weight(D))
+            assert eng.load_train(ds, -1) == 1
+            assert eng.train_band_rows() == int(band_rows)
+            kind = eng.train_product_margin()
+            for _ in range(2):
+                eng.train_step(0, 0.2, 1.0)
+            return eng.get_weights(), kind
+        finally:
+            eng.close()
+
+    got, kind = run("1")
+    assert kind == 1
+    ref, kind0 = run("0")
+    assert kind0 == 0
+    assert_same_weights(got, ref, "windowed product margin vs gathers")
+    rp, col, val, lab = ds.csr()
+    w = dlr.init_weight(D)
+    for _ in range(2):
+        g = oracle.grad_csr((rp, col, val), lab, np.arange(n), w)
+        oracle.server_update(w, [g], 0.2)
+    assert_same_weights(got, w, "windowed product margin vs oracle")

@@ -16,10 +16,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = [
     # round 4: the margin in the gradient's launch (one launch per step)
     ("traffic.json", "r04_pmc_c2", "D1000000_nnz50_B65536", "lds", 0),
-    # round 3: the band-pipelined margin is dispatched per band; 20 step-
-    # equivalents (bench --steps 6 --warmup 2: 2 + 6 timed + 6 + 6 stage and
-    # breakdown steps)
-    ("traffic_c3.json", "r03_pmc_c3", "D16777216_nnz39_B-1", "classic", 20),
+    # round 5: C3 in the reference order (hot-column product stream); 14
+    # step-equivalents (bench --steps 6 --warmup 2 --no-stage-pass: 2 + 6 +
+    # 6 steps)
+    ("traffic_c3.json", "r05_pmc_c3", "D16777216_nnz39_B-1", "classic", 14),
+    # round 3: C3 in the FAST order (c3f); the band-pipelined margin is
+    # dispatched per band; 20 step-equivalents (bench --steps 6 --warmup 2:
+    # 2 + 6 timed + 6 + 6 stage and breakdown steps)
+    ("traffic_c3f.json", "r03_pmc_c3", "D16777216_nnz39_B-1", "classic", 20),
     # round 4: C4 in the reference order (K6r, one launch per step)
     ("traffic_c4.json", "r04_pmc_c4", "D4096_nnz4096_B65536", "dense", 0),
     ("traffic_c5.json", "r02_pmc_c5", "D268435456_nnz10_B1024", "touched", 0),
