@@ -1909,7 +1909,7 @@ hipError_t launch_pm_windows(dlr_ctx *c, int64_t b, int64_t r0, int64_t r1) {
 bool pm_mg_ok(const dlr_ctx *c, int64_t b) {
     const TrainShard &t = c->train;
     if (!t.pm_mg || c->comm || !t.pcsc || t.rt) return false;
-    return dlr::grad_lds_mg_ok(pm_view(c, b), c->D, t.plan[(size_t)b].rows, t.phases);
+    return dlr::grad_lds_mg_ok(pm_view(c, b), c->D, t.plan[(size_t)b].rows, t.phases, (int)(t.pR / 4096));
 }
 
 // rowsum_only (dlr_stage_time): the product margin's pass 2 alone, on
@@ -1946,9 +1946,9 @@ hipError_t launch_margin(dlr_ctx *c, int64_t b, bool rowsum_only = false, bool m
 dlr::DevPcsc pcsc_view(const dlr_ctx *c, int64_t b) {
     const TrainShard &t = c->train;
     if (t.gpu_pcsc)  // built on the device for the current batch
-        return {t.pbase + (size_t)b * (size_t)(t.pblocks + 1), t.gends, t.grow, t.gval, t.phases};
+        return {t.pbase + (size_t)b * (size_t)(t.pblocks + 1), t.gends, t.grow, t.gval, t.phases, (int)(t.pR / 4096)};
     return {t.pbase + (size_t)b * (size_t)(t.pblocks + 1), t.pends + (size_t)b * (size_t)t.pblocks * 64,
-            t.prow + t.poff[(size_t)b], t.pval + t.poff[(size_t)b], t.phases};
+            t.prow + t.poff[(size_t)b], t.pval + t.poff[(size_t)b], t.phases, (int)(t.pR / 4096)};
 }
 
 dlr::DevCsc csc_view(const dlr_ctx *c, int64_t b) {
@@ -2772,16 +2772,17 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
     int64_t resid_need = t.B;
     PcscBuild pb;
     if (!force_classic && t.B <= 65536 && D <= (int64_t)1 << 31) {
-        pb.R = (int64_t)dlr::grad_lds_fill(t.B) * 4096;
+        pb.R = dlr::grad_lds_phase_rows(t.B);
         pb.P = (int)((t.B + pb.R - 1) / pb.R);
         pb.groups = (D + 63) / 64;
         pb.pblocks = pb.groups * pb.P;
-        t.pcsc = pb.P <= 2 && pcsc_plan(src, t.plan, D, pb, nthreads);
+        t.pcsc = pb.P <= 4 && pcsc_plan(src, t.plan, D, pb, nthreads);
     }
     if (gk && strcmp(gk, "lds") == 0 && !t.pcsc)
         return fail(c, DLR_E_ARG, "dlr_load_train: DLR_GRAD_KERNEL=lds but the batches do not fit the LDS layout");
     if (t.pcsc) {
         t.phases = pb.P;
+        t.pR = pb.R;
         t.pblocks = pb.pblocks;
         t.poff.assign((size_t)nb + 1, 0);
         for (int64_t b = 0; b < nb; ++b) t.poff[(size_t)b + 1] = t.poff[(size_t)b] + pb.size[(size_t)b];
@@ -2843,7 +2844,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 // ... only if every batch's launch is resident at once
                 // (grad_lds_mg_ok; otherwise pass 2 runs in k_pm_margin)
                 for (int64_t b = 0; t.pm_mg && b < nb; ++b)
-                    t.pm_mg = dlr::grad_lds_mg_ok(pm_view(c, b), c->D, t.plan[(size_t)b].rows, t.phases);
+                    t.pm_mg = dlr::grad_lds_mg_ok(pm_view(c, b), c->D, t.plan[(size_t)b].rows, t.phases, (int)(t.pR / 4096));
                 if (t.pm_mg) {
                     const size_t cb = (size_t)dlr::DevP2::kMgCntWords * 4;
                     if ((rc = dev_alloc(c, (void **)&t.pm_cnt, cb))) return rc;

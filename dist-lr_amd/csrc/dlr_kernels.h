@@ -57,7 +57,9 @@ struct DevLong {
 };
 
 // One batch column-major, PHASE-SPLIT for the LDS-resident gradient
-// kernel: rows fall in phases of R = grad_lds_fill(B)*4,096 (1 or 2 phases).
+// kernel: rows fall in phases of R = fill*4,096 rows (grad_lds_phase_rows:
+// one phase of <= 16,384 rows, or up to four of 16,384 -- the
+// double-buffered form -- or, with DLR_GRAD_DB=0, up to two of 32,768).
 // For 64-column group g and phase p, block (g*phases + p) holds the entries
 // of those columns whose row is in the phase, column by column, rows
 // ascending; base[blk] is its first entry (4-aligned), ends[blk*64 + l] the
@@ -70,6 +72,7 @@ struct DevPcsc {
     const uint16_t *row;
     const float *val;
     int phases;
+    int fill;  // R / 4,096
 };
 
 // Short columns of one batch in ROW BANDS of 2^k rows (classic layout, large
@@ -335,6 +338,8 @@ hipError_t launch_long_phase(const DevLPhase &lp, const uint32_t *cols, const ui
 hipError_t launch_band_finalize(const float *gacc, float *w, float *gout, int64_t D, int64_t B, float lr, float C,
                                 bool fused, hipStream_t s);
 int grad_lds_fill(int64_t B);
+// Rows per phase of the LDS layout for batches of up to B rows.
+int64_t grad_lds_phase_rows(int64_t B);
 // The LDS layout (DevPcsc row/val/ends) of one batch built on the device
 // from its CSR and block bases (streamed shards); scratch: pblocks*64 uint32.
 hipError_t launch_pcsc_build(const DevBatch &bt, const uint32_t *base, int P, int64_t R, int64_t pblocks,
@@ -353,7 +358,7 @@ hipError_t launch_pm_margin(const DevPm &pm, const DevBatch &bt, const float *p,
 // mg != null: this batch's pass 2 too, in the same launch (DevP2; resid is
 // then mg->resid, written by the launch; p holds this batch's products);
 // grad_lds_mg_ok says whether the batch's shape allows it.
-bool grad_lds_mg_ok(const DevPm &cur, int64_t D, int64_t B, int phases);
+bool grad_lds_mg_ok(const DevPm &cur, int64_t D, int64_t B, int phases, int fill);
 hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const float *resid, float *w, float lr,
                               float C, const DevPm &next, float *p, hipStream_t s, const DevP2 *mg = nullptr);
 // The row-round gradient (DevRt): the update (fused) or the pushed gradient

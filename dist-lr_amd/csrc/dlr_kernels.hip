@@ -83,6 +83,20 @@ __device__ __forceinline__ float lds_rd32(uint32_t a) {
 __device__ __forceinline__ void lds_wr128(uint32_t a, v4f v) {
     asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
+// LDS-DMA hidden from the compiler: 16 bytes per lane from gsrc to LDS byte
+// address lds_dst (wave-uniform) + 16 * lane; M0 written and restored in
+// the statement (cdna_hip_programming.md, the LDS-DMA recipe).  The
+// compiler counts none of these in its vmcnt bookkeeping -- callers wait
+// for them with explicit vmcnt -- and, unlike the builtin, they do not make
+// its own waits for register loads in flight beside them vmcnt(0) (an
+// LDS-DMA pending beside plain loads is a mixed-event counter to it).
+__device__ __forceinline__ void lds_dma16(const void *gsrc, uint32_t lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
 __device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void lds_wait1(float &a) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a)); }
 __device__ __forceinline__ void lds_wait4(float &a, float &b, float &c, float &d) {
@@ -970,8 +984,18 @@ namespace {
 #define DLR_MG_EVEN 1
 #endif
 constexpr int kMgSub = 8;  // sub-counters per phase (DevP2)
+#ifndef DLR_WIN1_EARLY  // A/B builds: k_grad_lds two-phase issue order
+#define DLR_WIN1_EARLY 0
+#endif
+// DLR_LIST_LATE = k >= 1: the pass-1 list at the top of phase 1's group k - 1
+#ifndef DLR_LIST_LATE  // 1: C2 25.7 vs 26.5 us per step (profiles/r05_c2_issue_order.txt)
+#define DLR_LIST_LATE 1
+#endif
 #ifndef DLR_MG_FILL_SC1
 #define DLR_MG_FILL_SC1 0
+#endif
+#ifndef DLR_W_SC1
+#define DLR_W_SC1 0
 #endif
 #ifndef DLR_PM_SC1
 #define DLR_PM_SC1 ((DLR_ABL & 16) != 0)
@@ -1210,20 +1234,30 @@ __global__ __launch_bounds__(256) void k_pm_margin(DevPm pm, DevBatch bt, const 
 // after every block's copy of its region.  The launch boundary between the
 // margin and the gradient is gone and the gradient's window loads stream
 // while the blocks are summed.
-template <int FILL, bool FUSED, bool NTW, bool PM = false, bool MG = false>
+// DB (double-buffered phases; batches of 16,385-65,536 rows, FILL = 4): up
+// to four phases of 16,384 rows in two 64 KB residual buffers.  At the top
+// of phase p the workgroup issues phase p + 1's windows and fill into the
+// other buffer, then computes phase p: each fill streams while the previous
+// phase computes (the two-phase form waits for its second 128 KB fill with
+// nothing to do: profiles/r05_stamps_c2_pollskip.txt, 14.5 -> 18.2 us).
+// The same blocks, the same column order: bitwise the two-phase form.
+template <int FILL, bool FUSED, bool NTW, bool PM = false, bool MG = false, bool DB = false>
 __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int64_t D, int64_t B,
                                                                 const float *__restrict__ resid,
                                                                 float *__restrict__ w, float *__restrict__ gout,
                                                                 float Bf, double Bd, float lr, float C,
                                                                 DevPm pn = DevPm{}, float *__restrict__ pm_p = nullptr,
                                                                 DevP2 p2 = DevP2{}) {
-    constexpr int R = FILL * 4096;
+    constexpr int R = FILL * 4096;      // rows per phase
+    constexpr int NB = DB ? 2 : 1;      // residual buffers
+    constexpr int NPH = DB ? 4 : 2;     // phases
     constexpr int NG = kGradNG;
+    static_assert(!DB || FILL == 4, "double-buffered phases are 16,384 rows");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float *s_r = smem;
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // uniform: scalar block loads
-    float *s_p = smem + R + wv * kBlkPad;
+    float *s_p = smem + NB * R + wv * kBlkPad;
     const uint32_t s_r_a = lds_addr(s_r), s_p_a = lds_addr(s_p);
     const int P = pc.phases;
     const int64_t ng = (D + 63) / 64;
@@ -1236,7 +1270,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
         DLR_STAMP(11);
         if (blockIdx.x == 0 && wv < 8)  // the next launch's bank: 64 phases x 8 sub-counters
             p2.cnt[(((p2.gen + 1) & 1) * 64 + lane) * kMgSub * 32 + wv * 32] = 0u;
-        const int64_t k2 = blockIdx.x + (int64_t)gridDim.x * wv;  // wv < FILL (launch_grad_lds_pm)
+        const int64_t k2 = blockIdx.x + (int64_t)gridDim.x * wv;  // wv < NB * FILL (launch_grad_lds_pm)
         if (k2 < p2.pm.nblk) {  // wave-uniform
             pm_rowsum<8, true>(p2.pm, p2.bt, pm_p, p2.resid, k2, smem + wv * kPmCap, lane);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every residual of the block stored
@@ -1258,11 +1292,12 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     // wave 0 waits until every block of phase p is published (the caller's
     // barrier then holds the other waves' fills); a wait that runs out is
     // reported (Spin)
-    // The same poll reads the NEXT phase's counters too (lanes 8..15): the
-    // blocks of both phases are summed at the launch's start, so phase 1 is
-    // nearly always complete when phase 0 is, and its own poll -- a round
-    // trip queued behind the phase-1 windows and the pass-1 list loads --
-    // is skipped (mg_done: the phases known complete).
+    // The same poll reads the LATER phases' counters too (lane 8d + s:
+    // sub-counter s of phase p + d, d < NPH): the blocks of every phase are
+    // summed at the launch's start, so the later phases are nearly always
+    // complete when phase p is, and their own polls -- round trips queued
+    // behind the windows, fills and pass-1 list loads -- are skipped
+    // (mg_done: the phases known complete).
     Spin spin(MG ? p2.err : nullptr, kErrMgPublish);
     int mg_done = 0;
     auto mg_wait = [&](int p) {
@@ -1272,76 +1307,102 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
                 auto want_of = [&](int q) {
                     return (uint32_t)(min<int64_t>(p2.pm.nblk, (q + 1) * bpp) - q * bpp);
                 };
-                const bool two = p + 1 < P;
-                const uint32_t want = want_of(p), want1 = two ? want_of(p + 1) : 0u;
                 const __amdgpu_buffer_rsrc_t crs =
                     __builtin_amdgcn_make_buffer_rsrc(p2.cnt, 0, 0x7FFFFFFF, 0x00020000);
-                // lane s < 8 reads sub-counter s of phase p, lane 8 + s that
-                // of phase p + 1 (phase p again when p is the last)
-                const int q = p + ((lane >> 3) & 1 & (int)two);
+                // (phases past the last read the last one again)
+                const int q = min(p + ((lane >> 3) & (NPH - 1)), P - 1);
                 const int off = (int)(((((p2.gen & 1) * 64 + q) * kMgSub + (lane & (kMgSub - 1))) * 32) * 4);
                 for (int k = 0; spin.more(k); ++k) {
                     const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(crs, off, 0, 16);
-                    uint32_t n = 0, n1 = 0;
+                    uint32_t n[NPH];
 #pragma unroll
-                    for (int i = 0; i < kMgSub; ++i) {
-                        n += __builtin_amdgcn_readlane(v, i);
-                        n1 += __builtin_amdgcn_readlane(v, kMgSub + i);
+                    for (int d = 0; d < NPH; ++d) {
+                        n[d] = 0;
+#pragma unroll
+                        for (int i = 0; i < kMgSub; ++i) n[d] += __builtin_amdgcn_readlane(v, d * kMgSub + i);
                     }
-                    if (n >= want) {
-                        mg_done = two && n1 >= want1 ? p + 2 : p + 1;
-                        break;
+                    if (n[0] >= want_of(p)) {
+                        int done = p + 1;
+#pragma unroll
+                        for (int d = 1; d < NPH; ++d)
+                            if (done == p + d && p + d < P && n[d] >= want_of(p + d)) done = p + d + 1;
+                        // (DB: every phase, from phase 0 -- see its loop)
+                        if (!DB || done >= P) {
+                            mg_done = done;
+                            break;
+                        }
                     }
                     __builtin_amdgcn_s_sleep(DLR_MG_SLEEP);
                 }
             }
         }
     };
-    unsigned bs[NG][2], off[NG][2], cnt[NG][2], nblk[NG][2];
+    // per group: the bases of its phase blocks (blocks gc*P + q are
+    // consecutive: P + 1 bases give every block's first entry and its
+    // entries rounded up to 4 -- blocks are 4-aligned: a lane's first
+    // window slot 4*lane is an entry iff 4*lane < that) -- wave-uniform,
+    // all phases up front; per lane: its column's inclusive end offset in
+    // the block (<= 255) for the phases in registers (set p & 1; meta) --
+    // the column's start is lane - 1's end (a lane shuffle at its use, so
+    // that no arithmetic waits for the load where it is issued)
+    // (DB: three register sets -- windows are issued two phases ahead, as
+    // their HBM round trip under load is ~3.5 us, more than a phase)
+    constexpr int RS = DB ? 3 : 2;
+    auto rs = [](int p) { return DB ? p % 3 : p & 1; };
+    unsigned sb[NG][NPH + 1], hb[NG][RS];
     float acc[NG], wj[NG];
-    ushort4 rq[NG][2];
-    float4 vq[NG][2];
+    ushort4 rq[NG][RS];
+    float4 vq[NG][RS];
+    // (the bases first, and straight into SGPRs: the windows' addresses
+    // need them at once, and a base left in a VGPR made the compiler wait
+    // for every load in flight where the next phase's windows are issued)
 #pragma unroll
     for (int gi = 0; gi < NG; ++gi) {
         const int64_t g = gfirst + kGradWaves * gi;
-        const bool gv = g < ng;
-        const int64_t gc = gv ? g : ng - 1;
-        const int64_t j = g * 64 + lane;
-        const bool ok = gv && j < D;
+        const int64_t gc = g < ng ? g : ng - 1;
+#pragma unroll
+        for (int q = 0; q <= NPH; ++q) sb[gi][q] = pc.base[gc * P + (q < P ? q : P)];
+    }
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+#pragma unroll
+        for (int q = 0; q <= NPH; ++q) sb[gi][q] = __builtin_amdgcn_readfirstlane(sb[gi][q]);
+        const int64_t j = (gfirst + kGradWaves * gi) * 64 + lane;
         wj[gi] = (DLR_ABL & 8) ? 0.0f : w[j < D ? j : D - 1];
         acc[gi] = 0.0f;
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const int64_t blk = gc * P + (p < P ? p : P - 1);
-            bs[gi][p] = pc.base[blk];
-            // the block's entries rounded up to 4 (blocks are 4-aligned): a
-            // lane's first window slot 4*lane is an entry iff 4*lane < this
-            nblk[gi][p] = pc.base[blk + 1] - bs[gi][p];
-            const unsigned hi = pc.ends[blk * 64 + lane];
-            const unsigned lo = pc.ends[blk * 64 + (lane ? lane - 1 : 0)];
-            off[gi][p] = lane ? lo : 0u;
-            cnt[gi][p] = (ok && p < P) ? hi - (lane ? lo : 0u) : 0u;
-        }
     }
+    auto bs_of = [&](int gi, int p) { return sb[gi][p]; };
+    auto nblk_of = [&](int gi, int p) { return sb[gi][p + 1] - sb[gi][p]; };
+    auto meta = [&](int p) {
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) {
+            const int64_t g = gfirst + kGradWaves * gi;
+            const int64_t blk = (g < ng ? g : ng - 1) * P + (p < P ? p : P - 1);
+            hb[gi][rs(p)] = pc.ends[blk * 64 + lane];
+        }
+    };
+    meta(0);
+    if (!DB) meta(1);  // (DB: after the first fill)
     auto windows = [&](int p) {
 #pragma unroll
         for (int gi = 0; gi < NG; ++gi) {
             if ((DLR_ABL & 2) && p == 0) {
-                rq[gi][p] = ushort4{0, 0, 0, 0};
-                vq[gi][p] = make_float4(0.f, 0.f, 0.f, 0.f);
+                rq[gi][0] = ushort4{0, 0, 0, 0};
+                vq[gi][0] = make_float4(0.f, 0.f, 0.f, 0.f);
                 continue;
             }
             // lanes past the block re-read its last 4 entries: the wave's
             // addresses then span the block only (the next blocks' lines are
             // not pulled into this CU), and a duplicate address costs nothing
-            const unsigned nb4 = nblk[gi][p];
-            const unsigned e = bs[gi][p] + min((unsigned)lane * 4, nb4 ? nb4 - 4 : 0u);  // padded: in bounds
+            const unsigned nb4 = nblk_of(gi, p);
+            const unsigned e = bs_of(gi, p) + min((unsigned)lane * 4, nb4 ? nb4 - 4 : 0u);  // padded: in bounds
+            // (register set rs(p): DB holds three phases' windows at a time)
             if (NTW) {
-                rq[gi][p] = load_stream(reinterpret_cast<const ushort4 *>(pc.row + e));
-                vq[gi][p] = load_stream(reinterpret_cast<const float4 *>(pc.val + e));
+                rq[gi][rs(p)] = load_stream(reinterpret_cast<const ushort4 *>(pc.row + e));
+                vq[gi][rs(p)] = load_stream(reinterpret_cast<const float4 *>(pc.val + e));
             } else {
-                rq[gi][p] = *reinterpret_cast<const ushort4 *>(pc.row + e);
-                vq[gi][p] = *reinterpret_cast<const float4 *>(pc.val + e);
+                rq[gi][rs(p)] = *reinterpret_cast<const ushort4 *>(pc.row + e);
+                vq[gi][rs(p)] = *reinterpret_cast<const float4 *>(pc.val + e);
             }
         }
     };
@@ -1355,110 +1416,204 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     // belongs to one block -- so the first read of a line, and every later
     // hit on it, sees the stored values.  DLR_MG_FILL_SC1=1: sc1 fills.)
     const float *rsrc = MG ? p2.resid : resid;
-    auto fill = [&](int64_t lo) {
+    // (into residual buffer buf: DB's phase p goes to buffer p & 1, by the
+    // asm LDS-DMA: see lds_dma16)
+    auto fill = [&](int64_t lo, int buf) {
 #pragma unroll
         for (int f = 0; f < R / (kGradWaves * kWave * 4); ++f) {  // FILL with 16 waves
             const int o = (f * kGradWaves + wv) * kWave * 4;  // floats; this wave's 1 KiB slot
+            if (DB && !(MG && DLR_MG_FILL_SC1)) {
+                lds_dma16(rsrc + lo + o + lane * 4,
+                          __builtin_amdgcn_readfirstlane(s_r_a + 4u * (uint32_t)(buf * R + o)));
+                continue;
+            }
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)(rsrc + lo + o + lane * 4),
-                (__attribute__((address_space(3))) void *)(s_r + o), 16, 0, MG && DLR_MG_FILL_SC1 ? 16 : 0);
+                (__attribute__((address_space(3))) void *)(s_r + buf * R + o), 16, 0, MG && DLR_MG_FILL_SC1 ? 16 : 0);
         }
     };
-    // Phase 0's windows and the first fill are issued up front; phase 1's
-    // windows only after phase 0's first group has consumed its data (the
-    // compiler drains every older load there), so they stream from HBM while
-    // the rest of phase 0 computes instead of delaying its start.
+    // Group gi's products and column sums of phase p (residuals at LDS
+    // address sra); false when the wave has no group gi.
+    auto group = [&](int gi, int p, uint32_t sra) -> bool {
+        if (gfirst + kGradWaves * gi >= ng) return false;  // wave-uniform
+        // products of the block's entries only: the window's other slots
+        // (the next blocks' entries) are never read, so those lanes skip
+        // their residual gathers (LDS bank cycles) and the slab write
+        // (LDS through lds_* asm: the pass-1 loads stay in flight)
+        if ((unsigned)lane * 4 < nblk_of(gi, p)) {
+            const ushort4 r4 = rq[gi][rs(p)];
+            const float4 v4 = vq[gi][rs(p)];
+            float g0 = lds_rd32(sra + 4u * r4.x), g1 = lds_rd32(sra + 4u * r4.y);
+            float g2 = lds_rd32(sra + 4u * r4.z), g3 = lds_rd32(sra + 4u * r4.w);
+            lds_wait4(g0, g1, g2, g3);
+            const v4f q = {g0 * v4.x, g1 * v4.y, g2 * v4.z, g3 * v4.w};
+            lds_wr128(s_p_a + 16u * lane, q);
+        }
+        lds_wait();  // the slab is complete (one wave)
+        // this lane's column: cnt products in order from off.  The first
+        // eight are read at immediate offsets from s_p + o (the slab is
+        // padded, so no clamping) and added while any lane still has one
+        // (a wave-uniform exit: the sum stops at the wave's largest count,
+        // ~5 at C2's 1.6 entries per column and phase); the rare longer
+        // runs continue in a general loop.  Per product: compare, add,
+        // select.  Not the bound: the SQ counters put VALU issue at <= ~20%
+        // busy (profiles/r02f_c2_sq_counters.txt); the kernel is bound by
+        // its chain of dependent memory phases (tools/c2_stamps.py).
+        const unsigned hi = hb[gi][rs(p)];
+        // (the shuffle outside the lane test: inside it, lane 0 -- the
+        // source of lane 1's start -- would be inactive)
+        const unsigned up = (unsigned)__shfl_up((int)hi, 1);
+        const unsigned o = lane ? up : 0u;
+        const bool cok = p < P && (gfirst + kGradWaves * gi) * 64 + lane < D;
+        const unsigned c = cok ? hi - o : 0u;
+        const uint32_t sp = s_p_a + 4u * o;
+        float a = acc[gi];
+        // all eight reads issue together (one LDS round trip)
+        float x[8];
+        x[0] = lds_rd32<0>(sp), x[1] = lds_rd32<4>(sp), x[2] = lds_rd32<8>(sp), x[3] = lds_rd32<12>(sp);
+        x[4] = lds_rd32<16>(sp), x[5] = lds_rd32<20>(sp), x[6] = lds_rd32<24>(sp), x[7] = lds_rd32<28>(sp);
+        lds_wait4(x[0], x[1], x[2], x[3]);
+        lds_wait4(x[4], x[5], x[6], x[7]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const bool take = (unsigned)u < c;
+            if (__builtin_amdgcn_ballot_w64(take) == 0) break;  // wave-uniform
+            const float t = a + x[u];
+            a = take ? t : a;
+        }
+        for (unsigned k = 8; __builtin_amdgcn_ballot_w64(k < c) != 0; ++k) {
+            float xv = lds_rd32(s_p_a + 4u * min(o + k, (unsigned)kBlk - 1));
+            lds_wait1(xv);
+            if (k < c) a = a + xv;
+        }
+        acc[gi] = a;
+        wave_sync();
+        return true;
+    };
+    // Phase 0's windows and the first fill are issued up front.
     DLR_STAMP(0);
     windows(0);
+    if (!DB && DLR_WIN1_EARLY) windows(1);  // (A/B: see the two-phase loop)
     if constexpr (MG) {
         mg_wait(0);
         lds_barrier();  // and this workgroup's pass-2 regions are read
         DLR_STAMP(13);
     }
-    if (!(DLR_ABL & 1)) fill(0);
+    if (!(DLR_ABL & 1)) fill(0, 0);
+    if (DB) {
+        windows(1);
+        meta(1);
+    }
     DLR_STAMP(8);
 #ifdef DLR_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     DLR_STAMP(9);
 #endif
     DLR_STAMP(10);
+    if constexpr (DB) {
+        // Phase p + 1's fill (from L2) is issued at the top of phase p, and
+        // phase p + 2's windows and column ends (from HBM) after it: the top
+        // of phase p waits for all but those 12 youngest loads per thread
+        // (NG windows of two loads, NG end bytes: every thread issues them,
+        // addresses clamped past the last phase).  Every phase's margin
+        // blocks were awaited before phase 0 (mg_wait in DB form): the loop
+        // holds no poll, whose load loop would make the compiler's own waits
+        // for the window registers vmcnt(0).  The next batch's pass-1 list
+        // is issued at the top of the last phase, so it streams while that
+        // phase computes; batches of fewer phases issue it after the loop.
+        constexpr int lph = NPH - 1;
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
-        if (p >= P) break;  // uniform
-        if (p > 0) {
-            DLR_STAMP(2);
-            mg_wait(p);
-            lds_barrier();  // every wave is done reading the previous phase
-            DLR_STAMP(3);
-            fill((int64_t)p * R);  // resid is padded to P*R floats
+        for (int p = 0; p < NPH; ++p) {
+            if (p >= P) break;  // uniform
+            if (p + 1 < NPH)
+                asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // This phase's window registers, consumed here -- where the wait
+            // above has drained them -- so that the compiler, which does not
+            // read that asm wait, puts its own wait for them here and not at
+            // their use below, behind the later phases' loads.
+#pragma unroll
+            for (int gi = 0; gi < NG; ++gi) {
+                uint32_t r2[2];
+                __builtin_memcpy(r2, &rq[gi][rs(p)], 8);
+                const float4 v = vq[gi][rs(p)];
+                asm volatile("" ::"v"(r2[0]), "v"(r2[1]), "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w),
+                             "v"(hb[gi][rs(p)]));
+            }
+            // every wave's share of fill p is in LDS, and every wave is done
+            // with phase p - 1: its buffer takes phase p + 1
+            lds_barrier();
+            DLR_STAMP(p == 0 ? 1 : p == 1 ? 4 : p);  // slots 1, 4, 2, 3
+            asm volatile("" ::: "memory");
+            // (unconditional: a load issued on one path only would make the
+            // compiler wait for every load at the join; past the last phase
+            // the addresses are clamped to it)
+            if (p + 1 < NPH) fill((int64_t)min(p + 1, P - 1) * R, (p + 1) & 1);  // resid is padded to P*R floats
+            if (p + 2 < NPH) {
+                windows(p + 2);
+                meta(p + 2);
+            }
+            if (PM && !(DLR_ABL & 4) && p == lph) pm.fetch(pn, pm.c0);
+            asm volatile("" ::: "memory");
+            const uint32_t sra = s_r_a + 4u * (uint32_t)((p & 1) * R);
+#pragma unroll
+            for (int gi = 0; gi < NG; ++gi)
+                if (!group(gi, p, sra)) break;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA fill (not tracked by the compiler)
-        lds_barrier();
-        DLR_STAMP(1 + 3 * p);
+        // (a batch of fewer phases: the fill issued for the phase past its
+        // last is still landing in LDS that pass 1 reuses)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (PM && !(DLR_ABL & 4) && P <= lph) pm.fetch(pn, pm.c0);
+    } else {
+        bool listed = false;  // (wave-uniform) this wave issued its share of the pass-1 list
+        // Phase 1's windows only after phase 0's first group has consumed
+        // its data (the compiler drains every older load there), so they
+        // stream from HBM while the rest of phase 0 computes instead of
+        // delaying its start.
 #pragma unroll
-        for (int gi = 0; gi < NG; ++gi) {
-            if (p == 0 && gi == 1) {
-                // phase 1's windows and the next batch's pass-1 slice list
-                // (its range was loaded first thing) stream while the rest of
-                // phase 0 computes: issued here, after the first group's
-                // compiler-placed waits, they do not delay phase 0's start
-                asm volatile("" ::: "memory");
-                if (P > 1) windows(1);
-                if (PM && !(DLR_ABL & 4)) pm.fetch(pn, pm.c0);
-                asm volatile("" ::: "memory");
+        for (int p = 0; p < 2; ++p) {
+            if (p >= P) break;  // uniform
+            if (p > 0) {
+                DLR_STAMP(2);
+                mg_wait(p);
+                lds_barrier();  // every wave is done reading the previous phase
+                DLR_STAMP(3);
+                fill((int64_t)p * R, 0);  // resid is padded to P*R floats
             }
-            if (gfirst + kGradWaves * gi >= ng) break;  // wave-uniform
-            // products of the block's entries only: the window's other slots
-            // (the next blocks' entries) are never read, so those lanes skip
-            // their residual gathers (LDS bank cycles) and the slab write
-            // (LDS through lds_* asm: the pass-1 loads stay in flight)
-            if ((unsigned)lane * 4 < nblk[gi][p]) {
-                const ushort4 r4 = rq[gi][p];
-                const float4 v4 = vq[gi][p];
-                float g0 = lds_rd32(s_r_a + 4u * r4.x), g1 = lds_rd32(s_r_a + 4u * r4.y);
-                float g2 = lds_rd32(s_r_a + 4u * r4.z), g3 = lds_rd32(s_r_a + 4u * r4.w);
-                lds_wait4(g0, g1, g2, g3);
-                const v4f q = {g0 * v4.x, g1 * v4.y, g2 * v4.z, g3 * v4.w};
-                lds_wr128(s_p_a + 16u * lane, q);
-            }
-            lds_wait();  // the slab is complete (one wave)
-            // this lane's column: cnt products in order from off.  The first
-            // eight are read at immediate offsets from s_p + o (the slab is
-            // padded, so no clamping) and added while any lane still has one
-            // (a wave-uniform exit: the sum stops at the wave's largest count,
-            // ~5 at C2's 1.6 entries per column and phase); the rare longer
-            // runs continue in a general loop.  Per product: compare, add,
-            // select.  Not the bound: the SQ counters put VALU issue at <= ~20%
-            // busy (profiles/r02f_c2_sq_counters.txt); the kernel is bound by
-            // its chain of dependent memory phases (tools/c2_stamps.py).
-            const unsigned o = off[gi][p], c = cnt[gi][p];
-            const uint32_t sp = s_p_a + 4u * o;
-            float a = acc[gi];
-            // all eight reads issue together (one LDS round trip)
-            float x[8];
-            x[0] = lds_rd32<0>(sp), x[1] = lds_rd32<4>(sp), x[2] = lds_rd32<8>(sp), x[3] = lds_rd32<12>(sp);
-            x[4] = lds_rd32<16>(sp), x[5] = lds_rd32<20>(sp), x[6] = lds_rd32<24>(sp), x[7] = lds_rd32<28>(sp);
-            lds_wait4(x[0], x[1], x[2], x[3]);
-            lds_wait4(x[4], x[5], x[6], x[7]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA fill (not tracked by the compiler)
+            lds_barrier();
+            DLR_STAMP(1 + 3 * p);
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const bool take = (unsigned)u < c;
-                if (__builtin_amdgcn_ballot_w64(take) == 0) break;  // wave-uniform
-                const float t = a + x[u];
-                a = take ? t : a;
+            for (int gi = 0; gi < NG; ++gi) {
+                if (p == 0 && gi == 1) {
+                    // phase 1's windows and the next batch's pass-1 slice list
+                    // (its range was loaded first thing) stream while the rest of
+                    // phase 0 computes: issued here, after the first group's
+                    // compiler-placed waits, they do not delay phase 0's start
+                    // (A/B: DLR_WIN1_EARLY issues the windows with phase 0's,
+                    // DLR_LIST_LATE the list at the top of phase 1)
+                    asm volatile("" ::: "memory");
+                    if (P > 1 && !DLR_WIN1_EARLY) windows(1);
+                    if (PM && !(DLR_ABL & 4) && !(DLR_LIST_LATE && P > 1)) {
+                        pm.fetch(pn, pm.c0);
+                        listed = true;
+                    }
+                    asm volatile("" ::: "memory");
+                }
+                if (DLR_LIST_LATE && PM && !(DLR_ABL & 4) && p == 1 && gi == DLR_LIST_LATE - 1) {
+                    asm volatile("" ::: "memory");
+                    pm.fetch(pn, pm.c0);
+                    listed = true;
+                    asm volatile("" ::: "memory");
+                }
+                if (!group(gi, p, s_r_a)) break;
             }
-            for (unsigned k = 8; __builtin_amdgcn_ballot_w64(k < c) != 0; ++k) {
-                float xv = lds_rd32(s_p_a + 4u * min(o + k, (unsigned)kBlk - 1));
-                lds_wait1(xv);
-                if (k < c) a = a + xv;
-            }
-            acc[gi] = a;
-            wave_sync();
         }
+        // a wave with no column group left the loop before issuing its
+        // share of the pass-1 list (every thread takes part in pass 1)
+        if (PM && !(DLR_ABL & 4) && !listed) pm.fetch(pn, pm.c0);
     }
-    // a wave with no column group left the loop before issuing its share
-    // of the pass-1 list (every thread takes part in pass 1)
-    if (PM && !(DLR_ABL & 4) && gfirst >= ng) pm.fetch(pn, pm.c0);
 #ifdef DLR_STAMPS
     __syncthreads();
     DLR_STAMP(5);
@@ -1481,7 +1636,12 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
             if (FUSED) {
                 const float step = lr * g;
                 const float wn = wj[gi] - step;
-                w[j] = wn;
+                if (DLR_W_SC1 && PM) {  // (A/B: write-through, out of L2 before the kernel-end flush)
+                    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(w, 0, 0x7FFFFFFF, 0x00020000);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(wn), wr, (int)(j * 4), 0, 16);
+                } else {
+                    w[j] = wn;
+                }
                 if (PM) smem[(wv + kGradWaves * gi) * 64 + lane] = wn;  // column j - kPmSlice*blockIdx.x
             } else {
                 gout[j] = g;
@@ -4041,6 +4201,33 @@ int grad_lds_fill(int64_t B) {
     return 8;
 }
 
+// Batches of more than 16,384 rows: two phases of 32,768 rows in one
+// buffer by default; DLR_GRAD_DB=1 takes phases of 16,384 rows in two
+// buffers (k_grad_lds DB: measured slower -- C2 31.2 vs 26.5 us per step,
+// each 16,384-row phase costs nearly what a 32,768-row one does;
+// profiles/r05_stamps_c2_db.txt).
+int64_t grad_lds_phase_rows(int64_t B) {
+    static const bool db = [] {
+        const char *e = getenv("DLR_GRAD_DB");
+        return e && strcmp(e, "1") == 0;
+    }();
+    if (B > 16384 && db) return 16384;
+    return (int64_t)grad_lds_fill(B) * 4096;
+}
+
+namespace {
+// The kernel form of a layout: FILL = its rows per phase / 4,096, DB when
+// a 16,384-row layout has more than one phase.
+bool grad_lds_db(const DevPcsc &pc) { return pc.fill == 4 && pc.phases > 1; }
+bool grad_lds_form_ok(const DevPcsc &pc) {
+    const bool db = grad_lds_db(pc);
+    return (pc.fill == 1 || pc.fill == 2 || pc.fill == 4 || pc.fill == 8) && pc.phases >= 1 &&
+           pc.phases <= (db ? 4 : 2);
+}
+// residual floats in LDS
+size_t grad_lds_rrows(int fill, bool db) { return (size_t)fill * 4096 * (db ? 2 : 1); }
+}  // namespace
+
 hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float *resid, float *w, float *gout,
                            float lr, float C, bool fused, hipStream_t s) {
     if (D <= 0) return hipSuccess;
@@ -4049,8 +4236,10 @@ hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float 
     const dim3 blk(kGradWaves * kWave);
     const float Bf = (float)B;
     const double Bd = (double)B;
-    const int fill = grad_lds_fill(B);
-    const size_t lds = (size_t)fill * 4096 * 4 + (size_t)kGradWaves * kBlkPad * 4;
+    if (!grad_lds_form_ok(pc)) return hipErrorInvalidValue;
+    const int fill = pc.fill;
+    const bool db = grad_lds_db(pc);
+    const size_t lds = grad_lds_rrows(fill, db) * 4 + (size_t)kGradWaves * kBlkPad * 4;
     // Non-temporal window loads measured slower here (tools/ab_bench.sh,
     // C2: 19.4 vs 16.6 us -- this kernel is latency-bound in its prologue);
     // DLR_GRAD_NT=1 turns them on.
@@ -4073,6 +4262,15 @@ hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float 
             hipLaunchKernelGGL((k_grad_lds<F, false, false>), dim3(grid), blk, lds, s, pc, D, B, resid, w, gout, Bf, \
                                Bd, lr, C);                                                                          \
         break;
+    if (db) {
+        if (fused)
+            hipLaunchKernelGGL((k_grad_lds<4, true, false, false, false, true>), dim3(grid), blk, lds, s, pc, D, B,
+                               resid, w, gout, Bf, Bd, lr, C);
+        else
+            hipLaunchKernelGGL((k_grad_lds<4, false, false, false, false, true>), dim3(grid), blk, lds, s, pc, D, B,
+                               resid, w, gout, Bf, Bd, lr, C);
+        return hipGetLastError();
+    }
     switch (fill) {
         DLR_GL(1)
         DLR_GL(2)
@@ -4113,7 +4311,8 @@ hipError_t launch_pm_margin(const DevPm &pm, const DevBatch &bt, const float *p,
 namespace {
 // The one-launch step's kernel for a fill (a workgroup of every grid
 // size it may take must fit beside the others: they wait for each other).
-const void *grad_lds_mg_fn(int fill) {
+const void *grad_lds_mg_fn(int fill, bool db) {
+    if (db) return fill == 4 ? reinterpret_cast<const void *>(&k_grad_lds<4, true, false, true, true, true>) : nullptr;
     switch (fill) {
         case 1: return reinterpret_cast<const void *>(&k_grad_lds<1, true, false, true, true>);
         case 2: return reinterpret_cast<const void *>(&k_grad_lds<2, true, false, true, true>);
@@ -4122,8 +4321,9 @@ const void *grad_lds_mg_fn(int fill) {
         default: return nullptr;
     }
 }
-size_t grad_lds_pm_lds(int fill) {
-    return std::max((size_t)fill * 4096 * 4 + (size_t)kGradWaves * kBlkPad * 4, (size_t)(kPmSlice + kPmMaxBlocks) * 4);
+size_t grad_lds_pm_lds(int fill, bool db) {
+    return std::max(grad_lds_rrows(fill, db) * 4 + (size_t)kGradWaves * kBlkPad * 4,
+                    (size_t)(kPmSlice + kPmMaxBlocks) * 4);
 }
 
 // CUs of the current device (cached per device; 0 if the runtime cannot say)
@@ -4164,17 +4364,23 @@ int resident_grid(const void *fn, int threads, size_t lds) {
 // waits for blocks summed by the others, so one that is not resident
 // would leave the resident ones waiting (D = 2^21 at B =
 // 65,536 has 512 slices on 256 CUs; such batches take k_pm_margin).
-bool grad_lds_mg_ok(const DevPm &cur, int64_t D, int64_t B, int phases) {
+bool grad_lds_mg_ok(const DevPm &cur, int64_t D, int64_t B, int phases, int fill) {
     const int64_t grid = (D + kPmSlice - 1) / kPmSlice;
-    const int fill = grad_lds_fill(B);
-    if (!(D > 0 && cur.groups <= 8 && cur.nblk == (B + kPmRows - 1) / kPmRows && cur.nblk <= grid * fill &&
-          phases >= 1 && phases <= 64))
+    DevPcsc form{};
+    form.phases = phases;
+    form.fill = fill;
+    if (!grad_lds_form_ok(form)) return false;
+    const bool db = grad_lds_db(form);
+    // (wave v < the workgroup's pass-2 regions sums block x + grid * v)
+    const int64_t regions = (int64_t)grad_lds_rrows(fill, db) / kPmCap;
+    if (!(D > 0 && cur.groups <= 8 && cur.nblk == (B + kPmRows - 1) / kPmRows && cur.nblk <= grid * regions &&
+          (int64_t)phases * fill * 4096 >= B))
         return false;
-    static int cap[64][9] = {};  // per device and fill (cached: the check runs every step)
+    static int cap[64][2][9] = {};  // per device, form and fill (cached: the check runs every step)
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || fill < 1 || fill > 8) return false;
-    int &c = cap[dev][fill];
-    if (c == 0) c = resident_grid(grad_lds_mg_fn(fill), kGradWaves * kWave, grad_lds_pm_lds(fill));
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    int &c = cap[dev][db][fill];
+    if (c == 0) c = resident_grid(grad_lds_mg_fn(fill, db), kGradWaves * kWave, grad_lds_pm_lds(fill, db));
     return c > 0 && grad_lds_mg_grid(cur.nblk, grid) <= c;
 }
 
@@ -4185,15 +4391,26 @@ hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const flo
     const unsigned grid = (unsigned)((ng + kGradWaves * kGradNG - 1) / (kGradWaves * kGradNG));
     static_assert(kGradWaves * kGradNG * 64 == kPmSlice, "a gradient workgroup's columns are one slice");
     if ((int64_t)grid != next.S || next.nblk > kPmMaxBlocks) return hipErrorInvalidValue;
-    if (mg && (!grad_lds_mg_ok(mg->pm, D, B, pc.phases) || mg->bt.rows != B || !mg->cnt || !mg->resid))
+    if (!grad_lds_form_ok(pc)) return hipErrorInvalidValue;
+    if (mg && (!grad_lds_mg_ok(mg->pm, D, B, pc.phases, pc.fill) || mg->bt.rows != B || !mg->cnt || !mg->resid))
         return hipErrorInvalidValue;
     // MG: every workgroup resident at once (grad_lds_mg_ok checked it)
     const unsigned mgrid = mg ? (unsigned)grad_lds_mg_grid(mg->pm.nblk, grid) : grid;
     const dim3 blk(kGradWaves * kWave);
     const float Bf = (float)B;
     const double Bd = (double)B;
-    const int fill = grad_lds_fill(B);
-    const size_t lds = grad_lds_pm_lds(fill);
+    const int fill = pc.fill;
+    const bool db = grad_lds_db(pc);
+    const size_t lds = grad_lds_pm_lds(fill, db);
+    if (db) {
+        if (mg)
+            hipLaunchKernelGGL((k_grad_lds<4, true, false, true, true, true>), dim3(mgrid), blk, lds, s, pc, D, B,
+                               resid, w, nullptr, Bf, Bd, lr, C, next, p, *mg);
+        else
+            hipLaunchKernelGGL((k_grad_lds<4, true, false, true, false, true>), dim3(grid), blk, lds, s, pc, D, B,
+                               resid, w, nullptr, Bf, Bd, lr, C, next, p);
+        return hipGetLastError();
+    }
 #define DLR_GLP(F)                                                                                            \
     case F:                                                                                                   \
         if (mg)                                                                                               \
