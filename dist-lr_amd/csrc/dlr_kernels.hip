@@ -991,6 +991,12 @@ constexpr int kMgSub = 8;  // sub-counters per phase (DevP2)
 #ifndef DLR_LIST_LATE  // 1: C2 25.7 vs 26.5 us per step (profiles/r05_c2_issue_order.txt)
 #define DLR_LIST_LATE 1
 #endif
+#ifndef DLR_LIST_SPREAD  // 1: C2 25.3 vs 25.7 us per step (profiles/r05_c2_issue_order.txt)
+#define DLR_LIST_SPREAD 1
+#endif
+#ifndef DLR_WIN_SPREAD  // 1: 25.16 vs 25.24 us (profiles/r05_c2_issue_order.txt)
+#define DLR_WIN_SPREAD 1
+#endif
 #ifndef DLR_MG_FILL_SC1
 #define DLR_MG_FILL_SC1 0
 #endif
@@ -1383,9 +1389,10 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     };
     meta(0);
     if (!DB) meta(1);  // (DB: after the first fill)
-    auto windows = [&](int p) {
+    auto windows = [&](int p, int g0 = 0, int g1 = NG) {
 #pragma unroll
         for (int gi = 0; gi < NG; ++gi) {
+            if (gi < g0 || gi >= g1) continue;
             if ((DLR_ABL & 2) && p == 0) {
                 rq[gi][0] = ushort4{0, 0, 0, 0};
                 vq[gi][0] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1567,6 +1574,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
         if (PM && !(DLR_ABL & 4) && P <= lph) pm.fetch(pn, pm.c0);
     } else {
         bool listed = false;  // (wave-uniform) this wave issued its share of the pass-1 list
+        int nsets = 0;        // (DLR_LIST_SPREAD) the list's group sets issued
         // Phase 1's windows only after phase 0's first group has consumed
         // its data (the compiler drains every older load there), so they
         // stream from HBM while the rest of phase 0 computes instead of
@@ -1594,17 +1602,35 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
                     // (A/B: DLR_WIN1_EARLY issues the windows with phase 0's,
                     // DLR_LIST_LATE the list at the top of phase 1)
                     asm volatile("" ::: "memory");
-                    if (P > 1 && !DLR_WIN1_EARLY) windows(1);
+                    if (P > 1 && !DLR_WIN1_EARLY) {
+                        if (DLR_WIN_SPREAD)
+                            windows(1, 0, 2);  // (A/B: the rest before groups 2 and 3)
+                        else
+                            windows(1);
+                    }
                     if (PM && !(DLR_ABL & 4) && !(DLR_LIST_LATE && P > 1)) {
                         pm.fetch(pn, pm.c0);
                         listed = true;
                     }
                     asm volatile("" ::: "memory");
                 }
-                if (DLR_LIST_LATE && PM && !(DLR_ABL & 4) && p == 1 && gi == DLR_LIST_LATE - 1) {
+                if (DLR_WIN_SPREAD && !DLR_WIN1_EARLY && p == 0 && gi >= 2 && P > 1) {
+                    asm volatile("" ::: "memory");
+                    windows(1, gi, gi + 1);
+                    asm volatile("" ::: "memory");
+                }
+                if (DLR_LIST_LATE && !DLR_LIST_SPREAD && PM && !(DLR_ABL & 4) && p == 1 &&
+                    gi == DLR_LIST_LATE - 1) {
                     asm volatile("" ::: "memory");
                     pm.fetch(pn, pm.c0);
                     listed = true;
+                    asm volatile("" ::: "memory");
+                }
+                if (DLR_LIST_LATE && DLR_LIST_SPREAD && PM && !(DLR_ABL & 4) && p == 1) {
+                    // (A/B: one of the list's four group sets before each group)
+                    asm volatile("" ::: "memory");
+                    pm.fetch_one(pn, pm.c0, gi);
+                    nsets = gi + 1;
                     asm volatile("" ::: "memory");
                 }
                 if (!group(gi, p, s_r_a)) break;
@@ -1612,7 +1638,15 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
         }
         // a wave with no column group left the loop before issuing its
         // share of the pass-1 list (every thread takes part in pass 1)
-        if (PM && !(DLR_ABL & 4) && !listed) pm.fetch(pn, pm.c0);
+        if (PM && !(DLR_ABL & 4) && !listed) {
+            if (DLR_LIST_SPREAD && DLR_LIST_LATE && P > 1) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (u >= nsets) pm.fetch_one(pn, pm.c0, u);
+            } else {
+                pm.fetch(pn, pm.c0);
+            }
+        }
     }
 #ifdef DLR_STAMPS
     __syncthreads();
@@ -4207,10 +4241,8 @@ int grad_lds_fill(int64_t B) {
 // each 16,384-row phase costs nearly what a 32,768-row one does;
 // profiles/r05_stamps_c2_db.txt).
 int64_t grad_lds_phase_rows(int64_t B) {
-    static const bool db = [] {
-        const char *e = getenv("DLR_GRAD_DB");
-        return e && strcmp(e, "1") == 0;
-    }();
+    const char *e = getenv("DLR_GRAD_DB");  // (read at each load: tests switch it)
+    const bool db = e && strcmp(e, "1") == 0;
     if (B > 16384 && db) return 16384;
     return (int64_t)grad_lds_fill(B) * 4096;
 }

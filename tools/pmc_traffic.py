@@ -91,14 +91,15 @@ def main() -> int:
     # The product margin in the gradient's launch (k_grad_lds<F, true,
     # false, true, true>: pass 2 + gradient + update + next pass 1) is a step
     # of its own, like K6r.  A kernel counts in the first role that matches.
-    mg = ", true, false, true, true>"
+    # (round 5 added a sixth template argument, DB: both spellings)
+    mg = [", true, false, true, true>", ", true, false, true, true, "]
     roles = [("margin", ["k_margin", "k_pm_margin", "k_pm_products", "k_dense_fused", "k_dense_margin", "k_flag_store"]),
-             ("step", ["k_dense_ref<", mg]),  # one launch: margin + gradient + update
+             ("step", ["k_dense_ref<", *mg]),  # one launch: margin + gradient + update
              ("grad", ["k_grad", "k_long_", "k_band_finalize", "k_band_hot", "k_hot_chain", "k_dense_grad",
                        "k_dense_combine"]),
              ("update", ["k_dense_l2", "k_scatter", "k_merge_update", "k_sparse_merge"])]
     steps = args.steps or len([x for k in ["k_margin", "k_pm_margin", "k_dense_fused", "k_dense_margin", "k_dense_ref<",
-                                           mg] for x in pick(bf, k)]) or 1
+                                           *mg] for x in pick(bf, k)]) or 1
     taken: set[str] = set()
 
     def take(d, keys):
