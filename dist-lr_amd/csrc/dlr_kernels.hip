@@ -1003,6 +1003,9 @@ constexpr int kMgSub = 8;  // sub-counters per phase (DevP2)
 #ifndef DLR_W_SC1
 #define DLR_W_SC1 0
 #endif
+#ifndef DLR_PM_NT
+#define DLR_PM_NT 0
+#endif
 #ifndef DLR_PM_SC1
 #define DLR_PM_SC1 ((DLR_ABL & 16) != 0)
 #endif
@@ -1114,6 +1117,9 @@ struct PmPass1 {
                         const u32x4 b = {__float_as_uint(q.x), __float_as_uint(q.y), __float_as_uint(q.z),
                                          __float_as_uint(q.w)};
                         __builtin_amdgcn_raw_buffer_store_b128(b, rs, (int)((s_po[k] + j) * 4u), 0, 16);
+                    } else if (DLR_PM_NT) {  // (A/B: non-temporal product stores)
+                        const v4f qv = {q.x, q.y, q.z, q.w};
+                        __builtin_nontemporal_store(qv, reinterpret_cast<v4f *>(p + s_po[k] + j));
                     } else {
                         *reinterpret_cast<float4 *>(p + s_po[k] + j) = q;
                     }
