@@ -4390,9 +4390,24 @@ int64_t grad_lds_mg_grid(int64_t nblk, int64_t grid) {
 int resident_grid(const void *fn, int threads, size_t lds) {
     if (!fn) return 0;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds) != hipSuccess) {
-        (void)hipGetLastError();
-        return 0;
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds);
+    if (e != hipSuccess) (void)hipGetLastError();
+    if (e != hipSuccess || per_cu < 1) {
+        // The query failed (seen after ~100 tests in one process: every
+        // call then returned 0, while launches of the same kernel ran).  A
+        // kernel built with __launch_bounds__(threads) fits one workgroup of
+        // `threads` per CU in registers by construction, so one per CU is a
+        // lower bound whenever its LDS fits a CU's.
+        int dev = 0, cu_lds = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cu_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess) {
+            (void)hipGetLastError();
+            cu_lds = 0;
+        }
+        if (getenv("DLR_DEBUG_MG"))
+            fprintf(stderr, "resident_grid: occupancy query %d (%s), per_cu %d; CU LDS %d, request %zu\n", (int)e,
+                    hipGetErrorString(e), per_cu, cu_lds, lds);
+        per_cu = (cu_lds > 0 && lds <= (size_t)cu_lds && threads <= 1024) ? 1 : 0;
     }
     return per_cu * device_cus();
 }
@@ -4419,6 +4434,9 @@ bool grad_lds_mg_ok(const DevPm &cur, int64_t D, int64_t B, int phases, int fill
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
     int &c = cap[dev][db][fill];
     if (c == 0) c = resident_grid(grad_lds_mg_fn(fill, db), kGradWaves * kWave, grad_lds_pm_lds(fill, db));
+    if (getenv("DLR_DEBUG_MG"))
+        fprintf(stderr, "grad_lds_mg_ok: dev %d fill %d db %d resident %d cus %d grid %lld mgrid %lld\n", dev, fill,
+                (int)db, c, device_cus(), (long long)grid, (long long)grad_lds_mg_grid(cur.nblk, grid));
     return c > 0 && grad_lds_mg_grid(cur.nblk, grid) <= c;
 }
 
