@@ -14,8 +14,9 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CASES = [
-    # round 4: the margin in the gradient's launch (one launch per step)
-    ("traffic.json", "r04_pmc_c2", "D1000000_nnz50_B65536", "lds", 0),
+    # round 5: the margin in the gradient's launch (one launch per step),
+    # the round-5 issue order
+    ("traffic.json", "r05_pmc_c2", "D1000000_nnz50_B65536", "lds", 0),
     # round 5: C3 in the reference order (hot-column product stream); 14
     # step-equivalents (bench --steps 6 --warmup 2 --no-stage-pass: 2 + 6 +
     # 6 steps)
