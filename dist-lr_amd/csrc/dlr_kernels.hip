@@ -994,6 +994,15 @@ constexpr int kMgSub = 8;  // sub-counters per phase (DevP2)
 #ifndef DLR_LIST_SPREAD  // 1: C2 25.3 vs 25.7 us per step (profiles/r05_c2_issue_order.txt)
 #define DLR_LIST_SPREAD 1
 #endif
+#ifndef DLR_SLAB_NOWAIT  // 1: 25.05-25.10 vs 25.10-25.16 us (profiles/r05_c2_issue_order.txt)
+#define DLR_SLAB_NOWAIT 1
+#endif
+#ifndef DLR_GRP_PIPE  // 1: 24.57 vs 24.97-25.00 us (profiles/r05_c2_issue_order.txt)
+#define DLR_GRP_PIPE 1
+#endif
+#ifndef DLR_MG_POLL_FIRST
+#define DLR_MG_POLL_FIRST 0
+#endif
 #ifndef DLR_WIN_SPREAD  // 1: 25.16 vs 25.24 us (profiles/r05_c2_issue_order.txt)
 #define DLR_WIN_SPREAD 1
 #endif
@@ -1462,7 +1471,10 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
             const v4f q = {g0 * v4.x, g1 * v4.y, g2 * v4.z, g3 * v4.w};
             lds_wr128(s_p_a + 16u * lane, q);
         }
-        lds_wait();  // the slab is complete (one wave)
+        // the slab is complete (one wave; DLR_SLAB_NOWAIT, A/B: a wave's LDS
+        // operations complete in issue order, so the reads below follow the
+        // slab writes without a wait)
+        if (!DLR_SLAB_NOWAIT) lds_wait();
         // this lane's column: cnt products in order from off.  The first
         // eight are read at immediate offsets from s_p + o (the slab is
         // padded, so no clamping) and added while any lane still has one
@@ -1503,12 +1515,82 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
         wave_sync();
         return true;
     };
+    // All NG groups of phase p, software-pipelined (DLR_GRP_PIPE; the wave
+    // has all of them): per group one LDS round trip -- the slab write, its
+    // reads and the next group's residual gathers issued together, then a
+    // wait for all but those 4 gathers (LDS returns in order; an older
+    // scalar load in the count only makes the wait stricter).  The same
+    // products and the same additions as group(): bitwise.
+    auto group_pipe = [&](int p, uint32_t sra, auto &&hooks) {
+        unsigned o[NG], c[NG];
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) {
+            const unsigned hi = hb[gi][rs(p)];
+            const unsigned up = (unsigned)__shfl_up((int)hi, 1);
+            o[gi] = lane ? up : 0u;
+            c[gi] = (p < P && (gfirst + kGradWaves * gi) * 64 + lane < D) ? hi - o[gi] : 0u;
+        }
+        float g[2][4], x[8];
+        auto gath = [&](int gi, float(&gg)[4]) {
+            // every lane (lanes past the block gather its last entries'
+            // rows: in range, their products land in slab slots no run reads)
+            const ushort4 r4 = rq[gi][rs(p)];
+            gg[0] = lds_rd32(sra + 4u * r4.x), gg[1] = lds_rd32(sra + 4u * r4.y);
+            gg[2] = lds_rd32(sra + 4u * r4.z), gg[3] = lds_rd32(sra + 4u * r4.w);
+        };
+        gath(0, g[0]);
+        lds_wait4(g[0][0], g[0][1], g[0][2], g[0][3]);
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) {
+            hooks(gi);
+            float(&gc)[4] = g[gi & 1];
+            const float4 v4 = vq[gi][rs(p)];
+            const v4f q = {gc[0] * v4.x, gc[1] * v4.y, gc[2] * v4.z, gc[3] * v4.w};
+            lds_wr128(s_p_a + 16u * lane, q);
+            const uint32_t sp = s_p_a + 4u * o[gi];
+            x[0] = lds_rd32<0>(sp), x[1] = lds_rd32<4>(sp), x[2] = lds_rd32<8>(sp), x[3] = lds_rd32<12>(sp);
+            x[4] = lds_rd32<16>(sp), x[5] = lds_rd32<20>(sp), x[6] = lds_rd32<24>(sp), x[7] = lds_rd32<28>(sp);
+            if (gi + 1 < NG) {
+                float(&gn)[4] = g[(gi + 1) & 1];
+                gath(gi + 1, gn);
+                asm volatile("s_waitcnt lgkmcnt(4)"
+                             : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]),
+                               "+v"(x[7]));
+            } else {
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]),
+                               "+v"(x[7]));
+            }
+            float a = acc[gi];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const bool take = (unsigned)u < c[gi];
+                if (__builtin_amdgcn_ballot_w64(take) == 0) break;  // wave-uniform
+                const float t = a + x[u];
+                a = take ? t : a;
+            }
+            for (unsigned k = 8; __builtin_amdgcn_ballot_w64(k < c[gi]) != 0; ++k) {
+                float xv = lds_rd32(s_p_a + 4u * min(o[gi] + k, (unsigned)kBlk - 1));
+                lds_wait1(xv);  // (lgkmcnt(0): the next group's gathers land too)
+                if (k < c[gi]) a = a + xv;
+            }
+            acc[gi] = a;
+            if (gi + 1 < NG) {
+                float(&gn)[4] = g[(gi + 1) & 1];
+                lds_wait4(gn[0], gn[1], gn[2], gn[3]);
+            }
+        }
+    };
     // Phase 0's windows and the first fill are issued up front.
     DLR_STAMP(0);
-    windows(0);
+    // (A/B, DLR_MG_POLL_FIRST: wave 0 polls before its own window loads, so
+    // that its poll does not return behind them)
+    const bool poll_first = MG && DLR_MG_POLL_FIRST && wv == 0;
+    if (!poll_first) windows(0);
     if (!DB && DLR_WIN1_EARLY) windows(1);  // (A/B: see the two-phase loop)
     if constexpr (MG) {
         mg_wait(0);
+        if (poll_first) windows(0);
         lds_barrier();  // and this workgroup's pass-2 regions are read
         DLR_STAMP(13);
     }
@@ -1598,48 +1680,60 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA fill (not tracked by the compiler)
             lds_barrier();
             DLR_STAMP(1 + 3 * p);
-#pragma unroll
-            for (int gi = 0; gi < NG; ++gi) {
-                if (p == 0 && gi == 1) {
-                    // phase 1's windows and the next batch's pass-1 slice list
-                    // (its range was loaded first thing) stream while the rest of
-                    // phase 0 computes: issued here, after the first group's
-                    // compiler-placed waits, they do not delay phase 0's start
-                    // (A/B: DLR_WIN1_EARLY issues the windows with phase 0's,
-                    // DLR_LIST_LATE the list at the top of phase 1)
-                    asm volatile("" ::: "memory");
-                    if (P > 1 && !DLR_WIN1_EARLY) {
-                        if (DLR_WIN_SPREAD)
-                            windows(1, 0, 2);  // (A/B: the rest before groups 2 and 3)
-                        else
-                            windows(1);
-                    }
-                    if (PM && !(DLR_ABL & 4) && !(DLR_LIST_LATE && P > 1)) {
-                        pm.fetch(pn, pm.c0);
-                        listed = true;
-                    }
-                    asm volatile("" ::: "memory");
+            // the loads issued between phase p's groups (VMEM only)
+            auto hooks = [&](int gi) {
+            if (p == 0 && gi == 1) {
+                // phase 1's windows and the next batch's pass-1 slice list
+                // (its range was loaded first thing) stream while the rest of
+                // phase 0 computes: issued here, after the first group's
+                // compiler-placed waits, they do not delay phase 0's start
+                // (A/B: DLR_WIN1_EARLY issues the windows with phase 0's,
+                // DLR_LIST_LATE the list at the top of phase 1)
+                asm volatile("" ::: "memory");
+                if (P > 1 && !DLR_WIN1_EARLY) {
+                    if (DLR_WIN_SPREAD)
+                        windows(1, 0, 2);  // (A/B: the rest before groups 2 and 3)
+                    else
+                        windows(1);
                 }
-                if (DLR_WIN_SPREAD && !DLR_WIN1_EARLY && p == 0 && gi >= 2 && P > 1) {
-                    asm volatile("" ::: "memory");
-                    windows(1, gi, gi + 1);
-                    asm volatile("" ::: "memory");
-                }
-                if (DLR_LIST_LATE && !DLR_LIST_SPREAD && PM && !(DLR_ABL & 4) && p == 1 &&
-                    gi == DLR_LIST_LATE - 1) {
-                    asm volatile("" ::: "memory");
+                if (PM && !(DLR_ABL & 4) && !(DLR_LIST_LATE && P > 1)) {
                     pm.fetch(pn, pm.c0);
                     listed = true;
-                    asm volatile("" ::: "memory");
                 }
-                if (DLR_LIST_LATE && DLR_LIST_SPREAD && PM && !(DLR_ABL & 4) && p == 1) {
-                    // (A/B: one of the list's four group sets before each group)
-                    asm volatile("" ::: "memory");
-                    pm.fetch_one(pn, pm.c0, gi);
-                    nsets = gi + 1;
-                    asm volatile("" ::: "memory");
+                asm volatile("" ::: "memory");
+            }
+            if (DLR_WIN_SPREAD && !DLR_WIN1_EARLY && p == 0 && gi >= 2 && P > 1) {
+                asm volatile("" ::: "memory");
+                windows(1, gi, gi + 1);
+                asm volatile("" ::: "memory");
+            }
+            if (DLR_LIST_LATE && !DLR_LIST_SPREAD && PM && !(DLR_ABL & 4) && p == 1 &&
+                gi == DLR_LIST_LATE - 1) {
+                asm volatile("" ::: "memory");
+                pm.fetch(pn, pm.c0);
+                listed = true;
+                asm volatile("" ::: "memory");
+            }
+            if (DLR_LIST_LATE && DLR_LIST_SPREAD && PM && !(DLR_ABL & 4) && p == 1) {
+                // (A/B: one of the list's four group sets before each group)
+                asm volatile("" ::: "memory");
+                pm.fetch_one(pn, pm.c0, gi);
+                nsets = gi + 1;
+                asm volatile("" ::: "memory");
+            }
+            };
+            // (A/B, DLR_GRP_PIPE: a wave with all NG groups software-pipelines
+            // them -- group gi + 1's residual gathers in flight with group
+            // gi's slab reads and adds, the slab rewritten after the reads
+            // are issued: a wave's LDS operations complete in issue order)
+            if (DLR_GRP_PIPE && gfirst + kGradWaves * (NG - 1) < ng) {
+                group_pipe(p, s_r_a, hooks);
+            } else {
+#pragma unroll
+                for (int gi = 0; gi < NG; ++gi) {
+                    hooks(gi);
+                    if (!group(gi, p, s_r_a)) break;
                 }
-                if (!group(gi, p, s_r_a)) break;
             }
         }
         // a wave with no column group left the loop before issuing its
