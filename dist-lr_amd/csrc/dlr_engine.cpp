@@ -1908,7 +1908,9 @@ hipError_t launch_pm_windows(dlr_ctx *c, int64_t b, int64_t r0, int64_t r1) {
 // k_grad_lds MG): launch_margin then forms only the products, if missing.
 bool pm_mg_ok(const dlr_ctx *c, int64_t b) {
     const TrainShard &t = c->train;
-    if (!t.pm_mg || c->comm || !t.pcsc || t.rt) return false;
+    if (!t.pm_mg || c->comm || !t.pcsc) return false;
+    if (t.rt)  // the row-round gradient (k_grad_rt MG)
+        return dlr::grad_rt_mg_ok(pm_view(c, b), c->D, t.plan[(size_t)b].rows, t.rt_rounds, t.rt_val == nullptr);
     return dlr::grad_lds_mg_ok(pm_view(c, b), c->D, t.plan[(size_t)b].rows, t.phases, (int)(t.pR / 4096));
 }
 
@@ -2012,6 +2014,16 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
         if (t.pm_fused && fused) {
             const int64_t nx = (b + 1) % (int64_t)t.plan.size();
             const dlr::DevPm next = pm_view(c, nx);
+            if (pm_mg_ok(c, b)) {  // this batch's pass 2 in the same launch
+                const dlr::DevP2 mg{pm_view(c, b), batch_view(c, b), c->resid, t.pm_cnt, t.pm_gen, c->d_err, c->fault};
+                const hipError_t e = dlr::launch_grad_rt(rt, c->D, B, c->resid, c->w, nullptr, lr, C, true, &next,
+                                                         t.pm_p, c->stream, &mg);
+                if (e == hipSuccess) {
+                    ++t.pm_gen;
+                    c->pm_ready = nx;
+                }
+                return e;
+            }
             const hipError_t e =
                 dlr::launch_grad_rt(rt, c->D, B, c->resid, c->w, nullptr, lr, C, true, &next, t.pm_p, c->stream);
             if (e == hipSuccess) c->pm_ready = nx;
@@ -2840,11 +2852,15 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 // the margin inside the gradient launch (DLR_PM_MG=0: its own
                 // launch, k_pm_margin)
                 const char *pg = getenv("DLR_PM_MG");
-                t.pm_mg = t.pm_fused && !t.rt && !(pg && strcmp(pg, "0") == 0);
+                t.pm_mg = t.pm_fused && !(pg && strcmp(pg, "0") == 0);
                 // ... only if every batch's launch is resident at once
-                // (grad_lds_mg_ok; otherwise pass 2 runs in k_pm_margin)
+                // (grad_lds_mg_ok / grad_rt_mg_ok; otherwise pass 2 runs in
+                // k_pm_margin)
                 for (int64_t b = 0; t.pm_mg && b < nb; ++b)
-                    t.pm_mg = dlr::grad_lds_mg_ok(pm_view(c, b), c->D, t.plan[(size_t)b].rows, t.phases, (int)(t.pR / 4096));
+                    t.pm_mg = t.rt ? dlr::grad_rt_mg_ok(pm_view(c, b), c->D, t.plan[(size_t)b].rows, t.rt_rounds,
+                                                        t.rt_val == nullptr)
+                                   : dlr::grad_lds_mg_ok(pm_view(c, b), c->D, t.plan[(size_t)b].rows, t.phases,
+                                                         (int)(t.pR / 4096));
                 if (t.pm_mg) {
                     const size_t cb = (size_t)dlr::DevP2::kMgCntWords * 4;
                     if ((rc = dev_alloc(c, (void **)&t.pm_cnt, cb))) return rc;

@@ -212,6 +212,7 @@ struct DevP2 {
 constexpr int kRtRows = 8192;       // rows per round: 32 KB of residuals in LDS
 constexpr int kRtMaxRounds = 8;     // batches of up to 65,536 rows
 constexpr int kRtCap = 20480;       // entries of one slice (their products live in LDS)
+constexpr int kRtRegions = kRtCap / 4096;  // pass-2 regions (kPmCap floats) in the product area (MG)
 constexpr int kRtMaxRound = 4096;   // entries of one (slice, round): a 4-entry group per thread
 struct DevRt {
     const uint32_t *gq;
@@ -364,8 +365,11 @@ hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const flo
 // The row-round gradient (DevRt): the update (fused) or the pushed gradient
 // (gout); next != null (fused only): also the next batch's products, as
 // launch_grad_lds_pm.  resid must hold rounds * kRtRows floats.
+// mg (one rank, with next): batch b's pass 2 in the same launch, as
+// launch_grad_lds_pm; grad_rt_mg_ok says whether the batch's shape allows it.
 hipError_t launch_grad_rt(const DevRt &rt, int64_t D, int64_t B, const float *resid, float *w, float *gout, float lr,
-                          float C, bool fused, const DevPm *next, float *p, hipStream_t s);
+                          float C, bool fused, const DevPm *next, float *p, hipStream_t s, const DevP2 *mg = nullptr);
+bool grad_rt_mg_ok(const DevPm &cur, int64_t D, int64_t B, int rounds, bool unit);
 // Touched-column layout (dlr_kernels.hip "Touched-column layout"): cs.ptr
 // spans the ncols touched columns cols[] of the batch.
 hipError_t launch_grad_touched(const DevCsc &cs, const uint32_t *cols, int64_t ncols, const float *resid,

@@ -1000,6 +1000,9 @@ constexpr int kMgSub = 8;  // sub-counters per phase (DevP2)
 #ifndef DLR_GRP_PIPE  // 1: 24.57 vs 24.97-25.00 us (profiles/r05_c2_issue_order.txt)
 #define DLR_GRP_PIPE 1
 #endif
+#ifndef DLR_RT_POLLER  // k_grad_rt MG: the wave that polls (A/B: 15 = the last, no entry loads)
+#define DLR_RT_POLLER 0
+#endif
 #ifndef DLR_MG_POLL_FIRST
 #define DLR_MG_POLL_FIRST 0
 #endif
@@ -1819,11 +1822,18 @@ __device__ __forceinline__ void unroll_seq(F &&f, std::integer_sequence<int, I..
     (f(std::integral_constant<int, I>{}), ...);
 }
 
-template <bool FUSED, bool PM, bool UNIT>
+// MG (with PM; one rank): this batch's pass 2 runs at the start of the
+// launch, as in k_grad_lds MG: wave v < 5 of workgroup x sums block
+// x + grid * v in the product area (not yet in use), stores its residuals
+// with sc1 and counts them per round; the round's entries are loaded
+// meanwhile, and wave 0 waits for every round's blocks before any residual
+// load (plain loads of lines no CU read before their block was published).
+template <bool FUSED, bool PM, bool UNIT, bool MG = false>
 __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_rt(DevRt rt, int64_t D, const float *__restrict__ resid,
                                                                float *__restrict__ w, float *__restrict__ gout,
                                                                float Bf, double Bd, float lr, float C,
-                                                               DevPm pn = DevPm{}, float *__restrict__ pm_p = nullptr) {
+                                                               DevPm pn = DevPm{}, float *__restrict__ pm_p = nullptr,
+                                                               DevP2 p2 = DevP2{}) {
     constexpr int NT = kGradWaves * kWave;
     constexpr int NG = kGradNG;
     constexpr int kSink = 16;  // the sink slot kRtCap and the chain's unclamped reads past a run
@@ -1837,6 +1847,57 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_rt(DevRt rt, int64_t
     const int64_t gfirst = (int64_t)s * (kGradWaves * NG) + wv;
     DLR_STAMP(0);
     const int T = rt.rounds;
+    static_assert(!MG || (PM && FUSED), "the fused margin comes with the fused pass 1");
+    if constexpr (MG) {
+        if (blockIdx.x == 0 && wv < 8)  // the next launch's bank (DevP2)
+            p2.cnt[(((p2.gen + 1) & 1) * 64 + lane) * kMgSub * 32 + wv * 32] = 0u;
+        const int64_t k2 = blockIdx.x + (int64_t)gridDim.x * wv;  // wv < kRtRegions (launch_grad_rt)
+        if (wv < kRtRegions && k2 < p2.pm.nblk) {  // wave-uniform
+            pm_rowsum<8, true>(p2.pm, p2.bt, pm_p, p2.resid, k2, smem + wv * kPmCap, lane);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every residual of the block stored
+            if (lane == 0 && !(p2.fault == kFaultMgPublish && k2 == 0))
+                __hip_atomic_fetch_add(
+                    p2.cnt + (((p2.gen & 1) * 64 + (k2 * kPmRows) / kRtRows) * kMgSub + (k2 % kMgSub)) * 32, 1u,
+                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        lds_barrier();  // the regions are read: the product area is free
+    }
+    const float *rsrc = MG ? p2.resid : resid;
+    // (MG) wave kPoller waits until every round's blocks are published; the
+    // caller's barrier holds the other waves' residual loads.  (A/B,
+    // DLR_RT_POLLER=15: the last wave, which sums no block and, when no group
+    // of a round falls to it, issues no entry loads either -- measured no
+    // faster.)
+    constexpr int kPoller = DLR_RT_POLLER;
+    static_assert(kPoller == 0 || kPoller >= kRtRegions, "the poller sums no block");
+    auto mg_wait_all = [&]() {
+        if constexpr (MG) {
+            if (wv == kPoller) {
+                Spin spin(p2.err, kErrMgPublish);
+                const __amdgpu_buffer_rsrc_t crs =
+                    __builtin_amdgcn_make_buffer_rsrc(p2.cnt, 0, 0x7FFFFFFF, 0x00020000);
+                constexpr int64_t bpr = kRtRows / kPmRows;
+                // lane 8d + s: sub-counter s of round d (rounds past the last
+                // read the last one again)
+                const int q = min((lane >> 3) & (kRtMaxRounds - 1), T - 1);
+                const int off = (int)(((((p2.gen & 1) * 64 + q) * kMgSub + (lane & (kMgSub - 1))) * 32) * 4);
+                for (int k = 0; spin.more(k); ++k) {
+                    const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(crs, off, 0, 16);
+                    bool all = true;
+#pragma unroll
+                    for (int d = 0; d < kRtMaxRounds; ++d) {
+                        uint32_t n = 0;
+#pragma unroll
+                        for (int i = 0; i < kMgSub; ++i) n += __builtin_amdgcn_readlane(v, d * kMgSub + i);
+                        const uint32_t want = d < T ? (uint32_t)(min<int64_t>(p2.pm.nblk, (d + 1) * bpr) - d * bpr) : 0u;
+                        all = all && n >= want;
+                    }
+                    if (all) break;
+                    __builtin_amdgcn_s_sleep(DLR_MG_SLEEP);
+                }
+            }
+        }
+    };
     // residuals: three register sets, always indexed by compile-time
     // constants (rounds are unrolled by unroll_seq; a runtime-indexed set
     // goes to scratch).  Native vectors: a float4 struct copied to LDS goes
@@ -1846,7 +1907,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_rt(DevRt rt, int64_t
     };
     Rnd rr[3];
     auto issue = [&](int t, Rnd &x) __attribute__((always_inline)) {
-        const v4f *src = reinterpret_cast<const v4f *>(resid + (int64_t)t * kRtRows);
+        const v4f *src = reinterpret_cast<const v4f *>(rsrc + (int64_t)t * kRtRows);
         x.r0 = src[threadIdx.x];
         x.r1 = src[NT + threadIdx.x];
     };
@@ -1857,22 +1918,38 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_rt(DevRt rt, int64_t
     const float4 *val4 = reinterpret_cast<const float4 *>(rt.val);
     uint4 eq[kRtMaxRounds];
     float4 ev[kRtMaxRounds];
+    const bool no_entries = MG && wv == kPoller && (unsigned)(wv * kWave) >= ngrp;  // (wave-uniform)
     auto entries = [&](auto tc) __attribute__((always_inline)) {
         constexpr int t = decltype(tc)::value;
         if (t >= T) return;  // uniform
+        if (no_entries) return;  // (never read: no thread of the wave is `mine`)
         const int64_t g = ((int64_t)s * T + t) * ngrp + (mine ? threadIdx.x : 0u);
         eq[t] = load_stream(gq4 + g);
         ev[t] = UNIT ? make_float4(1.f, 1.f, 1.f, 1.f) : load_stream(val4 + g);
     };
     // the memory pipeline is in order: what round 0 needs first, then the
     // rest of the first rounds; rounds 4+ are issued four rounds ahead
-    issue(0, rr[0]);
-    entries(std::integral_constant<int, 0>{});
-    if (T > 1) issue(1, rr[1]);
-    entries(std::integral_constant<int, 1>{});
-    if (T > 2) issue(2, rr[2]);
-    entries(std::integral_constant<int, 2>{});
-    entries(std::integral_constant<int, 3>{});
+    // (MG: the entries first, then -- after every round's blocks are
+    // published -- the residuals)
+    if constexpr (MG) {
+        entries(std::integral_constant<int, 0>{});
+        entries(std::integral_constant<int, 1>{});
+        entries(std::integral_constant<int, 2>{});
+        entries(std::integral_constant<int, 3>{});
+        mg_wait_all();
+        lds_barrier();
+        issue(0, rr[0]);
+        if (T > 1) issue(1, rr[1]);
+        if (T > 2) issue(2, rr[2]);
+    } else {
+        issue(0, rr[0]);
+        entries(std::integral_constant<int, 0>{});
+        if (T > 1) issue(1, rr[1]);
+        entries(std::integral_constant<int, 1>{});
+        if (T > 2) issue(2, rr[2]);
+        entries(std::integral_constant<int, 2>{});
+        entries(std::integral_constant<int, 3>{});
+    }
     // this lane's columns (as k_grad_lds): weights and column-major runs
     float wj[NG];
     unsigned cb[NG], ce[NG];
@@ -4582,18 +4659,59 @@ hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const flo
     return hipGetLastError();
 }
 
+namespace {
+size_t grad_rt_lds() {
+    return std::max((size_t)(kRtCap + 16 + 2 * kRtRows) * 4, (size_t)(kPmSlice + kPmMaxBlocks) * 4);
+}
+const void *grad_rt_mg_fn(bool unit) {
+    return unit ? reinterpret_cast<const void *>(&k_grad_rt<true, true, true, true>)
+                : reinterpret_cast<const void *>(&k_grad_rt<true, true, false, true>);
+}
+}  // namespace
+
+// Whether batch b's pass 2 may run in its row-round gradient's launch: a
+// batch of >= 2 rounds (C2 at B = 16,384: 15.2 vs 16.6 us per step; at one
+// round, B = 8,192, the separate pass 2 is faster: 13.9 vs 14.9,
+// profiles/r05_c2_rt_mg.txt), every block has a summing wave (wave v <
+// kRtRegions of workgroup x sums block x + grid * v) and every workgroup of
+// the launch is resident at once.
+bool grad_rt_mg_ok(const DevPm &cur, int64_t D, int64_t B, int rounds, bool unit) {
+    const int64_t grid = (D + kPmSlice - 1) / kPmSlice;
+    if (!(D > 0 && cur.groups <= 8 && cur.nblk == (B + kPmRows - 1) / kPmRows && cur.nblk <= grid * kRtRegions &&
+          rounds >= 2 && rounds <= kRtMaxRounds && (int64_t)rounds * kRtRows >= B))
+        return false;
+    static int cap[64][2] = {};  // per device and value kind (cached: the check runs every step)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    int &c = cap[dev][unit];
+    if (c == 0) c = resident_grid(grad_rt_mg_fn(unit), kGradWaves * kWave, grad_rt_lds());
+    return c > 0 && grid <= c;
+}
+
 hipError_t launch_grad_rt(const DevRt &rt, int64_t D, int64_t B, const float *resid, float *w, float *gout, float lr,
-                          float C, bool fused, const DevPm *next, float *p, hipStream_t s) {
+                          float C, bool fused, const DevPm *next, float *p, hipStream_t s, const DevP2 *mg) {
     if (D <= 0) return hipSuccess;
-    if (rt.rounds < 1 || rt.rounds > kRtMaxRounds || (next && !fused)) return hipErrorInvalidValue;
+    if (rt.rounds < 1 || rt.rounds > kRtMaxRounds || (next && !fused) || (mg && !next)) return hipErrorInvalidValue;
+    if (mg && (!grad_rt_mg_ok(mg->pm, D, B, rt.rounds, rt.val == nullptr) || mg->bt.rows != B || !mg->cnt ||
+               !mg->resid))
+        return hipErrorInvalidValue;
     const unsigned grid = (unsigned)((D + kPmSlice - 1) / kPmSlice);
     static_assert(kGradWaves * kGradNG * 64 == kPmSlice, "a gradient workgroup's columns are one slice");
     if (next && ((int64_t)grid != next->S || next->nblk > kPmMaxBlocks)) return hipErrorInvalidValue;
     const dim3 blk(kGradWaves * kWave);
     const float Bf = (float)B;
     const double Bd = (double)B;
-    const size_t lds = std::max((size_t)(kRtCap + 16 + 2 * kRtRows) * 4, (size_t)(kPmSlice + kPmMaxBlocks) * 4);
+    const size_t lds = grad_rt_lds();
     const bool unit = rt.val == nullptr;
+    if (mg) {
+        if (unit)
+            hipLaunchKernelGGL((k_grad_rt<true, true, true, true>), dim3(grid), blk, lds, s, rt, D, resid, w, gout, Bf,
+                               Bd, lr, C, *next, p, *mg);
+        else
+            hipLaunchKernelGGL((k_grad_rt<true, true, false, true>), dim3(grid), blk, lds, s, rt, D, resid, w, gout,
+                               Bf, Bd, lr, C, *next, p, *mg);
+        return hipGetLastError();
+    }
 #define DLR_GRT(F, PMX, U)                                                                                     \
     hipLaunchKernelGGL((k_grad_rt<F, PMX, U>), dim3(grid), blk, lds, s, rt, D, resid, w, gout, Bf, Bd, lr, C, \
                        next ? *next : DevPm{}, p)

@@ -62,12 +62,14 @@ def _expect_device_error(fn):
     return str(ei.value)
 
 
-def test_mg_withheld_block_raises_then_reload_recovers():
+@pytest.mark.parametrize("B", [20_000, 16_384])
+def test_mg_withheld_block_raises_then_reload_recovers(B):
     # the one-launch step (kind 3) at D = 2^20 (256 slices: resident); margin
     # block 0 never publishes -> every CU's phase-0 wait runs out -> the
-    # step's weights are never returned
+    # step's weights are never returned.  B = 16,384: the row-round gradient
+    # (k_grad_rt MG), whose wave 0 waits for every round's blocks.
     D = 1 << 20
-    n, B = 45_000, 20_000
+    n = 45_000
     ds = dlr.Dataset.generate(n, D, 20, value_mode=1, seed=9, stream=1)
     rp, col, val, lab = ds.csr()
     w0 = dlr.init_weight(D)
