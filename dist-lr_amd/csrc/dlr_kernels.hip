@@ -4605,7 +4605,8 @@ bool grad_lds_mg_ok(const DevPm &cur, int64_t D, int64_t B, int phases, int fill
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
     int &c = cap[dev][db][fill];
     if (c == 0) c = resident_grid(grad_lds_mg_fn(fill, db), kGradWaves * kWave, grad_lds_pm_lds(fill, db));
-    if (getenv("DLR_DEBUG_MG"))
+    static const bool debug = getenv("DLR_DEBUG_MG") != nullptr;  // (checked every step)
+    if (debug)
         fprintf(stderr, "grad_lds_mg_ok: dev %d fill %d db %d resident %d cus %d grid %lld mgrid %lld\n", dev, fill,
                 (int)db, c, device_cus(), (long long)grid, (long long)grad_lds_mg_grid(cur.nblk, grid));
     return c > 0 && grad_lds_mg_grid(cur.nblk, grid) <= c;
