@@ -17,6 +17,8 @@
 #include <cstring>
 #include <functional>
 #include <memory>
+#include <mutex>
+#include <optional>
 #include <string>
 #include <thread>
 #include <type_traits>
@@ -101,6 +103,9 @@ struct TrainShard {
     // batch's pass 2 (DevP2): pm_cnt its hand-off counters, pm_gen the
     // launches so far.
     bool pm = false, pm_fused = false, pm_mg = false;
+    // the one-launch step (pm_mg) or K6r (dref) would have been used, but
+    // this context's in-launch wait ran out before (dlr_ctx::mg_demoted)
+    bool mg_demoted = false;
     // band mode (classic layout, batches of >= 2^21 rows: C2 at B = -1): the
     // margin as the product margin over WINDOWS of kPmWinRows rows (pass 1 +
     // pass 2 per window; the weights do not change inside the step); the
@@ -281,7 +286,15 @@ struct dlr_ctx {
     // host-mapped memory the kernels store to when a bounded wait runs out
     // (h_err: host view, d_err: device view); checked by check_device
     uint32_t *h_err = nullptr, *d_err = nullptr;
-    int fault = dlr::kFaultNone;  // dlr_set_fault (tests)
+    // ... followed by kStatWords event counters the kernels add to (DevStat;
+    // d_stat = d_err + kErrWords), and the host's own (dlr_stage_counters)
+    uint32_t *d_stat = nullptr;
+    int64_t hcount[DLR_COUNTERS] = {};
+    int fault = dlr::kFaultNone;  // dlr_set_fault (tests; cleared by every load)
+    // an in-launch wait of this context's one-launch step (kErrMgPublish) or
+    // K6r (kErrRef*) ran out: the device did not hold the whole grid (another
+    // process's work, CowaitScope) -- later loads use the separate launches
+    bool mg_demoted = false, dref_demoted = false;
     TrainShard train;
     TestShard test;
     // exchange / next-margin overlap (TrainShard::xslices): asked for unless
@@ -393,15 +406,91 @@ int check_device(dlr_ctx *c, const char *who) {
         if (__atomic_load_n(c->h_err + k, __ATOMIC_ACQUIRE) == 0u) continue;
         msg += msg.empty() ? "" : "; ";
         msg += what[k];
+        if (k == dlr::kErrMgPublish) c->mg_demoted = true;
+        if (k == dlr::kErrRefSlot || k == dlr::kErrRefLimit || k == dlr::kErrRefLds) c->dref_demoted = true;
     }
     if (msg.empty()) return DLR_OK;
     return fail(c, DLR_E_DEVICE, std::string(who) + ": in-launch wait ran out: " + msg +
-                                     " -- the weights are not the reference's; reload the shard");
+                                     " -- the weights are not the reference's; reload the shard" +
+                                     (c->mg_demoted || c->dref_demoted
+                                          ? " (this context's later loads run those steps in separate launches)"
+                                          : ""));
 }
 
 void clear_device_errors(dlr_ctx *c) {
     if (c->h_err)
         for (int k = 0; k < dlr::kErrWords; ++k) __atomic_store_n(c->h_err + k, 0u, __ATOMIC_RELEASE);
+}
+
+// dlr_stage_counters' counts start again with each loaded shard
+void clear_counters(dlr_ctx *c) {
+    if (c->h_err)
+        for (int k = 0; k < dlr::kStatWords; ++k) __atomic_store_n(c->h_err + dlr::kErrWords + k, 0u, __ATOMIC_RELEASE);
+    for (int64_t &v : c->hcount) v = 0;
+}
+
+// CO-WAITING LAUNCHES.  The one-launch step (k_grad_lds / k_grad_rt MG),
+// K6r (k_dense_ref) and the hot chains (k_hot_chain beside their band's
+// margins) have workgroups that wait INSIDE the GPU for data other
+// workgroups produce; they are sized to what the device holds at once
+// (resident_grid).  Two such grids from different streams -- two contexts
+// in one process (loopback ranks, engines on threads), or one context's
+// streams -- could each hold part of the CUs and wait for the rest.  So
+// every co-waiting launch (or launch sequence) of this process is queued
+// after the previous one of ANOTHER stream: under a process-wide lock, the
+// stream waits on an event recorded on that stream, and the lock is held
+// until the sequence is queued.  A context that keeps to one stream adds no
+// API call (the common case: one engine per process).  Other PROCESSES are
+// not covered: their launches are bounded by the in-launch waits (250 ms,
+// DLR_E_DEVICE), after which this context stops using the one-launch step
+// (mg_demoted).
+struct CowaitOrder {
+    std::mutex mu;
+    hipStream_t last[64] = {};  // per device: the stream of the last co-waiting sequence
+    hipEvent_t ev[64] = {};
+};
+CowaitOrder &cowait_order() {
+    static CowaitOrder *o = new CowaitOrder;  // (never destroyed: contexts may outlive static destructors)
+    return *o;
+}
+
+class CowaitScope {
+  public:
+    CowaitScope(dlr_ctx *c, hipStream_t s) : c_(c), s_(s), lk_(cowait_order().mu) {}
+    CowaitScope(const CowaitScope &) = delete;
+    CowaitScope &operator=(const CowaitScope &) = delete;
+    // order s after the last co-waiting sequence of another stream
+    hipError_t begin() {
+        CowaitOrder &o = cowait_order();
+        const int d = c_->device;
+        if (d < 0 || d >= 64) return hipErrorInvalidDevice;
+        if (o.last[d] && o.last[d] != s_) {
+            if (!o.ev[d]) {
+                const hipError_t e = hipEventCreateWithFlags(&o.ev[d], hipEventDisableTiming);
+                if (e != hipSuccess) return e;
+            }
+            hipError_t e = hipEventRecord(o.ev[d], o.last[d]);
+            if (e == hipSuccess) e = hipStreamWaitEvent(s_, o.ev[d], 0);
+            if (e != hipSuccess) return e;
+            ++c_->hcount[DLR_COUNT_COWAIT_SERIALISED];
+        }
+        o.last[d] = s_;
+        return hipSuccess;
+    }
+
+  private:
+    dlr_ctx *c_;
+    hipStream_t s_;
+    std::lock_guard<std::mutex> lk_;
+};
+
+// a destroyed stream is no longer anyone's predecessor
+void cowait_forget(dlr_ctx *c) {
+    CowaitOrder &o = cowait_order();
+    std::lock_guard<std::mutex> lk(o.mu);
+    if (c->device < 0 || c->device >= 64) return;
+    hipStream_t &l = o.last[c->device];
+    if (l && (l == c->stream || l == c->hstream || l == c->gstream)) l = nullptr;
 }
 
 int dev_alloc(dlr_ctx *c, void **p, size_t bytes) {
@@ -483,7 +572,9 @@ void free_train(dlr_ctx *c) {
         dev_free(c, p);
     t = TrainShard();
     c->pm_ready = -1;
-    clear_device_errors(c);  // nothing of the old shard runs any more
+    c->fault = dlr::kFaultNone;  // (test knob: one shard at most)
+    clear_device_errors(c);      // nothing of the old shard runs any more
+    clear_counters(c);
 }
 
 template <typename T>
@@ -1058,9 +1149,10 @@ void build_bands(const std::vector<uint32_t> &cptr, const std::vector<RowT> &cro
 // of them in the stream, 5.70 / 5.71 / 5.72 / 6.53 ms per step -- the
 // margin's hot-product writes grow with them, the band kernels' chains
 // shrink; profiles/r05_c3_hot_stream_max.txt)
-// A band flag not seen for this long ends the first k_hot_chain launch (the
-// resume launch finishes the chains): far above the ~0.1-0.3 ms between
-// flags when the margins run beside it, far below the 250 ms error bound
+// A band flag not seen for this long ends a k_hot_chain launch that is not
+// the step's last (the next one goes on; counted, DLR_COUNT_HOT_GIVEUPS):
+// far above the ~0.1-0.3 ms between flags when the margins run beside it,
+// far below the 250 ms error bound
 constexpr uint32_t kHsGiveUpTicks = 2000000;  // 20 ms at 100 MHz
 // rows of a window of the band-mode product margin (TrainShard::pmw): the
 // product margin's 1,024 blocks of 64 rows
@@ -1998,7 +2090,10 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
             const int64_t nw = dlr::dense_ref_sync_words(B);
             const dlr::DevRefSync sy{t.dref_sync, t.dref_sync + nw - 64, t.dref_sync + nw - 32, t.dref_seq,
                                      t.dref_lead, 0, c->d_err, c->fault};
-            e = dlr::launch_dense_ref(dd, first, B, c->w, gout, c->resid, sy, lr, C, fused, c->stream);
+            CowaitScope cw(c, c->stream);
+            e = cw.begin();
+            if (e == hipSuccess)
+                e = dlr::launch_dense_ref(dd, first, B, c->w, gout, c->resid, sy, lr, C, fused, c->stream);
             if (e == hipSuccess) ++c->train.dref_seq;
         } else if (e == hipSuccess)
             e = t.dfused ? dlr::launch_dense_combine(t.dpart, c->D, B, c->w, gout, lr, C, fused, c->stream)
@@ -2016,8 +2111,11 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
             const dlr::DevPm next = pm_view(c, nx);
             if (pm_mg_ok(c, b)) {  // this batch's pass 2 in the same launch
                 const dlr::DevP2 mg{pm_view(c, b), batch_view(c, b), c->resid, t.pm_cnt, t.pm_gen, c->d_err, c->fault};
-                const hipError_t e = dlr::launch_grad_rt(rt, c->D, B, c->resid, c->w, nullptr, lr, C, true, &next,
-                                                         t.pm_p, c->stream, &mg);
+                CowaitScope cw(c, c->stream);
+                hipError_t e = cw.begin();
+                if (e == hipSuccess)
+                    e = dlr::launch_grad_rt(rt, c->D, B, c->resid, c->w, nullptr, lr, C, true, &next, t.pm_p, c->stream,
+                                            &mg);
                 if (e == hipSuccess) {
                     ++t.pm_gen;
                     c->pm_ready = nx;
@@ -2037,8 +2135,11 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
             const int64_t nx = (b + 1) % (int64_t)t.plan.size();
             if (pm_mg_ok(c, b)) {
                 const dlr::DevP2 mg{pm_view(c, b), batch_view(c, b), c->resid, t.pm_cnt, t.pm_gen, c->d_err, c->fault};
-                const hipError_t e = dlr::launch_grad_lds_pm(pcsc_view(c, b), c->D, B, c->resid, c->w, lr, C,
-                                                             pm_view(c, nx), t.pm_p, c->stream, &mg);
+                CowaitScope cw(c, c->stream);
+                hipError_t e = cw.begin();
+                if (e == hipSuccess)
+                    e = dlr::launch_grad_lds_pm(pcsc_view(c, b), c->D, B, c->resid, c->w, lr, C, pm_view(c, nx), t.pm_p,
+                                                c->stream, &mg);
                 if (e == hipSuccess) {
                     ++t.pm_gen;
                     c->pm_ready = nx;
@@ -2131,6 +2232,15 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
     const size_t esz = t.row16 ? 2 : 4;
     const dlr::DevBatch all = batch_view(c, b);
     const int64_t BR = (int64_t)1 << t.band_shift;
+    // the hot chains wait inside the GPU for the margins beside them: the
+    // whole step is one co-waiting sequence (CowaitScope; everything below
+    // starts after the engine stream's first operation and joins it at the
+    // end)
+    std::optional<CowaitScope> cw;
+    if (hs) {
+        cw.emplace(c, c->stream);
+        if ((e = cw->begin()) != hipSuccess) return e;
+    }
     // the running sums are cleared on the engine stream (so the long-column
     // phases below are ordered after it too); the bands' stream starts
     // after that and everything queued before this step
@@ -2140,11 +2250,11 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
     if (e == hipSuccess && hot) e = hipStreamWaitEvent(c->hstream, c->ev_bstart, 0);
     dlr::DevHotOut ho{};
     dlr::DevHotChain hc{};
+    int64_t hc_end = 1;  // the band after which the next chain launch is queued
     if (hs) {
         ++t.hs_seq;
         hc = dlr::DevHotChain{t.hs_cols + t.hsco[bb], t.hs_seg + t.hsso[bb], t.hs_buf, t.hs_flag, nh, nbands,
-                              t.hs_seq, c->d_err, c->fault, t.hs_state, 0, kHsGiveUpTicks};
-        if (e == hipSuccess) e = dlr::launch_hot_chain(hc, t.gacc, c->hstream);
+                              t.hs_seq, c->d_err, c->fault, t.hs_state, 0, 0, kHsGiveUpTicks, c->d_stat};
         ho = dlr::DevHotOut{t.hs_off + t.hsoo[bb], t.hs_dest, t.hs_val, t.hs_buf};
     }
     for (int64_t k = 0; e == hipSuccess && k < nbands; ++k) {
@@ -2160,6 +2270,17 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
             : t.pmw      ? launch_pm_windows(c, b, r0, r1)
                          : dlr::launch_margin_residual(sub, c->w, c->resid + r0, c->stream);
         if (e == hipSuccess && hs) e = dlr::launch_flag_store(t.hs_flag + k, t.hs_seq, c->stream);
+        // the hot chains of bands [hc.b1, k + 1), queued after their margins
+        // (DevHotChain): groups of 1, 1, 2, 4, ... bands -- the first starts
+        // right after band 0's margin, and a later one waits behind the one
+        // before on hstream, so only a launch boundary per group is added
+        if (e == hipSuccess && hs && (k + 1 == hc_end || k + 1 == nbands)) {
+            hc.b0 = hc.b1;
+            hc.b1 = k + 1;
+            e = dlr::launch_hot_chain(hc, t.gacc, c->hstream);
+            ++c->hcount[DLR_COUNT_HOT_CHAIN_LAUNCHES];
+            hc_end = 2 * (k + 1);
+        }
         if (e == hipSuccess) e = hipEventRecord(c->ev_band[(size_t)k], c->stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(c->gstream, c->ev_band[(size_t)k], 0);
         const TrainShard::Band &bd = t.bands[(size_t)(t.bfirst[bb] + k)];
@@ -2178,13 +2299,6 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
     if (e == hipSuccess) e = launch_long_columns(c, b, B, gout, lr, C, fused);
     if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_bdone, 0);
     if (e == hipSuccess && hot) e = hipStreamWaitEvent(c->stream, c->ev_hdone, 0);
-    // the hot chains the first launch could not finish (it gives up on a
-    // flag when the margins cannot run beside it; DevHotChain): after every
-    // margin and that launch -- nothing to do in a concurrent run
-    if (e == hipSuccess && hs) {
-        hc.resume = 1;
-        e = dlr::launch_hot_chain(hc, t.gacc, c->stream);
-    }
     if (e == hipSuccess) e = dlr::launch_band_finalize(t.gacc, c->w, gout, c->D, B, lr, C, fused, c->stream);
     return e;
 }
@@ -2362,9 +2476,12 @@ int create_ctx(int device, int rank, int world, int64_t D, dlr::Comm *comm, dlr_
     if ((rc = dev_alloc(c.get(), (void **)&c->correct, 64))) return rc;
     HIPC(c.get(), hipHostMalloc((void **)&c->h_correct, 64, hipHostMallocDefault));
     HIPC(c.get(), hipHostMalloc((void **)&c->h_ll, 64, hipHostMallocDefault));
-    HIPC(c.get(), hipHostMalloc((void **)&c->h_err, dlr::kErrWords * 4, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPC(c.get(), hipHostMalloc((void **)&c->h_err, (dlr::kErrWords + dlr::kStatWords) * 4,
+                                hipHostMallocMapped | hipHostMallocCoherent));
     HIPC(c.get(), hipHostGetDevicePointer((void **)&c->d_err, c->h_err, 0));
+    c->d_stat = c->d_err + dlr::kErrWords;
     clear_device_errors(c.get());
+    clear_counters(c.get());
     // Gradient + receive buffers serve both the exchange and the
     // host-exchange (worker/server) entry points.
     if ((rc = dev_alloc(c.get(), (void **)&c->g, (size_t)c->Dpad * 4))) return rc;
@@ -2438,6 +2555,7 @@ int dlr_comm_abort(dlr_ctx *c, const char *why) {
 void dlr_destroy(dlr_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    cowait_forget(ctx);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->cstream) (void)hipStreamSynchronize(ctx->cstream);
     if (ctx->gstream) (void)hipStreamSynchronize(ctx->gstream);
@@ -2853,6 +2971,8 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 // launch, k_pm_margin)
                 const char *pg = getenv("DLR_PM_MG");
                 t.pm_mg = t.pm_fused && !(pg && strcmp(pg, "0") == 0);
+                t.mg_demoted = t.pm_mg && c->mg_demoted;
+                if (t.mg_demoted) t.pm_mg = false;
                 // ... only if every batch's launch is resident at once
                 // (grad_lds_mg_ok / grad_rt_mg_ok; otherwise pass 2 runs in
                 // k_pm_margin)
@@ -3263,6 +3383,8 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
         // margin kernel, then the column-chain kernel -- the same order)
         const char *dr = getenv("DLR_DENSE_REF");
         t.dref = dlr::dense_ref_ok(D, ds->n_rows, t.B) && (dr ? strcmp(dr, "0") != 0 : big);
+        t.mg_demoted = t.dref && c->dref_demoted;
+        if (t.mg_demoted) t.dref = false;
         // how far (in 256-row slots) the margins may run ahead of the column
         // chains: the rows the chains re-read stay in the Infinity Cache
         // (DLR_DENSE_REF_LEAD: A/B; 0 = no limit)
@@ -3478,6 +3600,7 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
         time_end(c, 3, t0);
     }
     if (c->train.sparse_stream) HIPC(c, sparse_batch_done(c, b));
+    if (c->train.mg_demoted) ++c->hcount[DLR_COUNT_MG_DEMOTED];
     time_end(c, 4, t_step);
     return DLR_OK;
 }
@@ -3489,7 +3612,9 @@ int dlr_train_epoch(dlr_ctx *c, float lr, float C, int mode) {
         int rc = dlr_train_step(c, b, lr, C, mode);
         if (rc) return rc;
     }
-    return DLR_OK;
+    // the epoch's success is definitive: its last step's in-launch waits
+    // are known to have completed
+    return dlr_sync(c);
 }
 
 int dlr_worker_gradient(dlr_ctx *c, int64_t b, float C, float *grad_out, int64_t D) {
@@ -3664,6 +3789,20 @@ int dlr_stage_time(dlr_ctx *c, int stage, int64_t first, int64_t count, float lr
     if (e != hipSuccess) return fail(c, DLR_E_HIP, std::string("dlr_stage_time: ") + hipGetErrorString(e));
     if (avg_ms) *avg_ms = (double)ms / (double)count;
     return check_device(c, "dlr_stage_time");
+}
+
+int dlr_stage_counters(dlr_ctx *c, int64_t *out, int n) {
+    if (!c || !out || n < 0 || n > DLR_COUNTERS) return fail(c, DLR_E_ARG, "dlr_stage_counters: bad argument");
+    HIPC(c, hipSetDevice(c->device));
+    for (hipStream_t s : {c->stream, c->gstream, c->hstream})
+        if (s) HIPC(c, hipStreamSynchronize(s));
+    int64_t v[DLR_COUNTERS];
+    for (int k = 0; k < DLR_COUNTERS; ++k) v[k] = c->hcount[k];
+    if (c->h_err)
+        v[DLR_COUNT_HOT_GIVEUPS] =
+            (int64_t)__atomic_load_n(c->h_err + dlr::kErrWords + dlr::kStatHotGiveUps, __ATOMIC_ACQUIRE);
+    for (int k = 0; k < n; ++k) out[k] = v[k];
+    return DLR_OK;
 }
 
 int dlr_set_fault(dlr_ctx *c, int fault) {

@@ -129,8 +129,15 @@ enum DevErr {
     kErrRefLimit = 2,   // k_dense_ref: the chains' limit never reached a margin unit
     kErrRefLds = 3,     // k_dense_ref: a hand-off between the waves of a workgroup
     kErrHotLds = 4,     // k_band_hot / k_hot_chain: a hand-off between the waves of a workgroup
-    kErrHotFlag = 5,    // k_hot_chain (resume launch): a band's hot products were never published
+    kErrHotFlag = 5,    // k_hot_chain (last launch of a step): a band's hot products were never published
     kErrWords = 8
+};
+// Event counters the kernels keep beside the error words (same host-mapped
+// array, words kErrWords + k): cumulative since the shard was loaded,
+// reported by dlr_stage_counters.
+enum DevStat {
+    kStatHotGiveUps = 0,  // k_hot_chain: a column's launch stopped at a band flag (the next launch went on)
+    kStatWords = 8
 };
 // Test-only fault injection (dlr_set_fault): a producer that never comes.
 enum DevFault {
@@ -141,9 +148,13 @@ enum DevFault {
 };
 
 // The largest grid of `threads`-thread workgroups with `lds` bytes of
-// dynamic LDS that is resident at once on the current device (occupancy
-// per CU x CUs) for kernel `fn`; 0 if the runtime cannot say.
+// dynamic LDS that is resident at once on the current device when nothing
+// else runs on it (workgroups per CU x CUs) for kernel `fn`; 0 if its
+// attributes cannot be read.  resident_per_cu: per CU, from the kernel's
+// attributes and gfx950's budgets, capped by the runtime's occupancy query
+// when that answers >= 1 (*query: its answer, -1 on error).
 int resident_grid(const void *fn, int threads, size_t lds);
+int resident_per_cu(const void *fn, int threads, size_t lds, int *query);
 
 // PRODUCT MARGIN of one batch (dlr_kernels.hip "Product margin"; LDS-layout
 // batches).  The batch's rows fall in blocks of kPmRows; its columns in
@@ -273,17 +284,20 @@ struct DevHotOut {
 // The margin kernel of a band publishes the band's hot products: after it,
 // flag[band] = seq (agent scope).
 hipError_t launch_flag_store(uint32_t *flag, uint32_t seq, hipStream_t s);
-// The hot columns' chains of one batch, ONE launch for every band (a
-// workgroup per hot column, persistent over the step): the column's
-// products streamed from buf in order, band s once flag[s] >= seq; chain
-// sum from +0 in batch-row order; the sum stored to gacc[cols[h]].  seg:
-// per (column h, band s) the segment's (start, count) in buf, h-major.
-// The flags need the margins to run BESIDE this launch.  Where kernels are
-// serialised instead (e.g. under counter collection) a flag that does not
-// come within `giveup` ticks (100 MHz) ends the launch: each column's first
-// band not added and its sum so far go to state[h], and a RESUME launch
-// (resume = 1), queued after the last margin, adds the rest -- the same
-// chain, so the same bits.  The first launch always writes state.
+// The hot columns' chains of one batch over bands [b0, b1) (a workgroup
+// per 4 hot columns, persistent over its bands): the column's products
+// streamed from buf in order, band s once flag[s] >= seq; chain sum from +0
+// in batch-row order, continued across launches through state[h] (the
+// first band not added, the sum so far; every launch writes it); the sum
+// stored to gacc[cols[h]] by the launch that adds the last band.  seg: per
+// (column h, band s) the segment's (start, count) in buf, h-major.
+// The engine queues the launch for bands [b0, b1) after the margin of band
+// b1 - 1 (geometric groups: 1, 1, 2, 4, ... bands), so the flags a launch
+// waits on come from margins queued BEFORE it: beside it on another
+// hardware queue, or ahead of it when the streams share one.  A flag not
+// up within `giveup` ticks (100 MHz) ends a launch that is not the last
+// (stats[kStatHotGiveUps] += 1 per column; the next launch adds the rest,
+// the same chain, the same bits); the last launch records kErrHotFlag.
 struct DevHotChain {
     const uint32_t *cols;
     const uint2 *seg;
@@ -294,8 +308,9 @@ struct DevHotChain {
     uint32_t *err;
     int fault;
     uint2 *state;  // nh: (first band not added, the sum's bits)
-    int resume;
+    int64_t b0, b1;
     uint32_t giveup;
+    uint32_t *stats;  // host-mapped counters (kStat*), or null
 };
 constexpr int kHotChunkF = 256;  // floats of one stream chunk (a band segment starts at a multiple)
 hipError_t launch_hot_chain(const DevHotChain &hc, float *gacc, hipStream_t s);

@@ -2403,16 +2403,17 @@ __global__ __launch_bounds__(2 * kHcCols * kWave) void k_hot_chain(DevHotChain h
     const int64_t h = (int64_t)blockIdx.x * kHcCols + pr;
     if (h >= hc.nh) return;  // wave-uniform (no barrier after this point)
     const uint2 *seg = hc.seg + h * hc.nbands;
-    // the resume launch continues where the first one stopped (state[h]:
-    // the first band not added, the chain's sum so far); nothing if it ended
+    // a launch after the first continues where the one before stopped
+    // (state[h]: the first band not added, the chain's sum so far)
     int64_t s0 = 0;
     float acc0 = 0.0f;
-    if (hc.resume) {
+    if (hc.b0 > 0) {
         const uint2 st = hc.state[h];
         s0 = st.x;
         acc0 = __uint_as_float(st.y);
-        if (s0 >= hc.nbands) return;
     }
+    if (s0 >= hc.b1) return;  // (wave-uniform; state stays as it is)
+    const bool last = hc.b1 >= hc.nbands;
     Spin spin(hc.err, kErrHotLds);
     if (wv >= kHcCols) {
         // the loader: chunk g of the column's stream (bands in order) into
@@ -2420,15 +2421,17 @@ __global__ __launch_bounds__(2 * kHcCols * kWave) void k_hot_chain(DevHotChain h
         const __amdgpu_buffer_rsrc_t frs =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(hc.flag), 0, 0x7FFFFFFF, 0x00020000);
         uint32_t g = 0, landed = 0, ck = 0;  // chunks issued, posted landed, known consumed
-        for (int64_t s = s0; s < hc.nbands; ++s) {
+        for (int64_t s = s0; s < hc.b1; ++s) {
             const uint2 sg = seg[s];
             const uint32_t nch = (sg.y + kHotChunkF - 1) / kHotChunkF;
             if (nch > 0) {
-                // the band's products are published -- or, after kGiveUp
-                // without them (the margins cannot run beside this launch:
-                // kernels serialised, e.g. under counter collection), the
-                // rest is left to the resume launch, which the engine queues
-                // after the last margin
+                // the band's products are published -- or, after `giveup`
+                // ticks without them, the rest is left to the next launch
+                // (counted in stats).  The engine queues a launch after the
+                // margins of its last band, so a flag is up by the time its
+                // launch runs unless the margins run BEHIND it on the same
+                // hardware queue -- which then cannot happen -- or kernels
+                // run one at a time
                 bool up = false;
                 uint64_t t0 = 0;
                 for (int k = 0;; ++k) {
@@ -2443,10 +2446,13 @@ __global__ __launch_bounds__(2 * kHcCols * kWave) void k_hot_chain(DevHotChain h
                     __builtin_amdgcn_s_sleep(8);
                 }
                 if (!up) {
-                    // (the resume launch runs after every margin: a flag it
+                    // (the last launch runs after every margin: a flag it
                     // does not see is an error)
-                    if (hc.resume && hc.err && lane == 0)
+                    if (last && hc.err && lane == 0)
                         __hip_atomic_store(hc.err + kErrHotFlag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (!last && hc.stats && lane == 0)
+                        __hip_atomic_fetch_add(hc.stats + kStatHotGiveUps, 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
                     if (lane == 0) ctl_post(ctl + 2, 0x80000000u | (uint32_t)(s - s0));
                     break;
                 }
@@ -2490,7 +2496,7 @@ __global__ __launch_bounds__(2 * kHcCols * kWave) void k_hot_chain(DevHotChain h
     };
     v4f da[8], db[8];
     int64_t s = s0;
-    for (; s < hc.nbands; ++s) {
+    for (; s < hc.b1; ++s) {
         // the loader is past band s's flag, or gave up before it
         const uint32_t want = (uint32_t)(s - s0 + 1);
         if ((bk & 0x7FFFFFFFu) < want && !(bk & 0x80000000u)) {
@@ -2500,7 +2506,7 @@ __global__ __launch_bounds__(2 * kHcCols * kWave) void k_hot_chain(DevHotChain h
                 bk = ctl_read(ctl + 2);
             }
         }
-        if ((bk & 0x7FFFFFFFu) < want) break;  // gave up here: the resume launch adds the rest
+        if ((bk & 0x7FFFFFFFu) < want) break;  // gave up here: the next launch adds the rest
         const uint2 sg = seg[s];
         const uint32_t nfull = sg.y / kHotChunkF, rem = sg.y % kHotChunkF;
         if (nfull > 0) {
@@ -2534,7 +2540,7 @@ __global__ __launch_bounds__(2 * kHcCols * kWave) void k_hot_chain(DevHotChain h
     }
     if (lane == 0) {
         if (s >= hc.nbands) gacc[hc.cols[h]] = acc;
-        if (!hc.resume) hc.state[h] = make_uint2((uint32_t)s, __float_as_uint(acc));
+        hc.state[h] = make_uint2((uint32_t)s, __float_as_uint(acc));
     }
 }
 
@@ -4558,30 +4564,54 @@ int64_t grad_lds_mg_grid(int64_t nblk, int64_t grid) {
 }
 }  // namespace
 
-int resident_grid(const void *fn, int threads, size_t lds) {
-    if (!fn) return 0;
-    int per_cu = 0;
-    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds);
-    if (e != hipSuccess) (void)hipGetLastError();
-    if (e != hipSuccess || per_cu < 1) {
-        // The query failed (seen after ~100 tests in one process: every
-        // call then returned 0, while launches of the same kernel ran).  A
-        // kernel built with __launch_bounds__(threads) fits one workgroup of
-        // `threads` per CU in registers by construction, so one per CU is a
-        // lower bound whenever its LDS fits a CU's.
-        int dev = 0, cu_lds = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cu_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess) {
-            (void)hipGetLastError();
-            cu_lds = 0;
-        }
-        if (getenv("DLR_DEBUG_MG"))
-            fprintf(stderr, "resident_grid: occupancy query %d (%s), per_cu %d; CU LDS %d, request %zu\n", (int)e,
-                    hipGetErrorString(e), per_cu, cu_lds, lds);
-        per_cu = (cu_lds > 0 && lds <= (size_t)cu_lds && threads <= 1024) ? 1 : 0;
+// Workgroups of kernel fn (`threads` threads, `lds` bytes of dynamic LDS)
+// that one CU holds at once, from the kernel's own attributes and gfx950's
+// per-CU budgets (MI355X_MICROARCH.md, "Register files" and "Residency"):
+// VGPRs 512 per lane per SIMD, allocated in granules of 8; at most 8 waves
+// per SIMD and 32 per CU; SGPRs 800 per SIMD in granules of 16 plus 16 per
+// wave (taken at the 112-register ceiling of a wave, since the attributes
+// do not report SGPRs); a workgroup's waves spread over the 4 SIMDs; LDS
+// 160 KiB per CU (static + dynamic).  The runtime's occupancy query is
+// consulted too and the LOWER answer wins when it answers >= 1 -- it can
+// say one block per CU too many near the SGPR steps (the guide's table);
+// an answer of 0 (seen with hipSuccess: DESIGN.md 2.1) is not taken.
+int resident_per_cu(const void *fn, int threads, size_t lds, int *query) {
+    if (query) *query = -1;
+    if (!fn || threads < 1) return 0;
+    hipFuncAttributes a{};
+    if (hipFuncGetAttributes(&a, fn) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
     }
-    return per_cu * device_cus();
+    int dev = 0, cu_lds = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cu_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    if (threads > a.maxThreadsPerBlock) return 0;
+    const int waves = (threads + kWave - 1) / kWave;
+    const int per_simd = (waves + 3) / 4;  // a workgroup's waves on its busiest SIMD
+    const int valloc = ((std::max(a.numRegs, 1) + 7) / 8) * 8;
+    const int simd_waves = std::min({8, 512 / valloc, 800 / (112 + 16)});
+    int n = std::min(simd_waves / per_simd, 32 / waves);
+    const size_t need = a.sharedSizeBytes + lds;
+    if (need > 0) n = std::min<int64_t>(n, (int64_t)cu_lds / (int64_t)need);
+    int q = 0;
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, fn, threads, lds);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        q = -1;
+    }
+    if (query) *query = q;
+    if (q >= 1) n = std::min(n, q);
+    if (getenv("DLR_DEBUG_MG"))
+        fprintf(stderr, "resident_per_cu: regs %d (alloc %d) static LDS %zu + %zu of %d, %d threads: %d per CU (query %d)\n",
+                a.numRegs, valloc, a.sharedSizeBytes, lds, cu_lds, threads, std::max(n, 0), q);
+    return std::max(n, 0);
 }
+
+int resident_grid(const void *fn, int threads, size_t lds) { return resident_per_cu(fn, threads, lds, nullptr) * device_cus(); }
 
 // Whether batch b's pass 2 may run in its gradient's launch: the shape
 // fits, and every workgroup of the launch is resident at once -- each one

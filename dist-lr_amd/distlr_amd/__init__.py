@@ -32,6 +32,9 @@ ORDER_REFERENCE, ORDER_FAST = 0, 1
 E_DEVICE = -8  # an in-launch hand-off never came (dlr_sync)
 # test-only producer faults (dlr_set_fault)
 FAULT_NONE, FAULT_MG_PUBLISH, FAULT_REF_PUBLISH, FAULT_HOT_RING = 0, 1, 2, 3
+# dlr_stage_counters indices
+COUNT_HOT_CHAIN_LAUNCHES, COUNT_HOT_GIVEUPS, COUNT_COWAIT_SERIALISED, COUNT_MG_DEMOTED = 0, 1, 2, 3
+COUNTERS = 4
 
 # Exported symbols, in include/distlr_amd.h order (tests check the .so
 # exports every one of them).
@@ -50,7 +53,7 @@ SYMBOLS = [
     "dlr_summation_order",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
     "dlr_set_fault",
-    "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_train_layout", "dlr_train_band_rows", "dlr_train_relabeled", "dlr_train_unit_values", "dlr_train_product_margin", "dlr_train_hot_columns", "dlr_train_row_rounds",
+    "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_stage_counters", "dlr_train_layout", "dlr_train_band_rows", "dlr_train_relabeled", "dlr_train_unit_values", "dlr_train_product_margin", "dlr_train_hot_columns", "dlr_train_row_rounds",
     "dlr_set_exchange_overlap", "dlr_exchange_overlap", "dlr_set_exchange_pieces", "dlr_exchange_pieces",
     "dlr_memory_info", "dlr_stream_bytes",
 ]
@@ -164,6 +167,7 @@ _sig("dlr_set_fault", C.c_int, P, C.c_int)
 _sig("dlr_timing", C.c_int, P, C.c_int)
 _sig("dlr_kernel_time", C.c_int, P, C.c_int, C.POINTER(C.c_double), C.POINTER(i64))
 _sig("dlr_stage_time", C.c_int, P, C.c_int, i64, i64, C.c_float, C.c_float, C.POINTER(C.c_double))
+_sig("dlr_stage_counters", C.c_int, P, C.POINTER(i64), C.c_int)
 _sig("dlr_train_layout", C.c_int, P)
 _sig("dlr_train_band_rows", C.c_int, P)
 _sig("dlr_train_relabeled", C.c_int, P)
@@ -576,6 +580,14 @@ class Engine:
         ms = C.c_double()
         self._c(lib.dlr_stage_time(self._h, stage, first_batch, count, lr, C_, C.byref(ms)))
         return ms.value
+
+    def stage_counters(self) -> dict:
+        """Event counts since the shard was loaded (dlr_stage_counters):
+        hot_chain_launches, hot_giveups, cowait_serialised, mg_demoted."""
+        out = (i64 * COUNTERS)()
+        self._c(lib.dlr_stage_counters(self._h, out, COUNTERS))
+        return {"hot_chain_launches": out[COUNT_HOT_CHAIN_LAUNCHES], "hot_giveups": out[COUNT_HOT_GIVEUPS],
+                "cowait_serialised": out[COUNT_COWAIT_SERIALISED], "mg_demoted": out[COUNT_MG_DEMOTED]}
 
     def train_layout(self) -> int:
         """LAYOUT_CLASSIC / LAYOUT_LDS / LAYOUT_TOUCHED of the loaded shard."""

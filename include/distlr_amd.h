@@ -294,7 +294,9 @@ int dlr_summation_order(dlr_ctx *ctx);
  * returns without waiting.  lr/C are the server learning rate
  * (LEARNING_RATE, main.cc:27) and LR's C (lr.h:10). */
 int dlr_train_step(dlr_ctx *ctx, int64_t batch, float learning_rate, float C, int mode);
-/* All batches of one epoch in order (LR::Train, lr.cc:28-45). */
+/* All batches of one epoch in order (LR::Train, lr.cc:28-45); ends with
+ * dlr_sync, so DLR_OK means the epoch's kernels completed without a device
+ * error. */
 int dlr_train_epoch(dlr_ctx *ctx, float learning_rate, float C, int mode);
 
 /* Parameter-server topology without RCCL (several contexts on one GPU, or a
@@ -357,6 +359,33 @@ int dlr_kernel_time(dlr_ctx *ctx, int which, double *total_ms, int64_t *launches
 #define DLR_STAGE_UPDATE 2
 int dlr_stage_time(dlr_ctx *ctx, int stage, int64_t first_batch, int64_t count, float learning_rate, float C,
                    double *avg_ms);
+
+/* Event counts of the steps since the training shard was loaded (n <= 
+ * DLR_COUNTERS entries into out; syncs the context's streams first):
+ *   DLR_COUNT_HOT_CHAIN_LAUNCHES  k_hot_chain launches queued (C3's hot
+ *                                 columns: a few per step, each after the
+ *                                 margins of its last band);
+ *   DLR_COUNT_HOT_GIVEUPS         hot chains that stopped at a band flag not
+ *                                 up within 20 ms and left the band to the
+ *                                 next launch (same bits, but the step ran
+ *                                 serialised behind that wait; 0 in a
+ *                                 healthy run);
+ *   DLR_COUNT_COWAIT_SERIALISED   co-waiting launches (one-launch step, K6r,
+ *                                 hot chains) that another context's
+ *                                 co-waiting launch in this process was
+ *                                 queued ahead of on another stream, so the
+ *                                 launch was ordered after it;
+ *   DLR_COUNT_MG_DEMOTED          steps run with a separate pass-2 launch
+ *                                 because an earlier one-launch step of this
+ *                                 context ran out of its in-launch wait.
+ * The reference has no such counters: they report how this engine met
+ * lr.cc:122/131's "wait until the data is there". */
+#define DLR_COUNT_HOT_CHAIN_LAUNCHES 0
+#define DLR_COUNT_HOT_GIVEUPS 1
+#define DLR_COUNT_COWAIT_SERIALISED 2
+#define DLR_COUNT_MG_DEMOTED 3
+#define DLR_COUNTERS 4
+int dlr_stage_counters(dlr_ctx *ctx, int64_t *out, int n);
 
 /* Column-major layout the loaded training shard uses for the gradient
  * (chosen by dlr_load_train; DLR_GRAD_KERNEL=classic|lds|touched forces

@@ -338,9 +338,10 @@ def test_long_phase_order_bitwise(monkeypatch, piece):
 
 
 
-def _hot_stream_run(ds, D, steps, hot, stream, band_rows="8192"):
+def _hot_stream_run(ds, D, steps, hot, stream, band_rows="8192", counters=None, extra_env=None):
     import os as _os
     env = {"DLR_BAND_ROWS": band_rows, "DLR_BAND_HOT": hot, "DLR_HOT_STREAM": stream, "DLR_GRAD_KERNEL": "classic"}
+    env.update(extra_env or {})
     old = {k: _os.environ.get(k) for k in env}
     _os.environ.update(env)
     eng = dlr.Engine(D)
@@ -350,7 +351,10 @@ def _hot_stream_run(ds, D, steps, hot, stream, band_rows="8192"):
         nh = eng.train_hot_columns()
         for _ in range(steps):
             eng.train_step(0, 0.2, 1.0)
-        return eng.get_weights(), nh
+        w = eng.get_weights()
+        if counters is not None:
+            counters.update(eng.stage_counters())
+        return w, nh
     finally:
         eng.close()
         for k, v in old.items():
@@ -418,29 +422,70 @@ def test_hot_stream_valued_and_ragged_bands():
     assert_same_weights(got, w, "hot stream vs oracle (valued)")
 
 
-def test_hot_stream_serialised_kernels_resume(tmp_path):
-    # the hot chains' first launch needs the margins to run beside it (their
-    # flags); with every kernel serialised (AMD_SERIALIZE_KERNEL=3, as under
-    # counter collection) it gives up on band 0's flag and the resume launch
-    # -- queued after the last margin -- adds every band: the same bits
+def _chain_launches(nbands):
+    # k_hot_chain launches per step: one after the margins of bands 1, 2,
+    # 4, 8, ... and of the last band (DevHotChain)
+    n, end = 0, 1
+    for k in range(1, nbands + 1):
+        if k == end or k == nbands:
+            n += 1
+            end = 2 * k
+    return n
+
+
+def test_hot_stream_serialised_kernels_no_giveup(tmp_path):
+    # every chain launch is queued after the margins of its last band, so
+    # even with every kernel serialised (AMD_SERIALIZE_KERNEL=3, as under
+    # counter collection) no launch waits for a flag: zero give-ups, the
+    # same bits as the concurrent run
+    import json
     import subprocess
     import sys
     D = 1 << 24
     ds = _c3_shards(1, rows=80_000)[0]
-    got, nh = _hot_stream_run(ds, D, 2, "2000", "1")
+    cnt = {}
+    got, nh = _hot_stream_run(ds, D, 2, "2000", "1", counters=cnt)
     assert nh > 0
+    nbands = -(-80_000 // 8192)
+    assert cnt["hot_chain_launches"] == 2 * _chain_launches(nbands), cnt
+    assert cnt["hot_giveups"] == 0, cnt
     out = tmp_path / "w.npy"
+    cout = tmp_path / "c.json"
     code = (
-        "import sys, numpy as np\n"
+        "import sys, json, numpy as np\n"
         "sys.path.insert(0, %r); sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
         "import test_gpu_bands as t, distlr_amd as dlr\n"
         "ds = t._c3_shards(1, rows=80_000)[0]\n"
-        "w, nh = t._hot_stream_run(ds, 1 << 24, 2, '2000', '1')\n"
+        "cnt = {}\n"
+        "w, nh = t._hot_stream_run(ds, 1 << 24, 2, '2000', '1', counters=cnt)\n"
         "assert nh > 0\n"
         "np.save(%r, w)\n"
+        "json.dump(cnt, open(%r, 'w'))\n"
     ) % (os.path.dirname(os.path.abspath(__file__)), os.path.join(os.path.dirname(os.path.dirname(
         os.path.abspath(__file__))), "dist-lr_amd"), os.path.join(os.path.dirname(os.path.dirname(
-        os.path.abspath(__file__))), "oracle"), str(out))
+        os.path.abspath(__file__))), "oracle"), str(out), str(cout))
     env = dict(os.environ, AMD_SERIALIZE_KERNEL="3")
     subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=240)
-    assert_same_weights(np.load(out), got, "serialised kernels (resume launch) vs concurrent")
+    assert_same_weights(np.load(out), got, "serialised kernels vs concurrent")
+    scnt = json.load(open(cout))
+    assert scnt["hot_giveups"] == 0, scnt
+
+
+def test_hot_stream_with_collective_streams_no_giveup():
+    # the C3 shape's hot chains with the world > 1 stream
+    # set on one GPU -- RCCL (one rank: DLR_FORCE_COLLECTIVES=1) adds its
+    # streams and the exchange stream beside the engine's three -- zero
+    # give-ups and the oracle's bits
+    D = 1 << 24
+    ds = _c3_shards(1, rows=80_000)[0]
+    cnt = {}
+    got, nh = _hot_stream_run(ds, D, 3, "2000", "1", counters=cnt, extra_env={"DLR_FORCE_COLLECTIVES": "1"})
+    assert nh > 0
+    assert cnt["hot_giveups"] == 0, cnt
+    assert cnt["hot_chain_launches"] == 3 * _chain_launches(-(-80_000 // 8192)), cnt
+    (rp, col, val), lab = _csr_shard(ds)
+    w = dlr.init_weight(D)
+    for _ in range(3):
+        g = oracle.grad_csr((rp, col, val), lab, np.arange(80_000), w)
+        oracle.server_update(w, [g], 0.2)
+    assert_same_weights(got, w, "hot stream under collectives vs oracle")

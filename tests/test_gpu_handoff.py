@@ -84,18 +84,85 @@ def test_mg_withheld_block_raises_then_reload_recovers(B):
         assert "fused margin" in msg
         _expect_device_error(lambda: eng.get_weights())
         _expect_device_error(lambda: eng.train_step(1, 0.2, 1.0))  # sticky until the next load
-        # a reload clears it; without the fault the step is bitwise again
-        eng.set_fault(dlr.FAULT_NONE)
+        # a reload clears it (and the fault: dlr_set_fault lasts one shard);
+        # the context no longer trusts its one-launch step -- pass 2 runs in
+        # its own launch (kind 2) -- and the steps are bitwise
         eng.set_weights(w0)
         nb = eng.load_train(ds, B)
+        assert eng.train_product_margin() == 2
         w = w0.copy()
         for b in range(nb):
             eng.train_step(b, 0.2, 1.0)
             g = oracle.grad_csr((rp, col, val), lab, oracle.batch_rows(n, B, b), w)
             oracle.server_update(w, [g], 0.2)
         assert_same_weights(eng.get_weights(), w)
+        assert eng.stage_counters()["mg_demoted"] == nb
     finally:
         eng.close()
+    # a fresh context still takes the one-launch step
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(w0)
+        eng.load_train(ds, B)
+        assert eng.train_product_margin() == 3
+    finally:
+        eng.close()
+
+
+def test_two_engines_concurrent_c2_shape():
+    # two single-rank engines on GPU 0, stepping at once
+    # from two threads at the C2 shape (D = 2^20, B = 65,536: the one-launch
+    # step, one 1,024-thread workgroup per CU on every CU).  Each grid needs
+    # the whole device; the engine queues a co-waiting launch after the last
+    # one another stream queued (CowaitScope), so neither waits on CUs the
+    # other holds: both bitwise vs the oracle, no DLR_E_DEVICE.
+    import threading
+    D, B, nb, epochs = 1 << 20, 65_536, 3, 2
+    n = nb * B
+    shards = [dlr.Dataset.generate(n, D, 50, value_mode=1, seed=21 + k, stream=1) for k in range(2)]
+    w0 = dlr.init_weight(D)
+    engines = [dlr.Engine(D) for _ in range(2)]
+    out, errs = [None, None], []
+    start = threading.Barrier(2)
+
+    def run(k):
+        try:
+            eng = engines[k]
+            eng.set_weights(w0)
+            assert eng.load_train(shards[k], B) == nb
+            assert eng.train_product_margin() == 3
+            start.wait(timeout=600)
+            for _ in range(epochs):
+                for b in range(nb):
+                    eng.train_step(b, 0.2, 1.0)
+            eng.sync()
+            out[k] = (eng.get_weights(), eng.stage_counters())
+        except BaseException as e:  # noqa: BLE001 (reported below)
+            errs.append(e)
+            start.abort()
+
+    try:
+        ts = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=900)
+        assert not errs, errs
+        for k in range(2):
+            rp, col, val, lab = shards[k].csr()
+            w = w0.copy()
+            for _ in range(epochs):
+                for b in range(nb):
+                    g = oracle.grad_csr((rp, col, val), lab, oracle.batch_rows(n, B, b), w)
+                    oracle.server_update(w, [g], 0.2)
+            assert_same_weights(out[k][0], w)
+        # the second engine's first one-launch step at least was ordered
+        # behind the other's
+        assert out[0][1]["cowait_serialised"] + out[1][1]["cowait_serialised"] >= 1, (out[0][1], out[1][1])
+        assert out[0][1]["mg_demoted"] == 0 and out[1][1]["mg_demoted"] == 0
+    finally:
+        for eng in engines:
+            eng.close()
 
 
 def test_dense_ref_withheld_unit_raises():
