@@ -115,17 +115,6 @@ struct TrainShard {
     std::vector<int64_t> pmw_first;
     uint32_t *pm_cnt = nullptr;
     uint32_t pm_gen = 0;
-    // multi-step launches (dlr_train_steps; dlr_kernels.h DevMs): every
-    // batch's one-launch step fits, so up to kMsMaxSteps consecutive steps
-    // run as ONE launch.  ms_batch: the batches' views (device); pm_p is then
-    // the product ring (kMsMaxSteps slots of pm_pstride floats, slot 0 the
-    // single-step buffer); ms_resid the residual ring (kMsMaxSteps slots of
-    // ms_rstride floats); ms_cnt the steps' hand-off counters.
-    bool ms = false;
-    dlr::DevMsBatch *ms_batch = nullptr;
-    float *ms_resid = nullptr;
-    uint32_t *ms_cnt = nullptr;
-    int64_t pm_pstride = 0, ms_rstride = 0;
     int64_t pmS = 0;
     int pm_groups = 0, pm_split = 1;
     uint32_t *pm_lbeg = nullptr, *pm_list = nullptr, *pm_pofs = nullptr, *pm_rg = nullptr, *pm_qoff = nullptr;
@@ -579,8 +568,7 @@ void free_train(dlr_ctx *c) {
                     (void *)t.lpslot, (void *)t.lpws, (void *)t.lprow, (void *)t.lpval, (void *)t.pm_lbeg,
                     (void *)t.pm_list, (void *)t.pm_pofs, (void *)t.pm_rg, (void *)t.pm_qoff, (void *)t.pm_val,
                     (void *)t.pm_p, (void *)t.pm_qs, (void *)t.xslices, (void *)t.rt_gq, (void *)t.rt_val,
-                    (void *)t.rt_cend, (void *)t.dref_sync, (void *)t.pm_cnt, (void *)t.ms_batch, (void *)t.ms_resid,
-                    (void *)t.ms_cnt})
+                    (void *)t.rt_cend, (void *)t.dref_sync, (void *)t.pm_cnt})
         dev_free(c, p);
     t = TrainShard();
     c->pm_ready = -1;
@@ -2315,47 +2303,6 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
     return e;
 }
 
-// Multi-step launches (TrainShard::ms) for a one-rank shard whose every
-// batch takes the one-launch step (k_grad_lds MG) with B rows: the batches'
-// views, the product ring (pm_p grows to kMsMaxSteps slots), the residual
-// ring and the counters.  DLR_MULTI_STEP=0: off (every step its own launch).
-int setup_multi_step(dlr_ctx *c, int64_t resid_need) {
-    TrainShard &t = c->train;
-    t.ms = false;
-    const char *env = getenv("DLR_MULTI_STEP");
-    if ((env && strcmp(env, "0") == 0) || !t.pm_mg || t.rt || c->comm || t.gpu_pcsc || t.sparse_stream || !t.pcsc)
-        return DLR_OK;
-    const int64_t nb = (int64_t)t.plan.size();
-    const int fill = (int)(t.pR / 4096);
-    for (int64_t b = 0; b < nb; ++b)
-        if (t.plan[(size_t)b].rows != t.B || !dlr::grad_lds_ms_ok(pm_view(c, b), c->D, t.B, t.phases, fill))
-            return DLR_OK;
-    const int64_t rstride = (resid_need + 63) / 64 * 64;
-    const size_t ring_p = (size_t)t.pm_pstride * dlr::kMsMaxSteps * 4, ring_r = (size_t)rstride * dlr::kMsMaxSteps * 4;
-    const size_t cnt_b = (size_t)dlr::kMsCntWords * dlr::kMsMaxSteps * 4;
-    size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
-        (void)hipGetLastError();
-        return DLR_OK;
-    }
-    if (free_b < ring_p + ring_r + cnt_b + ((size_t)8 << 30)) return DLR_OK;  // (the residency headroom)
-    std::vector<dlr::DevMsBatch> hb((size_t)nb);
-    for (int64_t b = 0; b < nb; ++b) hb[(size_t)b] = dlr::DevMsBatch{pcsc_view(c, b), pm_view(c, b), batch_view(c, b)};
-    int rc;
-    float *ring = nullptr;
-    if ((rc = dev_alloc(c, (void **)&ring, ring_p))) return rc;
-    HIPC(c, hipMemcpyAsync(ring, t.pm_p, (size_t)t.pm_pstride * 4, hipMemcpyDeviceToDevice, c->stream));
-    dev_free(c, t.pm_p);
-    t.pm_p = ring;  // slot 0: the single-step buffer, as before
-    if ((rc = upload(c, &t.ms_batch, hb.data(), hb.size()))) return rc;
-    if ((rc = dev_alloc(c, (void **)&t.ms_resid, ring_r))) return rc;
-    HIPC(c, hipMemsetAsync(t.ms_resid, 0, ring_r, c->stream));
-    if ((rc = dev_alloc(c, (void **)&t.ms_cnt, cnt_b))) return rc;
-    t.ms_rstride = rstride;
-    t.ms = true;
-    return wait_stream(c, c->stream, "dlr_load_train");
-}
-
 // The product margin's arrays (DevPm, and the row-round gradient's DevRt
 // when allow_rt) for `spans` -- a shard's batches (their index is the
 // batch's), or the 65,536-row WINDOWS of band-mode batches (TrainShard::
@@ -2483,9 +2430,8 @@ int build_pm(dlr_ctx *c, const CsrView &src, const std::vector<dlr::BatchSpan> &
                 std::vector<uint16_t>().swap(q.cend);
             }
         }
-        t.pm_pstride = (pcap + 64 + 63) / 64 * 64;
-        if ((rc = dev_alloc(c, (void **)&t.pm_p, (size_t)t.pm_pstride * 4))) return rc;
-        HIPC(c, hipMemsetAsync(t.pm_p, 0, (size_t)t.pm_pstride * 4, c->stream));
+        if ((rc = dev_alloc(c, (void **)&t.pm_p, (size_t)(pcap + 64) * 4))) return rc;
+        HIPC(c, hipMemsetAsync(t.pm_p, 0, (size_t)(pcap + 64) * 4, c->stream));
         csc_bytes += (int64_t)(lbeg_n * 4 + t.pmo_list.back() * (t.unit ? 2 : 6) +
                                t.pmo_pofs.back() * 4 + t.pmo_rg.back() * 8 + t.pmo_qs.back() * 2 + pcap * 4);
         built = true;
@@ -3346,7 +3292,6 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         if (int rc_ = wait_stream(c, c->stream, __func__)) return rc_;
         c->resid_cap = resid_need;
     }
-    if ((rc = setup_multi_step(c, resid_need))) return rc;
     if (t.sparse_stream && (rc = coalesce_stream(c, nthreads))) return rc;
     // streamed: the slots (counted by place()); resident: the shard arrays
     if (!t.sparse_stream)
@@ -3660,48 +3605,13 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
     return DLR_OK;
 }
 
-int dlr_train_steps(dlr_ctx *c, int64_t first, int64_t count, float lr, float C, int mode) {
-    if (!c) return fail(c, DLR_E_ARG, "dlr_train_steps: null context");
-    if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_steps: no training shard loaded");
-    TrainShard &t = c->train;
-    const int64_t nb = (int64_t)t.plan.size();
-    if (first < 0 || first >= nb || count < 0) return fail(c, DLR_E_ARG, "dlr_train_steps: batch out of range");
-    if (mode < 0 || mode > 2) return fail(c, DLR_E_ARG, "dlr_train_steps: bad mode");
-    if (!t.ms || count < 2) {
-        for (int64_t k = 0; k < count; ++k)
-            if (int rc = dlr_train_step(c, (first + k) % nb, lr, C, mode)) return rc;
-        return DLR_OK;
-    }
-    if (int rc = check_device(c, "dlr_train_steps")) return rc;  // what earlier steps recorded
-    HIPC(c, hipSetDevice(c->device));
-    const int fill = (int)(t.pR / 4096);
-    while (count > 0) {
-        const int k = (int)std::min<int64_t>(count, dlr::kMsMaxSteps);
-        hipEvent_t t_step;
-        time_begin(c, &t_step);
-        // step 0's products: formed by the previous step when it guessed
-        // this batch, else pass 1 now (launch_margin)
-        if (c->pm_ready != first) HIPC(c, dlr::launch_pm_products(pm_view(c, first), c->w, c->D, t.pm_p, c->stream));
-        HIPC(c, hipMemsetAsync(t.ms_cnt, 0, (size_t)k * dlr::kMsCntWords * 4, c->stream));
-        const dlr::DevMs ms{t.ms_batch, nb, first, k, t.ms_resid, t.ms_rstride, t.pm_p, t.pm_pstride, t.ms_cnt,
-                            c->d_err, c->fault};
-        {
-            CowaitScope cw(c, c->stream);
-            HIPC(c, cw.begin());
-            HIPC(c, dlr::launch_grad_lds_ms(ms, c->D, t.B, c->w, lr, C, fill, c->stream));
-        }
-        time_end(c, 4, t_step);
-        c->pm_ready = (first + k) % nb;  // the last step formed it, in slot 0
-        first = (first + k) % nb;
-        count -= k;
-    }
-    return DLR_OK;
-}
-
 int dlr_train_epoch(dlr_ctx *c, float lr, float C, int mode) {
     if (!c) return DLR_E_ARG;
     if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_epoch: no training shard loaded");
-    if (int rc = dlr_train_steps(c, 0, (int64_t)c->train.plan.size(), lr, C, mode)) return rc;
+    for (int64_t b = 0; b < (int64_t)c->train.plan.size(); ++b) {
+        int rc = dlr_train_step(c, b, lr, C, mode);
+        if (rc) return rc;
+    }
     // the epoch's success is definitive: its last step's in-launch waits
     // are known to have completed
     return dlr_sync(c);
@@ -3924,12 +3834,6 @@ int dlr_train_unit_values(dlr_ctx *c) {
     if (!c) return DLR_E_ARG;
     if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_unit_values: no training shard loaded");
     return c->train.unit ? 1 : 0;
-}
-
-int dlr_train_multi_step(dlr_ctx *c) {
-    if (!c) return DLR_E_ARG;
-    if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_multi_step: no training shard loaded");
-    return c->train.ms ? 1 : 0;
 }
 
 int dlr_train_product_margin(dlr_ctx *c) {

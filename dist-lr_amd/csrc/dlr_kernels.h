@@ -377,40 +377,6 @@ hipError_t launch_pm_margin(const DevPm &pm, const DevBatch &bt, const float *p,
 bool grad_lds_mg_ok(const DevPm &cur, int64_t D, int64_t B, int phases, int fill);
 hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const float *resid, float *w, float lr,
                               float C, const DevPm &next, float *p, hipStream_t s, const DevP2 *mg = nullptr);
-// MULTI-STEP one-launch steps (k_grad_lds_ms): `steps` consecutive batches
-// first, first + 1, ... (mod nb) in ONE launch, each the one-launch step
-// above, the launch boundary between steps replaced by an in-launch
-// hand-off of pass 1 (dlr_kernels.hip).  batch[b]: batch b's views (all
-// batches of B rows, one phase form).  Rings: step st's residuals at resid +
-// st * resid_stride; its products (the previous step's pass 1, or those
-// formed before the launch for st = 0) at prod + st * prod_stride, and its
-// pass 1 writes slot st + 1 -- the last step slot 0, where the next launch
-// starts.  cnt: steps x kMsCntWords words, ZERO when the launch starts.
-struct DevMsBatch {
-    DevPcsc pc;
-    DevPm pm;
-    DevBatch bt;
-};
-constexpr int kMsMaxSteps = 32;                        // steps per launch (ring slots)
-constexpr int64_t kMsP1Off = 64 * 8 * 32;              // a step's pass-1 sub-counters, after its phase counters
-constexpr int64_t kMsCntWords = kMsP1Off + 8 * 32;     // counter words per step
-struct DevMs {
-    const DevMsBatch *batch;
-    int64_t nb, first;
-    int steps;
-    float *resid;
-    int64_t resid_stride;
-    float *prod;
-    int64_t prod_stride;
-    uint32_t *cnt;
-    uint32_t *err;
-    int fault;
-};
-// Whether a shard's batches may run as multi-step launches (each batch's
-// one-launch step fits: grad_lds_mg_ok; and the multi-step grid is resident).
-bool grad_lds_ms_ok(const DevPm &cur, int64_t D, int64_t B, int phases, int fill);
-hipError_t launch_grad_lds_ms(const DevMs &ms, int64_t D, int64_t B, float *w, float lr, float C, int fill,
-                              hipStream_t s);
 // The row-round gradient (DevRt): the update (fused) or the pushed gradient
 // (gout); next != null (fused only): also the next batch's products, as
 // launch_grad_lds_pm.  resid must hold rounds * kRtRows floats.

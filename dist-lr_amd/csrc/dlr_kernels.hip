@@ -1265,18 +1265,13 @@ __global__ __launch_bounds__(256) void k_pm_margin(DevPm pm, DevBatch bt, const 
 // phase computes (the two-phase form waits for its second 128 KB fill with
 // nothing to do: profiles/r05_stamps_c2_pollskip.txt, 14.5 -> 18.2 us).
 // The same blocks, the same column order: bitwise the two-phase form.
-// MS (multi-step, k_grad_lds_ms): one step of a persistent launch -- pass 2
-// reads the products from pm_in (pm_p takes the next batch's), the bank of
-// p2.cnt is the step's own (zeroed before the launch: no bank is cleared
-// here), and the workgroup's weights come from wk when wk_ok (the previous
-// step's update, kept in registers) and go back to it.
-template <int FILL, bool FUSED, bool NTW, bool PM = false, bool MG = false, bool DB = false, bool MS = false>
-__device__ __forceinline__ void grad_lds_step(const DevPcsc &pc, int64_t D, int64_t B, const float *__restrict__ resid,
-                                              float *__restrict__ w, float *__restrict__ gout, float Bf, double Bd,
-                                              float lr, float C, const DevPm &pn, float *__restrict__ pm_p,
-                                              const DevP2 &p2, const float *__restrict__ pm_in, float (&wk)[kGradNG],
-                                              bool wk_ok, Spin *outer = nullptr) {
-    static_assert(!MS || MG, "a multi-step launch runs every step's pass 2 itself");
+template <int FILL, bool FUSED, bool NTW, bool PM = false, bool MG = false, bool DB = false>
+__global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int64_t D, int64_t B,
+                                                                const float *__restrict__ resid,
+                                                                float *__restrict__ w, float *__restrict__ gout,
+                                                                float Bf, double Bd, float lr, float C,
+                                                                DevPm pn = DevPm{}, float *__restrict__ pm_p = nullptr,
+                                                                DevP2 p2 = DevP2{}) {
     constexpr int R = FILL * 4096;      // rows per phase
     constexpr int NB = DB ? 2 : 1;      // residual buffers
     constexpr int NPH = DB ? 4 : 2;     // phases
@@ -1297,11 +1292,11 @@ __device__ __forceinline__ void grad_lds_step(const DevPcsc &pc, int64_t D, int6
     static_assert(!MG || (PM && FUSED), "the fused margin comes with the fused pass 1");
     if constexpr (MG) {
         DLR_STAMP(11);
-        if (!MS && blockIdx.x == 0 && wv < 8)  // the next launch's bank: 64 phases x 8 sub-counters
+        if (blockIdx.x == 0 && wv < 8)  // the next launch's bank: 64 phases x 8 sub-counters
             p2.cnt[(((p2.gen + 1) & 1) * 64 + lane) * kMgSub * 32 + wv * 32] = 0u;
         const int64_t k2 = blockIdx.x + (int64_t)gridDim.x * wv;  // wv < NB * FILL (launch_grad_lds_pm)
         if (k2 < p2.pm.nblk) {  // wave-uniform
-            pm_rowsum<8, true>(p2.pm, p2.bt, MS ? pm_in : pm_p, p2.resid, k2, smem + wv * kPmCap, lane);
+            pm_rowsum<8, true>(p2.pm, p2.bt, pm_p, p2.resid, k2, smem + wv * kPmCap, lane);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every residual of the block stored
             // sub-counter k2 % 8 of the phase (each on a line of its own:
             // the adds and the polls spread over 8 lines)
@@ -1327,10 +1322,7 @@ __device__ __forceinline__ void grad_lds_step(const DevPcsc &pc, int64_t D, int6
     // complete when phase p is, and their own polls -- round trips queued
     // behind the windows, fills and pass-1 list loads -- are skipped
     // (mg_done: the phases known complete).
-    // (MS: the launch's own, so that a wait that ran out in one step ends
-    // the waits of the later steps at once)
-    Spin spin_own(MG ? p2.err : nullptr, kErrMgPublish);
-    Spin &spin = outer ? *outer : spin_own;
+    Spin spin(MG ? p2.err : nullptr, kErrMgPublish);
     int mg_done = 0;
     auto mg_wait = [&](int p) {
         if constexpr (MG) {
@@ -1400,7 +1392,7 @@ __device__ __forceinline__ void grad_lds_step(const DevPcsc &pc, int64_t D, int6
 #pragma unroll
         for (int q = 0; q <= NPH; ++q) sb[gi][q] = __builtin_amdgcn_readfirstlane(sb[gi][q]);
         const int64_t j = (gfirst + kGradWaves * gi) * 64 + lane;
-        wj[gi] = (DLR_ABL & 8) ? 0.0f : (MS && wk_ok) ? wk[gi] : w[j < D ? j : D - 1];
+        wj[gi] = (DLR_ABL & 8) ? 0.0f : w[j < D ? j : D - 1];
         acc[gi] = 0.0f;
     }
     auto bs_of = [&](int gi, int p) { return sb[gi][p]; };
@@ -1788,7 +1780,6 @@ __device__ __forceinline__ void grad_lds_step(const DevPcsc &pc, int64_t D, int6
                     w[j] = wn;
                 }
                 if (PM) smem[(wv + kGradWaves * gi) * 64 + lane] = wn;  // column j - kPmSlice*blockIdx.x
-                if (MS) wk[gi] = wn;
             } else {
                 gout[j] = g;
             }
@@ -1809,84 +1800,6 @@ __device__ __forceinline__ void grad_lds_step(const DevPcsc &pc, int64_t D, int6
     __syncthreads();
     DLR_STAMP(7);
 #endif
-}
-
-template <int FILL, bool FUSED, bool NTW, bool PM = false, bool MG = false, bool DB = false>
-__global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int64_t D, int64_t B,
-                                                                const float *__restrict__ resid,
-                                                                float *__restrict__ w, float *__restrict__ gout,
-                                                                float Bf, double Bd, float lr, float C,
-                                                                DevPm pn = DevPm{}, float *__restrict__ pm_p = nullptr,
-                                                                DevP2 p2 = DevP2{}) {
-    float wk[kGradNG];
-    grad_lds_step<FILL, FUSED, NTW, PM, MG, DB>(pc, D, B, resid, w, gout, Bf, Bd, lr, C, pn, pm_p, p2, nullptr, wk,
-                                                false);
-}
-
-// MULTI-STEP one-launch steps (dlr_kernels.h DevMs; LR::Train's epoch loop,
-// lr.cc:29-44, as ONE launch per up to kMsMaxSteps batches): step st is the
-// one-launch step of batch first + st (k_grad_lds MG: pass 2, gradient,
-// update, the next batch's pass 1), and the launch boundary between steps
-// is replaced by an in-launch hand-off -- the next step's pass 2 reads
-// products that every slice's pass 1 formed, so each workgroup publishes
-// its pass 1 (its stores written back out of its XCD's L2: an agent-scope
-// release fence, then one add to step st's pass-1 count, sub-counter per
-// XCD) and waits, before step st + 1, until all S slices have.  What the
-// launch boundary also gave -- no CU holding a stale line of data another
-// XCD rewrote -- comes from the rings: step st's residuals and the products
-// it reads are lines no CU read earlier in the launch (resid ring slot st,
-// product ring slot st; the last step writes slot 0 for the next launch,
-// whose start drops every cached line).  A workgroup's weights stay in
-// registers from step to step (the columns it updates are its own).  The
-// same steps in the same order: bitwise the one-launch step per batch.
-template <int FILL>
-__global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds_ms(DevMs ms, int64_t D, int64_t B,
-                                                                   float *__restrict__ w, float Bf, double Bd, float lr,
-                                                                   float C) {
-    float wk[kGradNG] = {};
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    Spin spin(ms.err, kErrMgPublish);
-    int64_t b = ms.first;  // (batch first + st mod nb, stepped: no integer division here)
-    for (int st = 0; st < ms.steps; ++st, b = b + 1 == ms.nb ? 0 : b + 1) {
-        const int64_t nx = b + 1 == ms.nb ? 0 : b + 1;
-        const DevMsBatch cur = ms.batch[b];
-        const DevPm pn = ms.batch[nx].pm;
-        uint32_t *cnt = ms.cnt + (int64_t)st * kMsCntWords;
-        const DevP2 p2{cur.pm, cur.bt, ms.resid + (int64_t)st * ms.resid_stride, cnt, 0u, ms.err, ms.fault};
-        const float *pin = ms.prod + (int64_t)st * ms.prod_stride;
-        float *pout = ms.prod + (int64_t)(st + 1 < ms.steps ? st + 1 : 0) * ms.prod_stride;
-        if (st > 0) {
-            // every slice's pass 1 of step st - 1 is published (wave 0
-            // polls the 8 sub-counters of that step; bounded)
-            if (wv == 0) {
-                const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
-                    ms.cnt + (int64_t)(st - 1) * kMsCntWords + kMsP1Off, 0, 0x7FFFFFFF, 0x00020000);
-                const uint32_t want = (uint32_t)pn.S;
-                for (int k = 0; spin.more(k); ++k) {
-                    const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(crs, (int)((lane & 7) * 32 * 4), 0, 16);
-                    uint32_t n = 0;
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) n += __builtin_amdgcn_readlane(v, i);
-                    if (n >= want) break;
-                    __builtin_amdgcn_s_sleep(DLR_MG_SLEEP);
-                }
-            }
-            lds_barrier();
-        }
-        grad_lds_step<FILL, true, false, true, true, false, true>(cur.pc, D, B, nullptr, w, nullptr, Bf, Bd, lr, C,
-                                                                  pn, pout, p2, pin, wk, st > 0, &spin);
-        // publish this workgroup's pass 1: its product stores complete
-        // (every wave), written back out of the XCD's L2 (release), counted
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (blockIdx.x < pn.S && threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            __hip_atomic_fetch_add(cnt + kMsP1Off + (blockIdx.x & 7) * 32, 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    (void)lane;
 }
 
 // ---------------------------------------------------------------------------
@@ -4774,58 +4687,6 @@ hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const flo
             return hipErrorInvalidValue;
     }
 #undef DLR_GLP
-    return hipGetLastError();
-}
-
-namespace {
-const void *grad_lds_ms_fn(int fill) {
-    switch (fill) {
-        case 1: return reinterpret_cast<const void *>(&k_grad_lds_ms<1>);
-        case 2: return reinterpret_cast<const void *>(&k_grad_lds_ms<2>);
-        case 4: return reinterpret_cast<const void *>(&k_grad_lds_ms<4>);
-        case 8: return reinterpret_cast<const void *>(&k_grad_lds_ms<8>);
-        default: return nullptr;
-    }
-}
-}  // namespace
-
-// Multi-step launches: the one-launch step's shape (grad_lds_mg_ok), the
-// two-phase form (the DB form has no multi-step instance), and the
-// multi-step kernel's own grid resident at once.
-bool grad_lds_ms_ok(const DevPm &cur, int64_t D, int64_t B, int phases, int fill) {
-    if (!grad_lds_mg_ok(cur, D, B, phases, fill)) return false;
-    DevPcsc form{};
-    form.phases = phases;
-    form.fill = fill;
-    if (grad_lds_db(form)) return false;
-    static int cap[64][9] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || fill < 1 || fill > 8) return false;
-    int &c = cap[dev][fill];
-    if (c == 0) c = resident_grid(grad_lds_ms_fn(fill), kGradWaves * kWave, grad_lds_pm_lds(fill, false));
-    const int64_t grid = (D + kPmSlice - 1) / kPmSlice;
-    return c > 0 && grad_lds_mg_grid(cur.nblk, grid) <= c;
-}
-
-hipError_t launch_grad_lds_ms(const DevMs &ms, int64_t D, int64_t B, float *w, float lr, float C, int fill,
-                              hipStream_t s) {
-    if (D <= 0 || ms.steps < 1) return hipSuccess;
-    if (ms.steps > kMsMaxSteps || !ms.batch || !ms.cnt || !ms.resid || !ms.prod || ms.nb < 1) return hipErrorInvalidValue;
-    const int64_t grid = (D + kPmSlice - 1) / kPmSlice;
-    // (the caller checked grad_lds_ms_ok for every batch of the shard: the
-    // first batch's block count sets the evened grid as in the one-step form)
-    const unsigned mgrid = (unsigned)grad_lds_mg_grid((B + kPmRows - 1) / kPmRows, grid);
-    const dim3 blk(kGradWaves * kWave);
-    const size_t lds = grad_lds_pm_lds(fill, false);
-    const float Bf = (float)B;
-    const double Bd = (double)B;
-    switch (fill) {
-        case 1: hipLaunchKernelGGL(k_grad_lds_ms<1>, dim3(mgrid), blk, lds, s, ms, D, B, w, Bf, Bd, lr, C); break;
-        case 2: hipLaunchKernelGGL(k_grad_lds_ms<2>, dim3(mgrid), blk, lds, s, ms, D, B, w, Bf, Bd, lr, C); break;
-        case 4: hipLaunchKernelGGL(k_grad_lds_ms<4>, dim3(mgrid), blk, lds, s, ms, D, B, w, Bf, Bd, lr, C); break;
-        case 8: hipLaunchKernelGGL(k_grad_lds_ms<8>, dim3(mgrid), blk, lds, s, ms, D, B, w, Bf, Bd, lr, C); break;
-        default: return hipErrorInvalidValue;
-    }
     return hipGetLastError();
 }
 

@@ -51,7 +51,7 @@ SYMBOLS = [
     "dlr_set_weights", "dlr_get_weights", "dlr_load_train", "dlr_load_test", "dlr_load_train_dense",
     "dlr_load_test_dense", "dlr_set_residency", "dlr_train_residency", "dlr_set_summation_order",
     "dlr_summation_order",
-    "dlr_train_step", "dlr_train_steps", "dlr_train_multi_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
+    "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
     "dlr_set_fault",
     "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_stage_counters", "dlr_train_layout", "dlr_train_band_rows", "dlr_train_relabeled", "dlr_train_unit_values", "dlr_train_product_margin", "dlr_train_hot_columns", "dlr_train_row_rounds",
     "dlr_set_exchange_overlap", "dlr_exchange_overlap", "dlr_set_exchange_pieces", "dlr_exchange_pieces",
@@ -158,8 +158,6 @@ _sig("dlr_get_weights", C.c_int, P, P, i64)
 _sig("dlr_load_train", C.c_int, P, P, i64, C.POINTER(i64))
 _sig("dlr_load_test", C.c_int, P, P)
 _sig("dlr_train_step", C.c_int, P, i64, C.c_float, C.c_float, C.c_int)
-_sig("dlr_train_steps", C.c_int, P, i64, i64, C.c_float, C.c_float, C.c_int)
-_sig("dlr_train_multi_step", C.c_int, P)
 _sig("dlr_train_epoch", C.c_int, P, C.c_float, C.c_float, C.c_int)
 _sig("dlr_worker_gradient", C.c_int, P, i64, C.c_float, P, i64)
 _sig("dlr_server_apply", C.c_int, P, P, C.c_int, i64, C.c_float, C.c_int)
@@ -541,16 +539,6 @@ class Engine:
 
     def train_step(self, batch: int, lr: float, C_: float = 1.0, mode: int = MODE_SYNC_MEAN) -> None:
         self._c(lib.dlr_train_step(self._h, batch, lr, C_, mode))
-
-    def train_steps(self, first: int, count: int, lr: float, C_: float = 1.0, mode: int = MODE_SYNC_MEAN) -> None:
-        """`count` consecutive steps from batch `first` (mod the epoch):
-        multi-step launches where the shard allows (dlr_train_steps)."""
-        self._c(lib.dlr_train_steps(self._h, first, count, lr, C_, mode))
-
-    def train_multi_step(self) -> bool:
-        rc = lib.dlr_train_multi_step(self._h)
-        self._c(min(rc, 0))
-        return rc == 1
 
     def train_epoch(self, lr: float, C_: float = 1.0, mode: int = MODE_SYNC_MEAN) -> None:
         self._c(lib.dlr_train_epoch(self._h, lr, C_, mode))

@@ -294,19 +294,7 @@ int dlr_summation_order(dlr_ctx *ctx);
  * returns without waiting.  lr/C are the server learning rate
  * (LEARNING_RATE, main.cc:27) and LR's C (lr.h:10). */
 int dlr_train_step(dlr_ctx *ctx, int64_t batch, float learning_rate, float C, int mode);
-/* `count` consecutive steps on batches first, first + 1, ... (mod the
- * epoch) -- exactly `count` dlr_train_step calls, the same bits.  One-rank
- * shards whose every batch takes the one-launch step (dlr_train_product_
- * margin = 3; dlr_train_multi_step = 1, e.g. BASELINE C2) run up to 32
- * steps as ONE launch (k_grad_lds_ms: the launch boundary between steps
- * becomes an in-launch hand-off); others loop over dlr_train_step.  Like
- * dlr_train_step, returns before the kernels finish (dlr_sync). */
-int dlr_train_steps(dlr_ctx *ctx, int64_t first_batch, int64_t count, float learning_rate, float C, int mode);
-/* 1 when dlr_train_steps runs multi-step launches for the loaded shard
- * (DLR_MULTI_STEP=0 at load: never), else 0; < 0 on error. */
-int dlr_train_multi_step(dlr_ctx *ctx);
-/* All batches of one epoch in order (LR::Train, lr.cc:28-45, through
- * dlr_train_steps); ends with
+/* All batches of one epoch in order (LR::Train, lr.cc:28-45); ends with
  * dlr_sync, so DLR_OK means the epoch's kernels completed without a device
  * error. */
 int dlr_train_epoch(dlr_ctx *ctx, float learning_rate, float C, int mode);
