@@ -291,6 +291,10 @@ struct dlr_ctx {
     uint32_t *d_stat = nullptr;
     int64_t hcount[DLR_COUNTERS] = {};
     int fault = dlr::kFaultNone;  // dlr_set_fault (tests; cleared by every load)
+    // the loads' tuning (dlr_tuning): set by dlr_set_tuning, else taken from
+    // the environment at each load (load_tuning)
+    dlr_tuning tune{};
+    bool tune_set = false;
     // an in-launch wait of this context's one-launch step (kErrMgPublish) or
     // K6r (kErrRef*) ran out: the device did not hold the whole grid (another
     // process's work, CowaitScope) -- later loads use the separate launches
@@ -492,6 +496,14 @@ void cowait_forget(dlr_ctx *c) {
     hipStream_t &l = o.last[c->device];
     if (l && (l == c->stream || l == c->hstream || l == c->gstream)) l = nullptr;
 }
+
+// The tuning a load uses (dlr_tuning): the context's own, or the
+// environment's at this load.
+void load_tuning(dlr_ctx *c) {
+    if (!c->tune_set) dlr_tuning_from_env(&c->tune);
+}
+// a tuning field: its value, or `def` when DLR_AUTO
+inline int64_t tv(int64_t v, int64_t def) { return v == DLR_AUTO ? def : v; }
 
 int dev_alloc(dlr_ctx *c, void **p, size_t bytes) {
     *p = nullptr;
@@ -779,8 +791,7 @@ inline int64_t pid(const std::vector<int32_t> &p, int64_t j) { return p.empty() 
 // pure renaming: every sum keeps its order, results are bitwise unchanged.
 int column_order(dlr_ctx *c, const dlr_dataset &ds, std::vector<int32_t> &np) {
     np.clear();
-    const char *rl = getenv("DLR_RELABEL");
-    const int mode = rl ? atoi(rl) : -1;  // -1 auto, 0 off, 1 on
+    const int64_t mode = c->tune.relabel;  // DLR_AUTO, 0 off, 1 on
     const int64_t D = c->D;
     int64_t want = (mode == 1 || (mode < 0 && D >= 65536)) && D <= ((int64_t)1 << 25) ? 1 : 0;
     int rc;
@@ -821,12 +832,10 @@ int column_order(dlr_ctx *c, const dlr_dataset &ds, std::vector<int32_t> &np) {
     // miss L2 in the margin's gathers whatever their order among equals; in
     // order of FIRST OCCURRENCE (row-major, this rank's shard) instead of id,
     // the rare columns that rows close together introduce sit on the same
-    // cache lines (DLR_RELABEL_TAIL=0: by id).
-    const char *rt = getenv("DLR_RELABEL_TAIL");
-    const int tail_mode = rt ? atoi(rt) : 2;  // 0 by id, 1 by first occurrence among equal counts, 2 by it alone
+    // cache lines (relabel_tail 0: by id).
+    const int64_t tail_mode = tv(c->tune.relabel_tail, 2);  // 0 by id, 1 by first occurrence among equal counts, 2 by it alone
     if (tail_mode > 0) {
-        const char *rr = getenv("DLR_RELABEL_RARE");
-        const int64_t kRare = rr ? atoll(rr) : 16;
+        const int64_t kRare = tv(c->tune.relabel_rare, 16);
         // -first, reduced by max over the ranks: every rank numbers alike
         std::vector<int64_t> first((size_t)D, -INT64_MAX);
         const int64_t nnz = (int64_t)ds.col.size();
@@ -1157,18 +1166,14 @@ constexpr uint32_t kHsGiveUpTicks = 2000000;  // 20 ms at 100 MHz
 // rows of a window of the band-mode product margin (TrainShard::pmw): the
 // product margin's 1,024 blocks of 64 rows
 constexpr int64_t kPmWinRows = (int64_t)dlr::kPmMaxBlocks * dlr::kPmRows;
-static int64_t hs_max_cols() {
-    const char *e = getenv("DLR_HOT_STREAM_MAX");
-    return e ? std::max<int64_t>(1, atoll(e)) : 64;
-}
+static int64_t hs_max_cols(const dlr_ctx *c) { return std::max<int64_t>(1, tv(c->tune.hot_stream_max, 64)); }
 
-bool hot_stream_wanted() {
-    const char *e = getenv("DLR_HOT_STREAM");
-    return !(e && strcmp(e, "0") == 0);
-}
+bool hot_stream_wanted(const dlr_ctx *c) { return tv(c->tune.hot_stream, 1) != 0; }
 // The smallest threshold >= hot_min that leaves at most hs_max_cols() hot
 // columns in every batch (dlr::hot_chain_grid: kHcCols chains per CU).
-int64_t hot_stream_threshold(const std::vector<uint32_t> &cptr, int64_t nb, int64_t D, int64_t hot_min) {
+int64_t hot_stream_threshold(const dlr_ctx *c, const std::vector<uint32_t> &cptr, int64_t nb, int64_t D,
+                             int64_t hot_min) {
+    const int64_t maxc = hs_max_cols(c);
     int64_t thr = hot_min;
     for (int64_t b = 0; b < nb; ++b) {
         const uint32_t *cp = cptr.data() + (size_t)b * (size_t)(D + 1);
@@ -1177,9 +1182,9 @@ int64_t hot_stream_threshold(const std::vector<uint32_t> &cptr, int64_t nb, int6
             const int64_t n = (int64_t)(cp[j + 1] & 0x7FFFFFFFu) - (int64_t)(cp[j] & 0x7FFFFFFFu);
             if (n >= hot_min) big.push_back(n);
         }
-        if ((int64_t)big.size() > hs_max_cols()) {
-            std::nth_element(big.begin(), big.begin() + hs_max_cols(), big.end(), std::greater<int64_t>());
-            thr = std::max(thr, big[(size_t)hs_max_cols()] + 1);  // the (hs_max_cols()+1)-th largest is not hot
+        if ((int64_t)big.size() > maxc) {
+            std::nth_element(big.begin(), big.begin() + maxc, big.end(), std::greater<int64_t>());
+            thr = std::max(thr, big[(size_t)maxc] + 1);  // the (maxc + 1)-th largest is not hot
         }
     }
     return thr;
@@ -1188,7 +1193,7 @@ template <typename RowT>
 int build_hot_stream(dlr_ctx *c, const std::vector<uint32_t> &cptr, const std::vector<RowT> &crow,
                      const std::vector<float> &cval, int64_t hot_min, int shift) {
     TrainShard &t = c->train;
-    if (!hot_stream_wanted()) return DLR_OK;
+    if (!hot_stream_wanted(c)) return DLR_OK;
     const int64_t nb = (int64_t)t.plan.size(), D = c->D;
     std::vector<std::vector<uint32_t>> hot((size_t)nb);
     int64_t any = 0;
@@ -1197,7 +1202,7 @@ int build_hot_stream(dlr_ctx *c, const std::vector<uint32_t> &cptr, const std::v
         for (int64_t j = 0; j < D; ++j)
             if ((int64_t)(cp[j + 1] & 0x7FFFFFFFu) - (int64_t)(cp[j] & 0x7FFFFFFFu) >= hot_min && !(cp[j] & 0x80000000u))
                 hot[(size_t)b].push_back((uint32_t)j);
-        if ((int64_t)hot[(size_t)b].size() > hs_max_cols()) return DLR_OK;
+        if ((int64_t)hot[(size_t)b].size() > hs_max_cols(c)) return DLR_OK;
         any += (int64_t)hot[(size_t)b].size();
     }
     if (any == 0) return DLR_OK;
@@ -1302,9 +1307,8 @@ int build_hot_stream(dlr_ctx *c, const std::vector<uint32_t> &cptr, const std::v
 // pieces then start 63 floats apart in its LDS product slab, one bank
 // apart, where 64-entry pieces put every summing lane on the same bank --
 // C3 long phases 427 -> 333 us; tools/lp_ab.sh sweeps 31..127)
-int64_t long_piece() {
-    const char *e = getenv("DLR_LONG_PIECE");
-    const int64_t v = e ? atoll(e) : 63;
+int64_t long_piece(const dlr_tuning &tu) {
+    const int64_t v = tv(tu.long_piece, 63);
     return v >= 1 && v <= 1024 ? v : 63;
 }
 struct LPhaseBuild {
@@ -1316,9 +1320,9 @@ struct LPhaseBuild {
 };
 
 template <typename RowT>
-void build_long_phases(const std::vector<LongBatch<RowT>> &lb, int64_t B, bool unit, LPhaseBuild &out) {
+void build_long_phases(const std::vector<LongBatch<RowT>> &lb, int64_t B, bool unit, int64_t kPiece,
+                       LPhaseBuild &out) {
     const int64_t nph = (B + dlr::kLPhase - 1) / dlr::kLPhase;
-    const int64_t kPiece = long_piece();
     for (const LongBatch<RowT> &L : lb) {
         const int64_t nl = (int64_t)L.cols.size();
         std::vector<int64_t> cnt((size_t)(nph * nl), 0);  // [p][l]
@@ -1414,8 +1418,7 @@ void for_batches(int64_t nb, int nthreads, Fn fn) {
 // per-array host copies and device slots by two batch-sized slots.
 int coalesce_stream(dlr_ctx *c, int nthreads) {
     TrainShard &t = c->train;
-    const char *ev = getenv("DLR_STREAM_COALESCE");  // "0": one copy per array and batch (A/B; read per load)
-    if (ev && strcmp(ev, "0") == 0) return DLR_OK;
+    if (tv(c->tune.stream_coalesce, 1) == 0) return DLR_OK;  // one copy per array and batch
     const size_t nb = t.plan.size(), na = t.sarr.size();
     t.soff.assign(nb * na, 0);
     t.sbsz.assign(nb, 0);
@@ -1801,9 +1804,8 @@ void touched_batch(const CsrView &ds, const dlr::BatchSpan &sp, TouchedBatch &tb
 // a9a and Criteo-style hashed fields): fl32(t * 1.0f) == t, so the UNIT
 // kernels that never read values give the same bits.  DLR_UNIT_VALUES=0
 // keeps the value arrays (A/B and tests).
-bool unit_values(const std::vector<float> &val) {
-    const char *env = getenv("DLR_UNIT_VALUES");  // read at every load (tests switch it)
-    if ((env && strcmp(env, "0") == 0) || val.empty()) return false;
+bool unit_values(const dlr_ctx *c, const std::vector<float> &val) {
+    if (tv(c->tune.unit_values, 1) == 0 || val.empty()) return false;
     const size_t n = val.size();
     const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)dlr::default_threads(), n >> 20));
     std::atomic<bool> all{true};
@@ -2187,8 +2189,7 @@ hipError_t launch_gradient(dlr_ctx *c, int64_t b, int64_t B, float *gout, float 
 // rows one to one (the caller then runs margin and gradient in sequence).
 bool band_pipeline_ok(const dlr_ctx *c, int64_t b) {
     const TrainShard &t = c->train;
-    const char *pe = getenv("DLR_BAND_PIPE");  // "0": margin, then the gradient (A/B)
-    if ((pe && strcmp(pe, "0") == 0) || !t.band_shift || t.touched || t.dense || t.pcsc || t.sparse_stream) return false;
+    if (tv(c->tune.band_pipeline, 1) == 0 || !t.band_shift || t.touched || t.dense || t.pcsc || t.sparse_stream) return false;
     const int64_t rows = t.plan[(size_t)b].rows, BR = (int64_t)1 << t.band_shift;
     return t.bfirst[(size_t)b + 1] - t.bfirst[(size_t)b] == (rows + BR - 1) / BR;
 }
@@ -2210,15 +2211,10 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
     // band publishes them), or k_band_hot per band
     const bool hs = hot && t.hs;
     const int64_t nh = hs ? t.hs_nh[bb] : 0;
-    // with hot chains beside it, the persistent margin leaves their CUs (and
-    // DLR_BAND_CUS more to the other columns' band kernel, whose workgroups
-    // cannot share a CU with the margin's: A/B, measured no better at 32,
-    // 64, 96)
-    static const int band_cus = [] {
-        const char *e = getenv("DLR_BAND_CUS");
-        return e ? atoi(e) : 0;
-    }();
-    const int margin_reserve = hs ? dlr::hot_chain_grid(nh) + band_cus : hot ? (int)t.max_hot + band_cus : 0;
+    // with hot chains beside it, the persistent margin leaves their CUs
+    // (leaving 32-96 more to the other columns' band kernel measured no
+    // better)
+    const int margin_reserve = hs ? dlr::hot_chain_grid(nh) : hot ? (int)t.max_hot : 0;
     if (hot && !c->hstream) {
         e = hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_hdone, hipEventDisableTiming);
@@ -2320,14 +2316,14 @@ int build_pm(dlr_ctx *c, const CsrView &src, const std::vector<dlr::BatchSpan> &
     std::atomic<bool> ok{true};
     // the row-round gradient: by default for batches of <= 2 rounds
     // (C2 at B = 8,192: 7.5 vs 10.0 us for k_grad_lds); at 8 rounds
-    // (B = 65,536) k_grad_lds is faster.  DLR_GRAD_RT=1
-    // takes it for every batch that fits, =0 never.
-    const char *rte = getenv("DLR_GRAD_RT");
+    // (B = 65,536) k_grad_lds is faster.  row_rounds 1
+    // takes it for every batch that fits, 0 never.
+    const int64_t rte = c->tune.row_rounds;
     int64_t maxrows = 0;
     for (const dlr::BatchSpan &sp : spans) maxrows = std::max(maxrows, sp.rows);
     const int64_t rounds = (maxrows + dlr::kRtRows - 1) / dlr::kRtRows;
     const bool want_rt = allow_rt && rounds <= dlr::kRtMaxRounds &&
-                         (rte ? strcmp(rte, "0") != 0 : rounds <= 2);
+                         (rte != DLR_AUTO ? rte != 0 : rounds <= 2);
     for_batches(ns, nthreads, [&](int64_t b) {
         if (ok && !pm_batch(src, spans[(size_t)b], D, t.unit, want_rt, pm[(size_t)b])) ok = false;
     });
@@ -2379,8 +2375,8 @@ int build_pm(dlr_ctx *c, const CsrView &src, const std::vector<dlr::BatchSpan> &
             t.pm_groups = std::max(t.pm_groups, q.groups);
         }
         t.pm_split = (int)std::min<int64_t>(16, std::max<int64_t>(1, (maxslice + 16383) / 16384));
-        if (const char *sp = getenv("DLR_PM_SPLIT"))  // A/B: pass-1 workgroups per slice (separate pass)
-            t.pm_split = std::max(t.pm_split, std::min(16, std::max(1, atoi(sp))));
+        if (c->tune.pm_split != DLR_AUTO)  // pass-1 workgroups per slice (separate pass)
+            t.pm_split = std::max(t.pm_split, (int)std::min<int64_t>(16, std::max<int64_t>(1, c->tune.pm_split)));
         // one device array per member: the batches' parts back to back
         // (offsets off[b] / div elements), each batch's host part
         // released once copied, so the host peak stays ~1x the layout
@@ -2706,6 +2702,7 @@ int exchange_overlapped(dlr_ctx *c, int64_t b) {
 int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_t *n_batches) {
     if (!c) return fail(c, DLR_E_ARG, "dlr_load_train: bad argument");
     HIPC(c, hipSetDevice(c->device));
+    load_tuning(c);
     {
         std::string msg;
         if (!ds)
@@ -2757,10 +2754,10 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
     // collectively, since it also picks the exchange (sparse all-gather vs
     // key-range all-to-all).  DLR_GRAD_KERNEL=touched forces it.
     int rc;
-    const char *gk = getenv("DLR_GRAD_KERNEL");
+    const int64_t gk = c->tune.grad_layout;  // DLR_AUTO or a DLR_LAYOUT_*
     {
         const int64_t epb = std::max<int64_t>(1, t.coff[(size_t)nb] / std::max<int64_t>(1, nb));
-        int64_t want = (gk && strcmp(gk, "touched") == 0) ? 1 : (gk ? 0 : (D > 8 * epb ? 1 : 0));
+        int64_t want = gk == DLR_LAYOUT_TOUCHED ? 1 : (gk != DLR_AUTO ? 0 : (D > 8 * epb ? 1 : 0));
         if ((rc = coll_max_i64(c, &want))) return rc;
         t.touched = want != 0;
         if (c->comm && c->world > dlr::kMaxRanks)
@@ -2779,8 +2776,8 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         if ((rc = change_perm(c, std::move(np)))) return rc;
         // DLR_MARGIN_HOT=0|1 forces the LDS hot-weight margin (it needs D >=
         // kMarginHot); default: on for frequency-ordered shards
-        const char *mh = getenv("DLR_MARGIN_HOT");
-        t.margin_hot = D >= dlr::kMarginHot && (mh ? atoi(mh) != 0 : !c->perm.empty());
+        const int64_t mh = c->tune.margin_hot;
+        t.margin_hot = D >= dlr::kMarginHot && (mh != DLR_AUTO ? mh != 0 : !c->perm.empty());
         if (!c->perm.empty()) {
             mapped.resize(ds->col.size());
             const int nt = dlr::default_threads();
@@ -2795,12 +2792,12 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
     }
     const CsrView src{ds->n_rows, ds->row_ptr.data(), c->perm.empty() ? ds->col.data() : mapped.data(),
                       ds->val.data()};
-    t.unit = unit_values(ds->val);
+    t.unit = unit_values(c, ds->val);
     // Row bands (classic layout, DLR_BAND_ROWS: rows per band, rounded down
     // to a power of two; 0 = off; default 2^20 rows, a 4 MB residual slice,
     // for batches of >= 2 bands); the long columns then go in row phases.
-    const char *brs = getenv("DLR_BAND_ROWS");
-    const int64_t band_rows = brs ? atoll(brs) : (int64_t)1 << 20;
+    const bool brs = c->tune.band_rows != DLR_AUTO;  // forced
+    const int64_t band_rows = tv(c->tune.band_rows, (int64_t)1 << 20);
     int shift = 0;
     while (band_rows > 0 && ((int64_t)2 << shift) <= band_rows) ++shift;
     const bool band = !t.touched && band_rows > 0 && shift > 0 &&
@@ -2897,7 +2894,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
     // phase block fits one window; else the classic layout.
     // DLR_GRAD_KERNEL=classic|lds forces a choice (lds still needs to fit).
     const int nthreads = dlr::default_threads();
-    const bool force_classic = t.touched || (gk && strcmp(gk, "classic") == 0);
+    const bool force_classic = t.touched || gk == DLR_LAYOUT_CLASSIC;
     int64_t csc_bytes = 0;
     int64_t resid_need = t.B;
     PcscBuild pb;
@@ -2908,7 +2905,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         pb.pblocks = pb.groups * pb.P;
         t.pcsc = pb.P <= 4 && pcsc_plan(src, t.plan, D, pb, nthreads);
     }
-    if (gk && strcmp(gk, "lds") == 0 && !t.pcsc)
+    if (gk == DLR_LAYOUT_LDS && !t.pcsc)
         return fail(c, DLR_E_ARG, "dlr_load_train: DLR_GRAD_KERNEL=lds but the batches do not fit the LDS layout");
     if (t.pcsc) {
         t.phases = pb.P;
@@ -2918,8 +2915,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         for (int64_t b = 0; b < nb; ++b) t.poff[(size_t)b + 1] = t.poff[(size_t)b] + pb.size[(size_t)b];
         const int64_t total = t.poff[(size_t)nb];
         std::vector<uint32_t> base((size_t)nb * (size_t)(pb.pblocks + 1));
-        const char *gb = getenv("DLR_STREAM_DEVICE_LAYOUT");  // "0": stream the host-built layout (A/B)
-        t.gpu_pcsc = t.sparse_stream && !(gb && strcmp(gb, "0") == 0);
+        t.gpu_pcsc = t.sparse_stream && tv(c->tune.stream_device_layout, 1) != 0;
         if (t.gpu_pcsc) {
             pcsc_bases(src, t.plan, D, pb, base, nthreads);
             const int64_t pbk = pb.pblocks;
@@ -2957,20 +2953,18 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         // Product margin (dlr_kernels.hip "Product margin"): resident shards
         // whose batches fit it, with enough column slices to fill the GPU
         // (DLR_PM=0 off, =1 on whenever the batches fit).
-        const char *pme = getenv("DLR_PM");
+        const int64_t pme = c->tune.product_margin;  // DLR_AUTO, 0 off, 1 required
         const int64_t S = (D + dlr::kPmSlice - 1) / dlr::kPmSlice;
-        if (!t.sparse_stream && !(pme && strcmp(pme, "0") == 0) && ((pme && strcmp(pme, "1") == 0) || S >= 128)) {
+        if (!t.sparse_stream && pme != 0 && (pme == 1 || S >= 128)) {
             bool built = false;
-            if ((rc = build_pm(c, src, t.plan, true, pme && strcmp(pme, "1") == 0, nthreads, resid_need, csc_bytes, built)))
+            if ((rc = build_pm(c, src, t.plan, true, pme == 1, nthreads, resid_need, csc_bytes, built)))
                 return rc;
             if (built) {
                 t.pm = true;
-                const char *pf = getenv("DLR_PM_FUSED");
-                t.pm_fused = !c->comm && !(pf && strcmp(pf, "0") == 0);
-                // the margin inside the gradient launch (DLR_PM_MG=0: its own
-                // launch, k_pm_margin)
-                const char *pg = getenv("DLR_PM_MG");
-                t.pm_mg = t.pm_fused && !(pg && strcmp(pg, "0") == 0);
+                t.pm_fused = !c->comm && tv(c->tune.pm_fused, 1) != 0;
+                // the margin inside the gradient launch (pm_in_gradient 0: its
+                // own launch, k_pm_margin)
+                t.pm_mg = t.pm_fused && tv(c->tune.pm_in_gradient, 1) != 0;
                 t.mg_demoted = t.pm_mg && c->mg_demoted;
                 if (t.mg_demoted) t.pm_mg = false;
                 // ... only if every batch's launch is resident at once
@@ -2988,7 +2982,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                     t.pm_gen = 0;
                 }
                 if (c->comm && (rc = build_overlap_groups(c))) return rc;
-            } else if (pme && strcmp(pme, "1") == 0) {
+            } else if (pme == 1) {
                 return fail(c, DLR_E_ARG, "dlr_load_train: DLR_PM=1 but the batches do not fit the product margin");
             }
         }
@@ -3074,8 +3068,8 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
         // 512..16,384, profiles/r03t_*), otherwise 2^17; DLR_LONG_COLUMN
         // overrides the FAST threshold (A/B) and never changes the
         // reference order.
-        const char *lm = getenv("DLR_LONG_COLUMN");
-        const int64_t long_min = c->order != DLR_ORDER_FAST ? 0 : lm ? atoll(lm) : band ? 2048 : ((int64_t)1 << 17);
+        const int64_t lm = c->tune.long_column;
+        const int64_t long_min = c->order != DLR_ORDER_FAST ? 0 : lm != DLR_AUTO ? lm : band ? 2048 : ((int64_t)1 << 17);
         int64_t lbytes = 0;
         auto finish_long = [&](auto &lb) -> int {
             // concatenate the batches' long columns
@@ -3094,7 +3088,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             if (!t.any_long) return DLR_OK;
             if (band) {
                 LPhaseBuild ph;
-                build_long_phases(lb, t.B, t.unit, ph);
+                build_long_phases(lb, t.B, t.unit, long_piece(c->tune), ph);
                 std::vector<uint32_t> cols;
                 for (auto &L : lb) {
                     cols.insert(cols.end(), L.cols.begin(), L.cols.end());
@@ -3157,7 +3151,7 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             if ((r = place(c, &t.lcols, cols.data(), cols.size(), 0, r_cols))) return r;
             if ((r = place(c, &t.lcseg, cseg.data(), cseg.size(), 0, r_cseg))) return r;
             if ((r = place(c, &t.lsptr, sptr.data(), sptr.size(), 0, r_seg))) return r;
-            if (!(getenv("DLR_LONG_SCHED") && strcmp(getenv("DLR_LONG_SCHED"), "0") == 0) &&
+            if (tv(c->tune.long_sched, 1) != 0 &&
                 (r = place(c, &t.lsched, sched.data(), sched.size(), 0, r_seg)))
                 return r;
             if ((r = place(c, (RowT **)&t.lrow, row.data(), row.size(), dlr::kLongChunk, r_ent))) return r;
@@ -3181,13 +3175,12 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             // REFERENCE order: the hot columns' pairs run in k_band_hot
             // (DLR_BAND_HOT: entries in the batch that make a column hot;
             // 0 = none)
-            const char *bh = getenv("DLR_BAND_HOT");
-            int64_t hot_min = long_min == 0 ? (bh ? atoll(bh) : (int64_t)1 << 17) : 0;
+            int64_t hot_min = long_min == 0 ? tv(c->tune.band_hot, (int64_t)1 << 17) : 0;
             // with the hot-column product stream: at most hs_max_cols() hot
             // columns a batch (the hottest; the others' chains run in
             // k_grad_band, band by band)
-            if (hot_min > 0 && t.margin_hot && hot_stream_wanted())
-                hot_min = hot_stream_threshold(cptr, nb, D, hot_min);
+            if (hot_min > 0 && t.margin_hot && hot_stream_wanted(c))
+                hot_min = hot_stream_threshold(c, cptr, nb, D, hot_min);
             build_bands(cptr, crow, cval, t.coff, nb, D, t.B, shift, t.unit, nthreads, hot_min, bb);
             t.band_shift = shift;
             t.band_longrun = long_min == 0;
@@ -3260,10 +3253,9 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
             csc_bytes += (int64_t)(cptr.size() * 4 + (total + kPad) * ((t.row16 ? 2 : 4) + (t.unit ? 0 : 4)));
         csc_bytes += lbytes;
         // the windowed product margin (band mode, no hot-weight margin)
-        const char *pme = getenv("DLR_PM");
+        const int64_t pme = c->tune.product_margin;
         const int64_t S = (D + dlr::kPmSlice - 1) / dlr::kPmSlice;
-        if (band && !t.margin_hot && ((int64_t)1 << shift) % kPmWinRows == 0 && !(pme && strcmp(pme, "0") == 0) &&
-            ((pme && strcmp(pme, "1") == 0) || S >= 128)) {
+        if (band && !t.margin_hot && ((int64_t)1 << shift) % kPmWinRows == 0 && pme != 0 && (pme == 1 || S >= 128)) {
             std::vector<dlr::BatchSpan> spans;
             t.pmw_first.assign((size_t)nb + 1, 0);
             for (int64_t b = 0; b < nb; ++b) {
@@ -3275,11 +3267,11 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 t.pmw_first[(size_t)b + 1] = (int64_t)spans.size();
             }
             bool built = false;
-            if ((rc = build_pm(c, src, spans, false, pme && strcmp(pme, "1") == 0, nthreads, resid_need, csc_bytes,
+            if ((rc = build_pm(c, src, spans, false, pme == 1, nthreads, resid_need, csc_bytes,
                                built)))
                 return rc;
             t.pmw = built;
-            if (!built && pme && strcmp(pme, "1") == 0)
+            if (!built && pme == 1)
                 return fail(c, DLR_E_ARG, "dlr_load_train: DLR_PM=1 but the batches' windows do not fit the product margin");
         }
     }
@@ -3307,6 +3299,7 @@ int dlr_load_test(dlr_ctx *c, const dlr_dataset *ds) {
     if (!c || !ds) return fail(c, DLR_E_ARG, "dlr_load_test: bad argument");
     if (ds->D != c->D) return fail(c, DLR_E_ARG, "dlr_load_test: dataset D != context D");
     HIPC(c, hipSetDevice(c->device));
+    if (!c->train.loaded) load_tuning(c);  // (else the training shard's)
     if (int rc_ = wait_stream(c, c->stream, __func__)) return rc_;
     free_test(c);
     TestShard &t = c->test;
@@ -3320,7 +3313,7 @@ int dlr_load_test(dlr_ctx *c, const dlr_dataset *ds) {
     }
     if ((rc = upload(c, &t.row_ptr, ds->row_ptr.data(), (size_t)t.n_rows + 1))) return rc;
     if ((rc = upload(c, &t.col, c->perm.empty() ? ds->col.data() : mapped.data(), (size_t)t.nnz, kPad))) return rc;
-    if (!unit_values(ds->val) && (rc = upload(c, &t.val, ds->val.data(), (size_t)t.nnz, kPad))) return rc;
+    if (!unit_values(c, ds->val) && (rc = upload(c, &t.val, ds->val.data(), (size_t)t.nnz, kPad))) return rc;
     std::vector<float> lab(ds->label.begin(), ds->label.end());
     if ((rc = upload(c, &t.label, lab.data(), lab.size()))) return rc;
     t.grid = dlr::predict_grid(t.n_rows);
@@ -3338,6 +3331,7 @@ int dlr_load_test(dlr_ctx *c, const dlr_dataset *ds) {
 int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, int64_t *n_batches) {
     if (!c) return fail(c, DLR_E_ARG, "dlr_load_train_dense: bad argument");
     HIPC(c, hipSetDevice(c->device));
+    load_tuning(c);
     {
         std::string msg;
         if (!ds)
@@ -3370,26 +3364,25 @@ int dlr_load_train_dense(dlr_ctx *c, const dlr_dense *ds, int64_t batch_size, in
     // large batches, launch_dense_step); FAST -- for batch rows x D > 2^24
     // the fused one-pass kernel where D allows (C4), else the two-pass
     // blocked sums (DLR_DENSE_GRAD=blocked|fused picks a FAST variant).
-    const char *dg = c->order == DLR_ORDER_FAST ? getenv("DLR_DENSE_GRAD") : nullptr;
+    const int64_t dg = c->tune.dense_grad;  // FAST order: DLR_AUTO, 0 chain, 1 blocked, 2 fused
     const bool big = t.B * D > ((int64_t)1 << 24);
     if (c->order == DLR_ORDER_FAST) {
-        t.dfused = dg ? strcmp(dg, "fused") == 0 : (big && dlr::dense_fused_ok(D));
+        t.dfused = dg != DLR_AUTO ? dg == 2 : (big && dlr::dense_fused_ok(D));
         if (t.dfused && !dlr::dense_fused_ok(D))
-            return fail(c, DLR_E_ARG, "dlr_load_train_dense: DLR_DENSE_GRAD=fused needs D in {512, 1024, 2048, 4096}");
-        t.dblocked = t.dfused || (dg ? strcmp(dg, "blocked") == 0 : big);
+            return fail(c, DLR_E_ARG, "dlr_load_train_dense: the fused dense gradient needs D in {512, 1024, 2048, 4096}");
+        t.dblocked = t.dfused || (dg != DLR_AUTO ? dg == 1 : big);
     } else {
         // the banded reference-order launch (k_dense_ref) for large batches;
         // DLR_DENSE_REF=1|0 forces it on (where D allows) / off (A/B: the
         // margin kernel, then the column-chain kernel -- the same order)
-        const char *dr = getenv("DLR_DENSE_REF");
-        t.dref = dlr::dense_ref_ok(D, ds->n_rows, t.B) && (dr ? strcmp(dr, "0") != 0 : big);
+        const int64_t dr = c->tune.dense_ref;
+        t.dref = dlr::dense_ref_ok(D, ds->n_rows, t.B) && (dr != DLR_AUTO ? dr != 0 : big);
         t.mg_demoted = t.dref && c->dref_demoted;
         if (t.mg_demoted) t.dref = false;
         // how far (in 256-row slots) the margins may run ahead of the column
         // chains: the rows the chains re-read stay in the Infinity Cache
         // (DLR_DENSE_REF_LEAD: A/B; 0 = no limit)
-        const char *dl = getenv("DLR_DENSE_REF_LEAD");
-        t.dref_lead = dl ? atoi(dl) : 64;
+        t.dref_lead = (int)tv(c->tune.dense_ref_lead, 64);
     }
     t.fast = t.dblocked;
     // Residency: device-resident unless asked to stream, or (auto) the rows
@@ -3809,6 +3802,78 @@ int dlr_set_fault(dlr_ctx *c, int fault) {
     if (!c || fault < dlr::kFaultNone || fault > dlr::kFaultHotRing)
         return fail(c, DLR_E_ARG, "dlr_set_fault: bad fault");
     c->fault = fault;
+    return DLR_OK;
+}
+
+void dlr_tuning_default(dlr_tuning *t) {
+    if (!t) return;
+    int64_t *f = reinterpret_cast<int64_t *>(t);
+    for (size_t k = 0; k < sizeof(dlr_tuning) / sizeof(int64_t); ++k) f[k] = DLR_AUTO;
+}
+
+// The environment's tuning: each DLR_* variable the header names, parsed
+// as the engine always has (a numeric value, or 0 / any other value for a
+// switch; names for the layout and the dense gradient).
+void dlr_tuning_from_env(dlr_tuning *t) {
+    if (!t) return;
+    dlr_tuning_default(t);
+    auto num = [](const char *name, int64_t &f) {
+        if (const char *e = getenv(name)) f = atoll(e);
+    };
+    auto on_off = [](const char *name, int64_t &f) {  // "0" off, any other value on
+        if (const char *e = getenv(name)) f = strcmp(e, "0") == 0 ? 0 : 1;
+    };
+    if (const char *e = getenv("DLR_GRAD_KERNEL"))
+        t->grad_layout = strcmp(e, "classic") == 0 ? DLR_LAYOUT_CLASSIC
+                         : strcmp(e, "lds") == 0   ? DLR_LAYOUT_LDS
+                         : strcmp(e, "touched") == 0 ? DLR_LAYOUT_TOUCHED
+                                                     : DLR_AUTO;
+    if (const char *e = getenv("DLR_PM"))  // "0" off, "1" required, else automatic
+        t->product_margin = strcmp(e, "0") == 0 ? 0 : strcmp(e, "1") == 0 ? 1 : DLR_AUTO;
+    on_off("DLR_PM_FUSED", t->pm_fused);
+    on_off("DLR_PM_MG", t->pm_in_gradient);
+    num("DLR_PM_SPLIT", t->pm_split);
+    on_off("DLR_GRAD_RT", t->row_rounds);
+    num("DLR_BAND_ROWS", t->band_rows);
+    on_off("DLR_BAND_PIPE", t->band_pipeline);
+    num("DLR_BAND_HOT", t->band_hot);
+    on_off("DLR_HOT_STREAM", t->hot_stream);
+    num("DLR_HOT_STREAM_MAX", t->hot_stream_max);
+    if (const char *e = getenv("DLR_MARGIN_HOT")) t->margin_hot = atoi(e) != 0 ? 1 : 0;
+    num("DLR_LONG_COLUMN", t->long_column);
+    num("DLR_LONG_PIECE", t->long_piece);
+    on_off("DLR_LONG_SCHED", t->long_sched);
+    num("DLR_RELABEL", t->relabel);
+    num("DLR_RELABEL_TAIL", t->relabel_tail);
+    num("DLR_RELABEL_RARE", t->relabel_rare);
+    on_off("DLR_UNIT_VALUES", t->unit_values);
+    on_off("DLR_STREAM_COALESCE", t->stream_coalesce);
+    on_off("DLR_STREAM_DEVICE_LAYOUT", t->stream_device_layout);
+    if (const char *e = getenv("DLR_DENSE_GRAD"))
+        t->dense_grad = strcmp(e, "fused") == 0 ? 2 : strcmp(e, "blocked") == 0 ? 1 : 0;
+    on_off("DLR_DENSE_REF", t->dense_ref);
+    num("DLR_DENSE_REF_LEAD", t->dense_ref_lead);
+}
+
+int dlr_set_tuning(dlr_ctx *c, const dlr_tuning *t) {
+    if (!c) return fail(c, DLR_E_ARG, "dlr_set_tuning: null context");
+    if (t) {
+        if (t->grad_layout != DLR_AUTO && (t->grad_layout < DLR_LAYOUT_CLASSIC || t->grad_layout > DLR_LAYOUT_TOUCHED))
+            return fail(c, DLR_E_ARG, "dlr_set_tuning: grad_layout");
+        if (t->band_rows != DLR_AUTO && (t->band_rows < 0 || (t->band_rows & (t->band_rows - 1)) != 0))
+            return fail(c, DLR_E_ARG, "dlr_set_tuning: band_rows must be 0 or a power of two");
+        if (t->dense_grad != DLR_AUTO && (t->dense_grad < 0 || t->dense_grad > 2))
+            return fail(c, DLR_E_ARG, "dlr_set_tuning: dense_grad");
+        c->tune = *t;
+    }
+    c->tune_set = t != nullptr;
+    return DLR_OK;
+}
+
+int dlr_get_tuning(dlr_ctx *c, dlr_tuning *t) {
+    if (!c || !t) return fail(c, DLR_E_ARG, "dlr_get_tuning: bad argument");
+    if (!c->tune_set && !c->train.loaded) dlr_tuning_from_env(&c->tune);
+    *t = c->tune;
     return DLR_OK;
 }
 

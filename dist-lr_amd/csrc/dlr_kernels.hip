@@ -83,21 +83,6 @@ __device__ __forceinline__ float lds_rd32(uint32_t a) {
 __device__ __forceinline__ void lds_wr128(uint32_t a, v4f v) {
     asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
-// LDS-DMA hidden from the compiler: 16 bytes per lane from gsrc to LDS byte
-// address lds_dst (wave-uniform) + 16 * lane; M0 written and restored in
-// the statement (cdna_hip_programming.md, the LDS-DMA recipe).  The
-// compiler counts none of these in its vmcnt bookkeeping -- callers wait
-// for them with explicit vmcnt -- and, unlike the builtin, they do not make
-// its own waits for register loads in flight beside them vmcnt(0) (an
-// LDS-DMA pending beside plain loads is a mixed-event counter to it).
-__device__ __forceinline__ void lds_dma16(const void *gsrc, uint32_t lds_dst) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds_dst)
-                 : "memory");
-}
-__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void lds_wait1(float &a) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a)); }
 __device__ __forceinline__ void lds_wait4(float &a, float &b, float &c, float &d) {
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
@@ -977,50 +962,7 @@ namespace {
 #ifndef DLR_MG_SLEEP  // the fused margin's poll interval (x 64 cycles)
 #define DLR_MG_SLEEP 8
 #endif
-#ifndef DLR_MG_HOLD  // 1: C2 26.8 vs 28.0 us per step (profiles/r04mg5)
-#define DLR_MG_HOLD 1
-#endif
-#ifndef DLR_MG_EVEN  // workgroups past the slices to even out the blocks
-#define DLR_MG_EVEN 1
-#endif
 constexpr int kMgSub = 8;  // sub-counters per phase (DevP2)
-#ifndef DLR_WIN1_EARLY  // A/B builds: k_grad_lds two-phase issue order
-#define DLR_WIN1_EARLY 0
-#endif
-// DLR_LIST_LATE = k >= 1: the pass-1 list at the top of phase 1's group k - 1
-#ifndef DLR_LIST_LATE  // 1: C2 25.7 vs 26.5 us per step (profiles/r05_c2_issue_order.txt)
-#define DLR_LIST_LATE 1
-#endif
-#ifndef DLR_LIST_SPREAD  // 1: C2 25.3 vs 25.7 us per step (profiles/r05_c2_issue_order.txt)
-#define DLR_LIST_SPREAD 1
-#endif
-#ifndef DLR_SLAB_NOWAIT  // 1: 25.05-25.10 vs 25.10-25.16 us (profiles/r05_c2_issue_order.txt)
-#define DLR_SLAB_NOWAIT 1
-#endif
-#ifndef DLR_GRP_PIPE  // 1: 24.57 vs 24.97-25.00 us (profiles/r05_c2_issue_order.txt)
-#define DLR_GRP_PIPE 1
-#endif
-#ifndef DLR_RT_POLLER  // k_grad_rt MG: the wave that polls (A/B: 15 = the last, no entry loads)
-#define DLR_RT_POLLER 0
-#endif
-#ifndef DLR_MG_POLL_FIRST
-#define DLR_MG_POLL_FIRST 0
-#endif
-#ifndef DLR_WIN_SPREAD  // 1: 25.16 vs 25.24 us (profiles/r05_c2_issue_order.txt)
-#define DLR_WIN_SPREAD 1
-#endif
-#ifndef DLR_MG_FILL_SC1
-#define DLR_MG_FILL_SC1 0
-#endif
-#ifndef DLR_W_SC1
-#define DLR_W_SC1 0
-#endif
-#ifndef DLR_PM_NT
-#define DLR_PM_NT 0
-#endif
-#ifndef DLR_PM_SC1
-#define DLR_PM_SC1 ((DLR_ABL & 16) != 0)
-#endif
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 #ifndef DLR_GRAD_WAVES  // A/B builds only (make variant VDEFS=...): 16 x 4 in the product
@@ -1125,13 +1067,10 @@ struct PmPass1 {
                     q.y = s_w[(x >> 12) & 0xFFFu] * (unit ? 1.0f : v[u].y);
                     q.z = s_w[(x >> 24) | ((y & 0xFu) << 8)] * (unit ? 1.0f : v[u].z);
                     q.w = s_w[(y >> 4) & 0xFFFu] * (unit ? 1.0f : v[u].w);
-                    if (DLR_PM_SC1) {
+                    if (DLR_ABL & 16) {  // (stamps-build variant: write-through stores)
                         const u32x4 b = {__float_as_uint(q.x), __float_as_uint(q.y), __float_as_uint(q.z),
                                          __float_as_uint(q.w)};
                         __builtin_amdgcn_raw_buffer_store_b128(b, rs, (int)((s_po[k] + j) * 4u), 0, 16);
-                    } else if (DLR_PM_NT) {  // (A/B: non-temporal product stores)
-                        const v4f qv = {q.x, q.y, q.z, q.w};
-                        __builtin_nontemporal_store(qv, reinterpret_cast<v4f *>(p + s_po[k] + j));
                     } else {
                         *reinterpret_cast<float4 *>(p + s_po[k] + j) = q;
                     }
@@ -1258,14 +1197,11 @@ __global__ __launch_bounds__(256) void k_pm_margin(DevPm pm, DevBatch bt, const 
 // after every block's copy of its region.  The launch boundary between the
 // margin and the gradient is gone and the gradient's window loads stream
 // while the blocks are summed.
-// DB (double-buffered phases; batches of 16,385-65,536 rows, FILL = 4): up
-// to four phases of 16,384 rows in two 64 KB residual buffers.  At the top
-// of phase p the workgroup issues phase p + 1's windows and fill into the
-// other buffer, then computes phase p: each fill streams while the previous
-// phase computes (the two-phase form waits for its second 128 KB fill with
-// nothing to do: profiles/r05_stamps_c2_pollskip.txt, 14.5 -> 18.2 us).
-// The same blocks, the same column order: bitwise the two-phase form.
-template <int FILL, bool FUSED, bool NTW, bool PM = false, bool MG = false, bool DB = false>
+// (A double-buffered form -- phases of 16,384 rows in two 64 KB buffers,
+// each fill streaming while the previous phase computes -- was measured
+// slower: C2 31.2 vs 24.8 us per step, a phase costing nearly what a
+// 32,768-row one does; profiles/r05_stamps_c2_db.txt.  Removed in round 6.)
+template <int FILL, bool FUSED, bool PM = false, bool MG = false>
 __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int64_t D, int64_t B,
                                                                 const float *__restrict__ resid,
                                                                 float *__restrict__ w, float *__restrict__ gout,
@@ -1273,15 +1209,13 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
                                                                 DevPm pn = DevPm{}, float *__restrict__ pm_p = nullptr,
                                                                 DevP2 p2 = DevP2{}) {
     constexpr int R = FILL * 4096;      // rows per phase
-    constexpr int NB = DB ? 2 : 1;      // residual buffers
-    constexpr int NPH = DB ? 4 : 2;     // phases
+    constexpr int NPH = 2;              // phases
     constexpr int NG = kGradNG;
-    static_assert(!DB || FILL == 4, "double-buffered phases are 16,384 rows");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float *s_r = smem;
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // uniform: scalar block loads
-    float *s_p = smem + NB * R + wv * kBlkPad;
+    float *s_p = smem + R + wv * kBlkPad;
     const uint32_t s_r_a = lds_addr(s_r), s_p_a = lds_addr(s_p);
     const int P = pc.phases;
     const int64_t ng = (D + 63) / 64;
@@ -1294,7 +1228,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
         DLR_STAMP(11);
         if (blockIdx.x == 0 && wv < 8)  // the next launch's bank: 64 phases x 8 sub-counters
             p2.cnt[(((p2.gen + 1) & 1) * 64 + lane) * kMgSub * 32 + wv * 32] = 0u;
-        const int64_t k2 = blockIdx.x + (int64_t)gridDim.x * wv;  // wv < NB * FILL (launch_grad_lds_pm)
+        const int64_t k2 = blockIdx.x + (int64_t)gridDim.x * wv;  // wv < FILL (launch_grad_lds_pm)
         if (k2 < p2.pm.nblk) {  // wave-uniform
             pm_rowsum<8, true>(p2.pm, p2.bt, pm_p, p2.resid, k2, smem + wv * kPmCap, lane);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every residual of the block stored
@@ -1310,8 +1244,8 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
         if (blockIdx.x >= pn.S) return;  // a block-only workgroup (launch_grad_lds_pm): done
         // the other waves' window loads wait for the workgroup's blocks (the
         // blocks' loads have the CU's memory path to themselves: the phases
-        // wait for the slowest block; DLR_MG_HOLD=0 issues them at once)
-        if (DLR_MG_HOLD) lds_barrier();
+        // wait for the slowest block; issued at once: 28.0 vs 26.8 us)
+        lds_barrier();
     }
     // wave 0 waits until every block of phase p is published (the caller's
     // barrier then holds the other waves' fills); a wait that runs out is
@@ -1350,11 +1284,8 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
 #pragma unroll
                         for (int d = 1; d < NPH; ++d)
                             if (done == p + d && p + d < P && n[d] >= want_of(p + d)) done = p + d + 1;
-                        // (DB: every phase, from phase 0 -- see its loop)
-                        if (!DB || done >= P) {
-                            mg_done = done;
-                            break;
-                        }
+                        mg_done = done;
+                        break;
                     }
                     __builtin_amdgcn_s_sleep(DLR_MG_SLEEP);
                 }
@@ -1369,10 +1300,8 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     // the block (<= 255) for the phases in registers (set p & 1; meta) --
     // the column's start is lane - 1's end (a lane shuffle at its use, so
     // that no arithmetic waits for the load where it is issued)
-    // (DB: three register sets -- windows are issued two phases ahead, as
-    // their HBM round trip under load is ~3.5 us, more than a phase)
-    constexpr int RS = DB ? 3 : 2;
-    auto rs = [](int p) { return DB ? p % 3 : p & 1; };
+    constexpr int RS = 2;
+    auto rs = [](int p) { return p & 1; };
     unsigned sb[NG][NPH + 1], hb[NG][RS];
     float acc[NG], wj[NG];
     ushort4 rq[NG][RS];
@@ -1406,7 +1335,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
         }
     };
     meta(0);
-    if (!DB) meta(1);  // (DB: after the first fill)
+    meta(1);
     auto windows = [&](int p, int g0 = 0, int g1 = NG) {
 #pragma unroll
         for (int gi = 0; gi < NG; ++gi) {
@@ -1421,14 +1350,10 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
             // not pulled into this CU), and a duplicate address costs nothing
             const unsigned nb4 = nblk_of(gi, p);
             const unsigned e = bs_of(gi, p) + min((unsigned)lane * 4, nb4 ? nb4 - 4 : 0u);  // padded: in bounds
-            // (register set rs(p): DB holds three phases' windows at a time)
-            if (NTW) {
-                rq[gi][rs(p)] = load_stream(reinterpret_cast<const ushort4 *>(pc.row + e));
-                vq[gi][rs(p)] = load_stream(reinterpret_cast<const float4 *>(pc.val + e));
-            } else {
-                rq[gi][rs(p)] = *reinterpret_cast<const ushort4 *>(pc.row + e);
-                vq[gi][rs(p)] = *reinterpret_cast<const float4 *>(pc.val + e);
-            }
+            // (plain loads: non-temporal ones measured slower, 19.4 vs 16.6 us
+            // for the gradient alone -- the kernel is latency-bound)
+            rq[gi][rs(p)] = *reinterpret_cast<const ushort4 *>(pc.row + e);
+            vq[gi][rs(p)] = *reinterpret_cast<const float4 *>(pc.val + e);
         }
     };
     // Residual fills by LDS-DMA (no VGPRs): each wave-instruction copies
@@ -1439,22 +1364,15 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
     // holding no residual line (the kernel-start acquire), the blocks' sc1
     // stores have reached memory before their counter moved, and a line
     // belongs to one block -- so the first read of a line, and every later
-    // hit on it, sees the stored values.  DLR_MG_FILL_SC1=1: sc1 fills.)
+    // hit on it, sees the stored values.)
     const float *rsrc = MG ? p2.resid : resid;
-    // (into residual buffer buf: DB's phase p goes to buffer p & 1, by the
-    // asm LDS-DMA: see lds_dma16)
-    auto fill = [&](int64_t lo, int buf) {
+    auto fill = [&](int64_t lo) {
 #pragma unroll
         for (int f = 0; f < R / (kGradWaves * kWave * 4); ++f) {  // FILL with 16 waves
             const int o = (f * kGradWaves + wv) * kWave * 4;  // floats; this wave's 1 KiB slot
-            if (DB && !(MG && DLR_MG_FILL_SC1)) {
-                lds_dma16(rsrc + lo + o + lane * 4,
-                          __builtin_amdgcn_readfirstlane(s_r_a + 4u * (uint32_t)(buf * R + o)));
-                continue;
-            }
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)(rsrc + lo + o + lane * 4),
-                (__attribute__((address_space(3))) void *)(s_r + buf * R + o), 16, 0, MG && DLR_MG_FILL_SC1 ? 16 : 0);
+                (__attribute__((address_space(3))) void *)(s_r + o), 16, 0, 0);
         }
     };
     // Group gi's products and column sums of phase p (residuals at LDS
@@ -1474,10 +1392,8 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
             const v4f q = {g0 * v4.x, g1 * v4.y, g2 * v4.z, g3 * v4.w};
             lds_wr128(s_p_a + 16u * lane, q);
         }
-        // the slab is complete (one wave; DLR_SLAB_NOWAIT, A/B: a wave's LDS
-        // operations complete in issue order, so the reads below follow the
-        // slab writes without a wait)
-        if (!DLR_SLAB_NOWAIT) lds_wait();
+        // the slab is complete: a wave's LDS operations complete in issue
+        // order, so the reads below follow the slab writes without a wait
         // this lane's column: cnt products in order from off.  The first
         // eight are read at immediate offsets from s_p + o (the slab is
         // padded, so no clamping) and added while any lane still has one
@@ -1518,8 +1434,8 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
         wave_sync();
         return true;
     };
-    // All NG groups of phase p, software-pipelined (DLR_GRP_PIPE; the wave
-    // has all of them): per group one LDS round trip -- the slab write, its
+    // All NG groups of phase p, software-pipelined (the wave has all of
+    // them; 24.6 vs 25.0 us against group() in turn): per group one LDS round trip -- the slab write, its
     // reads and the next group's residual gathers issued together, then a
     // wait for all but those 4 gathers (LDS returns in order; an older
     // scalar load in the count only makes the wait stricter).  The same
@@ -1584,171 +1500,90 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
             }
         }
     };
-    // Phase 0's windows and the first fill are issued up front.
+    // Phase 0's windows and the first fill are issued up front.  (Wave 0's
+    // poll returns behind its own window loads -- vmcnt is in order -- but
+    // polling first was no faster: 26.96 us, profiles/r04mg.)
     DLR_STAMP(0);
-    // (A/B, DLR_MG_POLL_FIRST: wave 0 polls before its own window loads, so
-    // that its poll does not return behind them)
-    const bool poll_first = MG && DLR_MG_POLL_FIRST && wv == 0;
-    if (!poll_first) windows(0);
-    if (!DB && DLR_WIN1_EARLY) windows(1);  // (A/B: see the two-phase loop)
+    windows(0);
     if constexpr (MG) {
         mg_wait(0);
-        if (poll_first) windows(0);
         lds_barrier();  // and this workgroup's pass-2 regions are read
         DLR_STAMP(13);
     }
-    if (!(DLR_ABL & 1)) fill(0, 0);
-    if (DB) {
-        windows(1);
-        meta(1);
-    }
+    if (!(DLR_ABL & 1)) fill(0);
     DLR_STAMP(8);
 #ifdef DLR_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     DLR_STAMP(9);
 #endif
     DLR_STAMP(10);
-    if constexpr (DB) {
-        // Phase p + 1's fill (from L2) is issued at the top of phase p, and
-        // phase p + 2's windows and column ends (from HBM) after it: the top
-        // of phase p waits for all but those 12 youngest loads per thread
-        // (NG windows of two loads, NG end bytes: every thread issues them,
-        // addresses clamped past the last phase).  Every phase's margin
-        // blocks were awaited before phase 0 (mg_wait in DB form): the loop
-        // holds no poll, whose load loop would make the compiler's own waits
-        // for the window registers vmcnt(0).  The next batch's pass-1 list
-        // is issued at the top of the last phase, so it streams while that
-        // phase computes; batches of fewer phases issue it after the loop.
-        constexpr int lph = NPH - 1;
+    bool listed = false;  // (wave-uniform) this wave issued its share of the pass-1 list
+    int nsets = 0;        // the list's group sets issued (phase 1: one before each group)
 #pragma unroll
-        for (int p = 0; p < NPH; ++p) {
-            if (p >= P) break;  // uniform
-            if (p + 1 < NPH)
-                asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            // This phase's window registers, consumed here -- where the wait
-            // above has drained them -- so that the compiler, which does not
-            // read that asm wait, puts its own wait for them here and not at
-            // their use below, behind the later phases' loads.
-#pragma unroll
-            for (int gi = 0; gi < NG; ++gi) {
-                uint32_t r2[2];
-                __builtin_memcpy(r2, &rq[gi][rs(p)], 8);
-                const float4 v = vq[gi][rs(p)];
-                asm volatile("" ::"v"(r2[0]), "v"(r2[1]), "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w),
-                             "v"(hb[gi][rs(p)]));
-            }
-            // every wave's share of fill p is in LDS, and every wave is done
-            // with phase p - 1: its buffer takes phase p + 1
-            lds_barrier();
-            DLR_STAMP(p == 0 ? 1 : p == 1 ? 4 : p);  // slots 1, 4, 2, 3
-            asm volatile("" ::: "memory");
-            // (unconditional: a load issued on one path only would make the
-            // compiler wait for every load at the join; past the last phase
-            // the addresses are clamped to it)
-            if (p + 1 < NPH) fill((int64_t)min(p + 1, P - 1) * R, (p + 1) & 1);  // resid is padded to P*R floats
-            if (p + 2 < NPH) {
-                windows(p + 2);
-                meta(p + 2);
-            }
-            if (PM && !(DLR_ABL & 4) && p == lph) pm.fetch(pn, pm.c0);
-            asm volatile("" ::: "memory");
-            const uint32_t sra = s_r_a + 4u * (uint32_t)((p & 1) * R);
-#pragma unroll
-            for (int gi = 0; gi < NG; ++gi)
-                if (!group(gi, p, sra)) break;
+    for (int p = 0; p < 2; ++p) {
+        if (p >= P) break;  // uniform
+        if (p > 0) {
+            DLR_STAMP(2);
+            mg_wait(p);
+            lds_barrier();  // every wave is done reading the previous phase
+            DLR_STAMP(3);
+            fill((int64_t)p * R);  // resid is padded to P*R floats
         }
-        // (a batch of fewer phases: the fill issued for the phase past its
-        // last is still landing in LDS that pass 1 reuses)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (PM && !(DLR_ABL & 4) && P <= lph) pm.fetch(pn, pm.c0);
-    } else {
-        bool listed = false;  // (wave-uniform) this wave issued its share of the pass-1 list
-        int nsets = 0;        // (DLR_LIST_SPREAD) the list's group sets issued
-        // Phase 1's windows only after phase 0's first group has consumed
-        // its data (the compiler drains every older load there), so they
-        // stream from HBM while the rest of phase 0 computes instead of
-        // delaying its start.
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            if (p >= P) break;  // uniform
-            if (p > 0) {
-                DLR_STAMP(2);
-                mg_wait(p);
-                lds_barrier();  // every wave is done reading the previous phase
-                DLR_STAMP(3);
-                fill((int64_t)p * R, 0);  // resid is padded to P*R floats
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA fill (not tracked by the compiler)
-            lds_barrier();
-            DLR_STAMP(1 + 3 * p);
-            // the loads issued between phase p's groups (VMEM only)
-            auto hooks = [&](int gi) {
-            if (p == 0 && gi == 1) {
-                // phase 1's windows and the next batch's pass-1 slice list
-                // (its range was loaded first thing) stream while the rest of
-                // phase 0 computes: issued here, after the first group's
-                // compiler-placed waits, they do not delay phase 0's start
-                // (A/B: DLR_WIN1_EARLY issues the windows with phase 0's,
-                // DLR_LIST_LATE the list at the top of phase 1)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA fill (not tracked by the compiler)
+        lds_barrier();
+        DLR_STAMP(1 + 3 * p);
+        // The loads issued between phase p's groups (VMEM only), after the
+        // first group's compiler-placed waits so that they do not delay
+        // phase 0's start: in phase 0, phase 1's windows group by group
+        // (2 before group 1, then one per group: 25.16 vs 25.24 us at once);
+        // in phase 1, the next batch's pass-1 list, one of its four group
+        // sets before each group (25.3 vs 25.7 at once, vs 26.5 in phase 0:
+        // profiles/r05_c2_issue_order.txt).  A one-phase batch issues the
+        // whole list in phase 0.
+        auto hooks = [&](int gi) {
+            if (p == 0 && gi >= 1) {
                 asm volatile("" ::: "memory");
-                if (P > 1 && !DLR_WIN1_EARLY) {
-                    if (DLR_WIN_SPREAD)
-                        windows(1, 0, 2);  // (A/B: the rest before groups 2 and 3)
+                if (P > 1) {
+                    if (gi == 1)
+                        windows(1, 0, 2);
                     else
-                        windows(1);
-                }
-                if (PM && !(DLR_ABL & 4) && !(DLR_LIST_LATE && P > 1)) {
+                        windows(1, gi, gi + 1);
+                } else if (gi == 1 && PM && !(DLR_ABL & 4)) {
                     pm.fetch(pn, pm.c0);
                     listed = true;
                 }
                 asm volatile("" ::: "memory");
             }
-            if (DLR_WIN_SPREAD && !DLR_WIN1_EARLY && p == 0 && gi >= 2 && P > 1) {
-                asm volatile("" ::: "memory");
-                windows(1, gi, gi + 1);
-                asm volatile("" ::: "memory");
-            }
-            if (DLR_LIST_LATE && !DLR_LIST_SPREAD && PM && !(DLR_ABL & 4) && p == 1 &&
-                gi == DLR_LIST_LATE - 1) {
-                asm volatile("" ::: "memory");
-                pm.fetch(pn, pm.c0);
-                listed = true;
-                asm volatile("" ::: "memory");
-            }
-            if (DLR_LIST_LATE && DLR_LIST_SPREAD && PM && !(DLR_ABL & 4) && p == 1) {
-                // (A/B: one of the list's four group sets before each group)
+            if (p == 1 && PM && !(DLR_ABL & 4)) {
                 asm volatile("" ::: "memory");
                 pm.fetch_one(pn, pm.c0, gi);
                 nsets = gi + 1;
                 asm volatile("" ::: "memory");
             }
-            };
-            // (A/B, DLR_GRP_PIPE: a wave with all NG groups software-pipelines
-            // them -- group gi + 1's residual gathers in flight with group
-            // gi's slab reads and adds, the slab rewritten after the reads
-            // are issued: a wave's LDS operations complete in issue order)
-            if (DLR_GRP_PIPE && gfirst + kGradWaves * (NG - 1) < ng) {
-                group_pipe(p, s_r_a, hooks);
-            } else {
+        };
+        // a wave with all NG groups software-pipelines them -- group gi +
+        // 1's residual gathers in flight with group gi's slab reads and
+        // adds, the slab rewritten after the reads are issued: a wave's LDS
+        // operations complete in issue order (24.6 vs 25.0 us in turn)
+        if (gfirst + kGradWaves * (NG - 1) < ng) {
+            group_pipe(p, s_r_a, hooks);
+        } else {
 #pragma unroll
-                for (int gi = 0; gi < NG; ++gi) {
-                    hooks(gi);
-                    if (!group(gi, p, s_r_a)) break;
-                }
+            for (int gi = 0; gi < NG; ++gi) {
+                hooks(gi);
+                if (!group(gi, p, s_r_a)) break;
             }
         }
-        // a wave with no column group left the loop before issuing its
-        // share of the pass-1 list (every thread takes part in pass 1)
-        if (PM && !(DLR_ABL & 4) && !listed) {
-            if (DLR_LIST_SPREAD && DLR_LIST_LATE && P > 1) {
+    }
+    // a wave with no column group left the loop before issuing its share of
+    // the pass-1 list (every thread takes part in pass 1)
+    if (PM && !(DLR_ABL & 4) && !listed) {
+        if (P > 1) {
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (u >= nsets) pm.fetch_one(pn, pm.c0, u);
-            } else {
-                pm.fetch(pn, pm.c0);
-            }
+            for (int u = 0; u < 4; ++u)
+                if (u >= nsets) pm.fetch_one(pn, pm.c0, u);
+        } else {
+            pm.fetch(pn, pm.c0);
         }
     }
 #ifdef DLR_STAMPS
@@ -1773,12 +1608,7 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_lds(DevPcsc pc, int6
             if (FUSED) {
                 const float step = lr * g;
                 const float wn = wj[gi] - step;
-                if (DLR_W_SC1 && PM) {  // (A/B: write-through, out of L2 before the kernel-end flush)
-                    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(w, 0, 0x7FFFFFFF, 0x00020000);
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(wn), wr, (int)(j * 4), 0, 16);
-                } else {
-                    w[j] = wn;
-                }
+                w[j] = wn;
                 if (PM) smem[(wv + kGradWaves * gi) * 64 + lane] = wn;  // column j - kPmSlice*blockIdx.x
             } else {
                 gout[j] = g;
@@ -1864,11 +1694,9 @@ __global__ __launch_bounds__(kGradWaves *kWave) void k_grad_rt(DevRt rt, int64_t
     }
     const float *rsrc = MG ? p2.resid : resid;
     // (MG) wave kPoller waits until every round's blocks are published; the
-    // caller's barrier holds the other waves' residual loads.  (A/B,
-    // DLR_RT_POLLER=15: the last wave, which sums no block and, when no group
-    // of a round falls to it, issues no entry loads either -- measured no
-    // faster.)
-    constexpr int kPoller = DLR_RT_POLLER;
+    // caller's barrier holds the other waves' residual loads.  (The last
+    // wave, which sums no block, polling instead: measured no faster.)
+    constexpr int kPoller = 0;
     static_assert(kPoller == 0 || kPoller >= kRtRegions, "the poller sums no block");
     auto mg_wait_all = [&]() {
         if constexpr (MG) {
@@ -3067,13 +2895,6 @@ struct ChainCfg {
     static constexpr int count(int h) { return (kXI - (h - 1) + 2) / 3 + (h == 3 ? 1 : 0); }
     static constexpr size_t kLds = ((size_t)kRing * (R * kChainCols + 256) + 2 * kChainCols * kPad) * 4;
 };
-int dense_chain_rows() {
-    static const int r = [] {
-        const char *e = getenv("DLR_CHAIN_ROWS");  // A/B: batch rows per staging slot
-        return e && atoi(e) == 128 ? 128 : 256;
-    }();
-    return r;
-}
 
 template <bool FUSED, int R>
 __global__ __launch_bounds__(256) void k_dense_grad_chain(DevDense dd, int64_t first, int64_t B,
@@ -4248,11 +4069,6 @@ inline unsigned grid_for(int64_t n, int per_block) { return (unsigned)((n + per_
 // Rows per wave for the margin: aim for about one window of entries per
 // wave (fewer, longer-running waves for short rows; more for long rows).
 int margin_seg(const DevBatch &bt) {
-    static const int forced = [] {
-        const char *e = getenv("DLR_MARGIN_SEG");
-        return e ? atoi(e) : 0;
-    }();
-    if (forced == 16 || forced == 32 || forced == 64) return forced;
     if (bt.rows <= 0) return 64;
     const double avg = (double)bt.nnz / (double)bt.rows;
     if (avg * 64 <= kWin) return 64;
@@ -4327,23 +4143,12 @@ hipError_t launch_margin_hot(const DevBatch &bt, const float *w, int64_t D, floa
     // 8, two per CU (1.779 ms).  Also
     // measured on C3: 16,384 x 8 (2.01 ms), 24,576 x 8 (2.00), 4,096 x 8
     // (2.04), 2,048 x 8 (1.87), 8,192 x 4 (1.79), 4,096 x 4 (2.22).
-    // DLR_MARGIN_HOT_SHAPE (A/B only): 1 = 8,192 x 8, 2 = 16,384 x 8,
-    // 3 = 24,576 x 8, 4 = 24,576 x 16, 5 = 20,480 x 16, 6 = 16,384 x 16
-    // (each only when D >= its hot count).
-    static const int shape = [] {
-        const char *e = getenv("DLR_MARGIN_HOT_SHAPE");
-        return e ? atoi(e) : 0;
-    }();
     // (a compacted-cold-gather variant -- ballot + list of the cold entries
     // -- measured slower: 1.90 vs 1.76 ms, profiles/r02_c3_margin_ab.txt)
     // 24,576 x 16 (LDS: exactly 160 KiB) since the rare-column order: C3
     // margin 1.579 vs 1.601 ms for 16,384 x 16 (profiles/r03j_bench_c3_*.json)
-    if (shape == 0 && D >= 24576) return launch_mh<24576, 16>(bt, w, resid, (unsigned)ncu, s, ho);
-    if ((shape == 0 || shape == 6) && D >= 16384) return launch_mh<16384, 16>(bt, w, resid, (unsigned)ncu, s, ho);
-    if (shape == 2 && D >= 16384) return launch_mh<16384, 8>(bt, w, resid, (unsigned)ncu, s, ho);
-    if (shape == 3 && D >= 24576) return launch_mh<24576, 8>(bt, w, resid, (unsigned)ncu, s, ho);
-    if (shape == 4 && D >= 24576) return launch_mh<24576, 16>(bt, w, resid, (unsigned)ncu, s, ho);
-    if (shape == 5 && D >= 20480) return launch_mh<20480, 16>(bt, w, resid, (unsigned)ncu, s, ho);
+    if (D >= 24576) return launch_mh<24576, 16>(bt, w, resid, (unsigned)ncu, s, ho);
+    if (D >= 16384) return launch_mh<16384, 16>(bt, w, resid, (unsigned)ncu, s, ho);
     return launch_mh<kMarginHot, kMarginHotWaves>(bt, w, resid, (unsigned)ncu * 2, s, ho);
 }
 
@@ -4418,29 +4223,18 @@ int grad_lds_fill(int64_t B) {
     return 8;
 }
 
-// Batches of more than 16,384 rows: two phases of 32,768 rows in one
-// buffer by default; DLR_GRAD_DB=1 takes phases of 16,384 rows in two
-// buffers (k_grad_lds DB: measured slower -- C2 31.2 vs 26.5 us per step,
-// each 16,384-row phase costs nearly what a 32,768-row one does;
-// profiles/r05_stamps_c2_db.txt).
-int64_t grad_lds_phase_rows(int64_t B) {
-    const char *e = getenv("DLR_GRAD_DB");  // (read at each load: tests switch it)
-    const bool db = e && strcmp(e, "1") == 0;
-    if (B > 16384 && db) return 16384;
-    return (int64_t)grad_lds_fill(B) * 4096;
-}
+// Batches of more than 16,384 rows: two phases of 32,768 rows in one buffer
+// (k_grad_lds, "A double-buffered form").
+int64_t grad_lds_phase_rows(int64_t B) { return (int64_t)grad_lds_fill(B) * 4096; }
 
 namespace {
-// The kernel form of a layout: FILL = its rows per phase / 4,096, DB when
-// a 16,384-row layout has more than one phase.
-bool grad_lds_db(const DevPcsc &pc) { return pc.fill == 4 && pc.phases > 1; }
+// The kernel form of a layout: FILL = its rows per phase / 4,096; one or
+// two phases.
 bool grad_lds_form_ok(const DevPcsc &pc) {
-    const bool db = grad_lds_db(pc);
-    return (pc.fill == 1 || pc.fill == 2 || pc.fill == 4 || pc.fill == 8) && pc.phases >= 1 &&
-           pc.phases <= (db ? 4 : 2);
+    return (pc.fill == 1 || pc.fill == 2 || pc.fill == 4 || pc.fill == 8) && pc.phases >= 1 && pc.phases <= 2;
 }
 // residual floats in LDS
-size_t grad_lds_rrows(int fill, bool db) { return (size_t)fill * 4096 * (db ? 2 : 1); }
+size_t grad_lds_rrows(int fill) { return (size_t)fill * 4096; }
 }  // namespace
 
 hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float *resid, float *w, float *gout,
@@ -4453,39 +4247,16 @@ hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float 
     const double Bd = (double)B;
     if (!grad_lds_form_ok(pc)) return hipErrorInvalidValue;
     const int fill = pc.fill;
-    const bool db = grad_lds_db(pc);
-    const size_t lds = grad_lds_rrows(fill, db) * 4 + (size_t)kGradWaves * kBlkPad * 4;
-    // Non-temporal window loads measured slower here (tools/ab_bench.sh,
-    // C2: 19.4 vs 16.6 us -- this kernel is latency-bound in its prologue);
-    // DLR_GRAD_NT=1 turns them on.
-    static const bool ntw = [] {
-        const char *e = getenv("DLR_GRAD_NT");
-        return e ? atoi(e) != 0 : false;
-    }();
+    const size_t lds = grad_lds_rrows(fill) * 4 + (size_t)kGradWaves * kBlkPad * 4;
 #define DLR_GL(F)                                                                                                   \
     case F:                                                                                                         \
-        if (fused && ntw)                                                                                           \
-            hipLaunchKernelGGL((k_grad_lds<F, true, true>), dim3(grid), blk, lds, s, pc, D, B, resid, w, gout, Bf,   \
-                               Bd, lr, C);                                                                          \
-        else if (fused)                                                                                             \
-            hipLaunchKernelGGL((k_grad_lds<F, true, false>), dim3(grid), blk, lds, s, pc, D, B, resid, w, gout, Bf,  \
-                               Bd, lr, C);                                                                          \
-        else if (ntw)                                                                                               \
-            hipLaunchKernelGGL((k_grad_lds<F, false, true>), dim3(grid), blk, lds, s, pc, D, B, resid, w, gout, Bf,  \
-                               Bd, lr, C);                                                                          \
+        if (fused)                                                                                                  \
+            hipLaunchKernelGGL((k_grad_lds<F, true>), dim3(grid), blk, lds, s, pc, D, B, resid, w, gout, Bf, Bd, lr, \
+                               C);                                                                                  \
         else                                                                                                        \
-            hipLaunchKernelGGL((k_grad_lds<F, false, false>), dim3(grid), blk, lds, s, pc, D, B, resid, w, gout, Bf, \
-                               Bd, lr, C);                                                                          \
+            hipLaunchKernelGGL((k_grad_lds<F, false>), dim3(grid), blk, lds, s, pc, D, B, resid, w, gout, Bf, Bd,    \
+                               lr, C);                                                                              \
         break;
-    if (db) {
-        if (fused)
-            hipLaunchKernelGGL((k_grad_lds<4, true, false, false, false, true>), dim3(grid), blk, lds, s, pc, D, B,
-                               resid, w, gout, Bf, Bd, lr, C);
-        else
-            hipLaunchKernelGGL((k_grad_lds<4, false, false, false, false, true>), dim3(grid), blk, lds, s, pc, D, B,
-                               resid, w, gout, Bf, Bd, lr, C);
-        return hipGetLastError();
-    }
     switch (fill) {
         DLR_GL(1)
         DLR_GL(2)
@@ -4526,19 +4297,17 @@ hipError_t launch_pm_margin(const DevPm &pm, const DevBatch &bt, const float *p,
 namespace {
 // The one-launch step's kernel for a fill (a workgroup of every grid
 // size it may take must fit beside the others: they wait for each other).
-const void *grad_lds_mg_fn(int fill, bool db) {
-    if (db) return fill == 4 ? reinterpret_cast<const void *>(&k_grad_lds<4, true, false, true, true, true>) : nullptr;
+const void *grad_lds_mg_fn(int fill) {
     switch (fill) {
-        case 1: return reinterpret_cast<const void *>(&k_grad_lds<1, true, false, true, true>);
-        case 2: return reinterpret_cast<const void *>(&k_grad_lds<2, true, false, true, true>);
-        case 4: return reinterpret_cast<const void *>(&k_grad_lds<4, true, false, true, true>);
-        case 8: return reinterpret_cast<const void *>(&k_grad_lds<8, true, false, true, true>);
+        case 1: return reinterpret_cast<const void *>(&k_grad_lds<1, true, true, true>);
+        case 2: return reinterpret_cast<const void *>(&k_grad_lds<2, true, true, true>);
+        case 4: return reinterpret_cast<const void *>(&k_grad_lds<4, true, true, true>);
+        case 8: return reinterpret_cast<const void *>(&k_grad_lds<8, true, true, true>);
         default: return nullptr;
     }
 }
-size_t grad_lds_pm_lds(int fill, bool db) {
-    return std::max(grad_lds_rrows(fill, db) * 4 + (size_t)kGradWaves * kBlkPad * 4,
-                    (size_t)(kPmSlice + kPmMaxBlocks) * 4);
+size_t grad_lds_pm_lds(int fill) {
+    return std::max(grad_lds_rrows(fill) * 4 + (size_t)kGradWaves * kBlkPad * 4, (size_t)(kPmSlice + kPmMaxBlocks) * 4);
 }
 
 // CUs of the current device (cached per device; 0 if the runtime cannot say)
@@ -4553,13 +4322,12 @@ int device_cus() {
     return ncu[dev];
 }
 
-// The MG launch's workgroups: one per slice, or (DLR_MG_EVEN) more when
-// that evens the blocks out over the CUs (C2: 1,024 blocks on 256
-// workgroups, 4 each, not 245 with up to 5); the extra workgroups only
-// sum blocks.
+// The MG launch's workgroups: one per slice, or more when that evens the
+// blocks out over the CUs (C2: 1,024 blocks on 256 workgroups, 4 each, not
+// 245 with up to 5: 26.6 vs 26.9 us); the extra workgroups only sum blocks.
 int64_t grad_lds_mg_grid(int64_t nblk, int64_t grid) {
     const int64_t even = (nblk + 3) / 4;
-    if (DLR_MG_EVEN && even > grid && even <= device_cus()) return even;
+    if (even > grid && even <= device_cus()) return even;
     return grid;
 }
 }  // namespace
@@ -4605,9 +4373,6 @@ int resident_per_cu(const void *fn, int threads, size_t lds, int *query) {
     }
     if (query) *query = q;
     if (q >= 1) n = std::min(n, q);
-    if (getenv("DLR_DEBUG_MG"))
-        fprintf(stderr, "resident_per_cu: regs %d (alloc %d) static LDS %zu + %zu of %d, %d threads: %d per CU (query %d)\n",
-                a.numRegs, valloc, a.sharedSizeBytes, lds, cu_lds, threads, std::max(n, 0), q);
     return std::max(n, 0);
 }
 
@@ -4624,21 +4389,16 @@ bool grad_lds_mg_ok(const DevPm &cur, int64_t D, int64_t B, int phases, int fill
     form.phases = phases;
     form.fill = fill;
     if (!grad_lds_form_ok(form)) return false;
-    const bool db = grad_lds_db(form);
     // (wave v < the workgroup's pass-2 regions sums block x + grid * v)
-    const int64_t regions = (int64_t)grad_lds_rrows(fill, db) / kPmCap;
+    const int64_t regions = (int64_t)grad_lds_rrows(fill) / kPmCap;
     if (!(D > 0 && cur.groups <= 8 && cur.nblk == (B + kPmRows - 1) / kPmRows && cur.nblk <= grid * regions &&
           (int64_t)phases * fill * 4096 >= B))
         return false;
-    static int cap[64][2][9] = {};  // per device, form and fill (cached: the check runs every step)
+    static int cap[64][9] = {};  // per device and fill (cached: the check runs every step)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
-    int &c = cap[dev][db][fill];
-    if (c == 0) c = resident_grid(grad_lds_mg_fn(fill, db), kGradWaves * kWave, grad_lds_pm_lds(fill, db));
-    static const bool debug = getenv("DLR_DEBUG_MG") != nullptr;  // (checked every step)
-    if (debug)
-        fprintf(stderr, "grad_lds_mg_ok: dev %d fill %d db %d resident %d cus %d grid %lld mgrid %lld\n", dev, fill,
-                (int)db, c, device_cus(), (long long)grid, (long long)grad_lds_mg_grid(cur.nblk, grid));
+    int &c = cap[dev][fill];
+    if (c == 0) c = resident_grid(grad_lds_mg_fn(fill), kGradWaves * kWave, grad_lds_pm_lds(fill));
     return c > 0 && grad_lds_mg_grid(cur.nblk, grid) <= c;
 }
 
@@ -4658,25 +4418,15 @@ hipError_t launch_grad_lds_pm(const DevPcsc &pc, int64_t D, int64_t B, const flo
     const float Bf = (float)B;
     const double Bd = (double)B;
     const int fill = pc.fill;
-    const bool db = grad_lds_db(pc);
-    const size_t lds = grad_lds_pm_lds(fill, db);
-    if (db) {
-        if (mg)
-            hipLaunchKernelGGL((k_grad_lds<4, true, false, true, true, true>), dim3(mgrid), blk, lds, s, pc, D, B,
-                               resid, w, nullptr, Bf, Bd, lr, C, next, p, *mg);
-        else
-            hipLaunchKernelGGL((k_grad_lds<4, true, false, true, false, true>), dim3(grid), blk, lds, s, pc, D, B,
-                               resid, w, nullptr, Bf, Bd, lr, C, next, p);
-        return hipGetLastError();
-    }
-#define DLR_GLP(F)                                                                                            \
-    case F:                                                                                                   \
-        if (mg)                                                                                               \
-            hipLaunchKernelGGL((k_grad_lds<F, true, false, true, true>), dim3(mgrid), blk, lds, s, pc, D, B,  \
-                               resid, w, nullptr, Bf, Bd, lr, C, next, p, *mg);                               \
-        else                                                                                                  \
-            hipLaunchKernelGGL((k_grad_lds<F, true, false, true>), dim3(grid), blk, lds, s, pc, D, B, resid,  \
-                               w, nullptr, Bf, Bd, lr, C, next, p);                                           \
+    const size_t lds = grad_lds_pm_lds(fill);
+#define DLR_GLP(F)                                                                                                \
+    case F:                                                                                                       \
+        if (mg)                                                                                                   \
+            hipLaunchKernelGGL((k_grad_lds<F, true, true, true>), dim3(mgrid), blk, lds, s, pc, D, B, resid, w,   \
+                               nullptr, Bf, Bd, lr, C, next, p, *mg);                                             \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_grad_lds<F, true, true>), dim3(grid), blk, lds, s, pc, D, B, resid, w, nullptr, \
+                               Bf, Bd, lr, C, next, p);                                                           \
         break;
     switch (fill) {
         DLR_GLP(1)
@@ -5067,11 +4817,7 @@ hipError_t launch_dense_grad(const DevDense &dd, int64_t first, int64_t B, const
     else                                                                                                            \
         hipLaunchKernelGGL((k_dense_grad_chain<false, R>), dim3(grid), dim3(256), ChainCfg<R>::kLds, s, dd, first,   \
                            B, resid, w, gout, Bf, Bd, lr, C);
-        if (dense_chain_rows() == 128) {
-            DLR_CH(128)
-        } else {
-            DLR_CH(256)
-        }
+        DLR_CH(256)  // (256 rows per staging slot; 128 measured no faster)
 #undef DLR_CH
         return hipGetLastError();
     }

@@ -49,7 +49,8 @@ SYMBOLS = [
     "dlr_init_weight", "dlr_format_model", "dlr_key_range",
     "dlr_get_unique_id", "dlr_create", "dlr_create_group", "dlr_comm_abort", "dlr_comm_info", "dlr_destroy", "dlr_last_error",
     "dlr_set_weights", "dlr_get_weights", "dlr_load_train", "dlr_load_test", "dlr_load_train_dense",
-    "dlr_load_test_dense", "dlr_set_residency", "dlr_train_residency", "dlr_set_summation_order",
+    "dlr_load_test_dense", "dlr_set_residency", "dlr_train_residency",
+    "dlr_tuning_default", "dlr_tuning_from_env", "dlr_set_tuning", "dlr_get_tuning", "dlr_set_summation_order",
     "dlr_summation_order",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
     "dlr_set_fault",
@@ -109,6 +110,39 @@ class DenseSpec(C.Structure):
     ]
 
 
+AUTO = -1  # DLR_AUTO: the engine's own choice
+
+
+class Tuning(C.Structure):
+    """dlr_tuning (include/distlr_amd.h): the loads' layout / kernel-form
+    choices, every field AUTO or forced.  Tuning.from_env() is what a load
+    uses unless Engine.set_tuning was called."""
+    _fields_ = [(n, C.c_int64) for n in (
+        "grad_layout", "product_margin", "pm_fused", "pm_in_gradient", "pm_split", "row_rounds",
+        "band_rows", "band_pipeline", "band_hot", "hot_stream", "hot_stream_max", "margin_hot",
+        "long_column", "long_piece", "long_sched",
+        "relabel", "relabel_tail", "relabel_rare", "unit_values",
+        "stream_coalesce", "stream_device_layout",
+        "dense_grad", "dense_ref", "dense_ref_lead")]
+
+    @classmethod
+    def default(cls, **fields) -> "Tuning":
+        t = cls()
+        lib.dlr_tuning_default(C.byref(t))
+        for k, v in fields.items():
+            setattr(t, k, v)
+        return t
+
+    @classmethod
+    def from_env(cls) -> "Tuning":
+        t = cls()
+        lib.dlr_tuning_from_env(C.byref(t))
+        return t
+
+    def as_dict(self) -> dict:
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
 def _sig(name, res, *args):
     f = getattr(lib, name)
     f.restype = res
@@ -164,6 +198,10 @@ _sig("dlr_server_apply", C.c_int, P, P, C.c_int, i64, C.c_float, C.c_int)
 _sig("dlr_predict", C.c_int, P, C.POINTER(i64), C.POINTER(i64), C.POINTER(C.c_double))
 _sig("dlr_sync", C.c_int, P)
 _sig("dlr_set_fault", C.c_int, P, C.c_int)
+_sig("dlr_tuning_default", None, P)
+_sig("dlr_tuning_from_env", None, P)
+_sig("dlr_set_tuning", C.c_int, P, P)
+_sig("dlr_get_tuning", C.c_int, P, P)
 _sig("dlr_timing", C.c_int, P, C.c_int)
 _sig("dlr_kernel_time", C.c_int, P, C.c_int, C.POINTER(C.c_double), C.POINTER(i64))
 _sig("dlr_stage_time", C.c_int, P, C.c_int, i64, i64, C.c_float, C.c_float, C.POINTER(C.c_double))
@@ -509,6 +547,16 @@ class Engine:
         self._c(lib.dlr_load_train_dense(self._h, ds.handle, batch_size, C.byref(nb)))
         self._train_src = ds  # a streamed shard reads the host rows in place: keep them alive
         return nb.value
+
+    def set_tuning(self, tuning: "Tuning | None") -> None:
+        """The tuning of this engine's later loads (None: the environment's
+        at each load, the default; dlr_set_tuning)."""
+        self._c(lib.dlr_set_tuning(self._h, C.byref(tuning) if tuning is not None else None))
+
+    def get_tuning(self) -> "Tuning":
+        t = Tuning()
+        self._c(lib.dlr_get_tuning(self._h, C.byref(t)))
+        return t
 
     def set_residency(self, mode: int) -> None:
         """RESIDENCY_AUTO / _DEVICE / _STREAM for the next dense training

@@ -264,6 +264,65 @@ int dlr_load_test_dense(dlr_ctx *ctx, const dlr_dense *ds);
 int dlr_set_residency(dlr_ctx *ctx, int mode);
 int dlr_train_residency(dlr_ctx *ctx);
 
+/* TUNING of the loads (one struct instead of scattered switches).  The
+ * engine picks layouts and kernel forms itself at dlr_load_train* time;
+ * each field below can force one choice (DLR_AUTO = the engine's pick).
+ * None of them changes the arithmetic order (DLR_ORDER_REFERENCE stays
+ * bitwise the oracle's whatever is forced), only the layout and kernels
+ * doing it.  Unless dlr_set_tuning was called, every load takes the fields
+ * from the environment variable named beside each (dlr_tuning_from_env),
+ * so A/B runs need no code.
+ *   grad_layout          DLR_GRAD_KERNEL  classic|lds|touched -> DLR_LAYOUT_*
+ *   product_margin       DLR_PM           0 off; 1 required (the load fails
+ *                                         if the batches do not fit it)
+ *   pm_fused             DLR_PM_FUSED     0: the next batch's pass 1 in its own launch
+ *   pm_in_gradient       DLR_PM_MG        0: pass 2 in its own launch (no
+ *                                         one-launch step)
+ *   pm_split             DLR_PM_SPLIT     pass-1 workgroups per slice (separate pass 1)
+ *   row_rounds           DLR_GRAD_RT      0 never / 1 whenever the batch fits
+ *                                         the row-round gradient (auto: <= 2 rounds)
+ *   band_rows            DLR_BAND_ROWS    rows per band (power of two; 0 off)
+ *   band_pipeline        DLR_BAND_PIPE    0: margin, then the bands' gradient
+ *   band_hot             DLR_BAND_HOT     entries that make a column hot (0 none)
+ *   hot_stream           DLR_HOT_STREAM   0: hot columns in k_band_hot
+ *   hot_stream_max       DLR_HOT_STREAM_MAX  most streamed hot columns a batch (64)
+ *   margin_hot           DLR_MARGIN_HOT   0/1: the LDS hot-weight margin
+ *   long_column          DLR_LONG_COLUMN  FAST order: entries of a long column
+ *   long_piece           DLR_LONG_PIECE   FAST order: entries per long piece (63)
+ *   long_sched           DLR_LONG_SCHED   0: long chunks in chunk order
+ *   relabel              DLR_RELABEL      0/1: frequency order of the columns
+ *   relabel_tail         DLR_RELABEL_TAIL 0 id, 1, 2 (default) first occurrence
+ *   relabel_rare         DLR_RELABEL_RARE count below which a column is rare (16)
+ *   unit_values          DLR_UNIT_VALUES  0: keep the value array of an all-1 shard
+ *   stream_coalesce      DLR_STREAM_COALESCE  0: one copy per streamed array
+ *   stream_device_layout DLR_STREAM_DEVICE_LAYOUT  0: stream the host-built layout
+ *   dense_grad           DLR_DENSE_GRAD   FAST order: 0 chain, 1 blocked, 2 fused
+ *                                         (fused|blocked in the environment)
+ *   dense_ref            DLR_DENSE_REF    0/1: K6r, the one-launch dense step
+ *   dense_ref_lead       DLR_DENSE_REF_LEAD  K6r margin lead in slots (64; 0 none)
+ * Process-level switches stay in the environment (read at dlr_create*):
+ * DLR_RESIDENCY (dlr_set_residency's default), DLR_FORCE_COLLECTIVES (RCCL
+ * at one rank), DLR_LOOPBACK_SYNC and DLR_LOOPBACK_TIMEOUT_S (loopback
+ * group). */
+#define DLR_AUTO (-1)
+typedef struct dlr_tuning {
+    int64_t grad_layout, product_margin, pm_fused, pm_in_gradient, pm_split, row_rounds;
+    int64_t band_rows, band_pipeline, band_hot, hot_stream, hot_stream_max, margin_hot;
+    int64_t long_column, long_piece, long_sched;
+    int64_t relabel, relabel_tail, relabel_rare, unit_values;
+    int64_t stream_coalesce, stream_device_layout;
+    int64_t dense_grad, dense_ref, dense_ref_lead;
+} dlr_tuning;
+/* Every field DLR_AUTO. */
+void dlr_tuning_default(dlr_tuning *t);
+/* DLR_AUTO, then each field whose environment variable is set. */
+void dlr_tuning_from_env(dlr_tuning *t);
+/* The tuning of the context's later loads (t = NULL: back to the
+ * environment at each load, the default); dlr_get_tuning: the tuning the
+ * last load used (or the set one, before any load). */
+int dlr_set_tuning(dlr_ctx *ctx, const dlr_tuning *t);
+int dlr_get_tuning(dlr_ctx *ctx, dlr_tuning *t);
+
 /* Summation order of the next training shard's sums (applies at the next
  * dlr_load_train / dlr_load_train_dense; every rank must ask for the same
  * order, else the load fails on every rank).

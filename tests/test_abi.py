@@ -43,6 +43,30 @@ def test_python_binding_covers_header():
     assert sorted(distlr_amd.SYMBOLS) == declared_functions()
 
 
+def test_tuning_struct_matches_header_and_env(monkeypatch):
+    # dlr_tuning: the binding's fields are the header's, in order; every
+    # field AUTO by default; dlr_tuning_from_env parses the environment as
+    # the engine reads it (no GPU needed)
+    import distlr_amd
+    with open(os.path.join(ROOT, "include", "distlr_amd.h")) as f:
+        h = f.read()
+    body = re.search(r"typedef struct dlr_tuning \{(.*?)\} dlr_tuning;", h, re.S).group(1)
+    fields = re.findall(r"(\w+)(?=[,;])", re.sub(r"int64_t", "", body))
+    assert [n for n, _ in distlr_amd.Tuning._fields_] == fields
+    assert all(v == distlr_amd.AUTO for v in distlr_amd.Tuning.default().as_dict().values())
+    for k in [k for k in os.environ if k.startswith("DLR_")]:
+        monkeypatch.delenv(k)
+    monkeypatch.setenv("DLR_GRAD_KERNEL", "touched")
+    monkeypatch.setenv("DLR_PM", "1")
+    monkeypatch.setenv("DLR_PM_MG", "0")
+    monkeypatch.setenv("DLR_BAND_ROWS", "8192")
+    monkeypatch.setenv("DLR_DENSE_GRAD", "blocked")
+    t = distlr_amd.Tuning.from_env().as_dict()
+    assert t["grad_layout"] == distlr_amd.LAYOUT_TOUCHED and t["product_margin"] == 1
+    assert t["pm_in_gradient"] == 0 and t["band_rows"] == 8192 and t["dense_grad"] == 1
+    assert t["pm_fused"] == distlr_amd.AUTO and t["hot_stream"] == distlr_amd.AUTO
+
+
 def test_library_links_hip_and_rccl():
     out = subprocess.run(["readelf", "-d", LIB], check=True, capture_output=True, text=True).stdout
     assert "libamdhip64" in out and "librccl" in out

@@ -124,6 +124,37 @@ def test_auto_layout_choice():
     assert _layout_of(big, 1 << 22, 256) == dlr.LAYOUT_TOUCHED
 
 
+def test_tuning_struct_forces_layout_over_environment(monkeypatch):
+    # dlr_set_tuning: the struct, not the environment, decides the next
+    # load; set_tuning(None) goes back to the environment.  Each form is
+    # bitwise the oracle (tuning changes kernels, never the sums' order).
+    monkeypatch.setenv("DLR_GRAD_KERNEL", "lds")
+    D, B = 50000, 512
+    ds = dlr.Dataset.generate(2000, D, 20, value_mode=1, seed=3, stream=1)
+    rp, col, val, lab = ds.csr()
+    w0 = dlr.init_weight(D)
+    eng = dlr.Engine(D)
+    try:
+        for tuning, layout in [(dlr.Tuning.default(grad_layout=dlr.LAYOUT_CLASSIC), dlr.LAYOUT_CLASSIC),
+                               (dlr.Tuning.default(grad_layout=dlr.LAYOUT_TOUCHED), dlr.LAYOUT_TOUCHED),
+                               (None, dlr.LAYOUT_LDS)]:
+            eng.set_tuning(tuning)
+            eng.set_weights(w0)
+            nb = eng.load_train(ds, B)
+            assert eng.train_layout() == layout
+            assert eng.get_tuning().grad_layout == layout
+            w = w0.copy()
+            for b in range(nb):
+                eng.train_step(b, 0.2, 1.0)
+                g = oracle.grad_csr((rp, col, val), lab, oracle.batch_rows(len(lab), B, b), w)
+                oracle.server_update(w, [g], 0.2)
+            assert_same_weights(eng.get_weights(), w)
+        with pytest.raises(dlr.DLRError):
+            eng.set_tuning(dlr.Tuning.default(band_rows=3000))  # not a power of two
+    finally:
+        eng.close()
+
+
 def test_c5_shape_touched_steps():
     # BASELINE C5: 2^28 features (1 GiB of weights), 10 nnz/row, B = 1,024;
     # every step also applies the dense L2 term to all 2^28 weights.

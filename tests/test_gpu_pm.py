@@ -386,16 +386,13 @@ def test_pm_row_round_gradient(monkeypatch, rt, B):
         eng.close()
 
 
-@pytest.mark.parametrize("db", ["0", "1"])
 @pytest.mark.parametrize("B", [20000, 65536])
-def test_pm_margin_in_gradient_launch(monkeypatch, B, db):
+def test_pm_margin_in_gradient_launch(monkeypatch, B):
     # Pass 2 inside the fused gradient's launch (dlr_train_product_margin 3,
     # k_grad_lds MG): ragged rows of 0..64 entries (empty rows, whole empty
     # 64-row blocks), a wrapping last batch, steps out of order and repeated,
     # set_weights between steps (the products are re-formed: a guess missed)
-    # -- bitwise the separate pass 2 (DLR_PM_MG=0) and the oracle.  db "1":
-    # the double-buffered 16,384-row phases (k_grad_lds DB: 2 and 4 phases).
-    monkeypatch.setenv("DLR_GRAD_DB", db)
+    # -- bitwise the separate pass 2 (DLR_PM_MG=0) and the oracle.
     D = 1 << 20
     rng = np.random.default_rng(21)
     n = 150_000
