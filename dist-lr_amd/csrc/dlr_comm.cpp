@@ -31,10 +31,15 @@ bool nccl_ok(ncclResult_t r, const char *what, std::string &err) {
 
 // ------------------------------------------------------------------ RCCL
 
+// rec (tests, make_rccl_recorder): no communicator -- every RCCL call the
+// transport would make is appended to *rec as a line instead (the calls'
+// arguments as RCCL would get them: counts, peers, buffer offsets in words).
 class RcclComm final : public Comm {
 public:
-    RcclComm(ncclComm_t c, int world, int rank) : comm_(c), world_(world), rank_(rank) {}
+    RcclComm(ncclComm_t c, int world, int rank, std::string *rec = nullptr)
+        : comm_(c), world_(world), rank_(rank), rec_(rec) {}
     ~RcclComm() override {
+        if (rec_) return;
         if (abort_req_.load())
             abort_now();
         else
@@ -68,14 +73,17 @@ public:
     const char *kind() const override { return "rccl"; }
     bool all_reduce_i64(int64_t *d, size_t n, bool max, hipStream_t s, std::string &err) override {
         if (flagged(err)) return false;
+        if (rec_) return log("ncclAllReduce int64 count=" + std::to_string(n) + (max ? " max" : " sum"));
         return nccl_ok(ncclAllReduce(d, d, n, ncclInt64, max ? ncclMax : ncclSum, comm_, s), "ncclAllReduce", err);
     }
     bool all_gather(const void *send, void *recv, size_t words, hipStream_t s, std::string &err) override {
         if (flagged(err)) return false;
+        if (rec_) return log("ncclAllGather uint32 count=" + std::to_string(words));
         return nccl_ok(ncclAllGather(send, recv, words, ncclUint32, comm_, s), "ncclAllGather", err);
     }
     bool all_to_all(const void *send, void *recv, size_t words, hipStream_t s, std::string &err) override {
         if (flagged(err)) return false;
+        if (rec_) return log("ncclAllToAll uint32 count=" + std::to_string(words));
         return nccl_ok(ncclAllToAll(send, recv, words, ncclUint32, comm_, s), "ncclAllToAll", err);
     }
     bool all_gather_part(void *buf, size_t chunk, size_t off, size_t count, hipStream_t s,
@@ -84,6 +92,17 @@ public:
         if (world_ == 1 || count == 0) return true;
         // point to point: the piece of every peer's block, strided by chunk
         uint32_t *b = static_cast<uint32_t *>(buf);
+        if (rec_) {
+            log("ncclGroupStart");
+            for (int q = 0; q < world_; ++q) {
+                if (q == rank_) continue;
+                log("ncclSend uint32 count=" + std::to_string(count) + " peer=" + std::to_string(q) +
+                    " at=" + std::to_string((size_t)rank_ * chunk + off));
+                log("ncclRecv uint32 count=" + std::to_string(count) + " peer=" + std::to_string(q) +
+                    " at=" + std::to_string((size_t)q * chunk + off));
+            }
+            return log("ncclGroupEnd");
+        }
         if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
         bool ok = true;
         for (int q = 0; q < world_ && ok; ++q) {
@@ -100,6 +119,11 @@ public:
     }
 
 private:
+    bool log(const std::string &line) {
+        *rec_ += line;
+        *rec_ += '\n';
+        return true;
+    }
     // the driving thread: a flagged communicator is aborted, the call fails
     bool flagged(std::string &err) {
         if (!abort_req_.load()) return false;
@@ -114,12 +138,29 @@ private:
 
     ncclComm_t comm_;
     int world_, rank_;
+    std::string *rec_;
     std::atomic<bool> abort_req_{false}, aborted_{false};
     std::mutex mu_;
     std::string why_;
 };
 
 }  // namespace
+
+Comm *make_rccl_recorder(int world, int rank, std::string *log) { return new RcclComm(nullptr, world, rank, log); }
+
+bool issue(Comm &comm, const CollOp &op, const void *send, void *recv, hipStream_t s, std::string &err) {
+    switch (op.kind) {
+        case kCollAllToAll:
+            return comm.all_to_all(send, recv, (size_t)op.words, s, err);
+        case kCollAllGather:
+            return comm.all_gather(send, recv, (size_t)op.words, s, err);
+        case kCollAllGatherPart:
+            return comm.all_gather_part(recv, (size_t)op.words, (size_t)op.off, (size_t)op.count, s, err);
+        default:
+            err = "unknown collective in the exchange plan";
+            return false;
+    }
+}
 
 bool rccl_unique_id(void *out, std::string &err) {
     ncclUniqueId id;

@@ -25,6 +25,8 @@
 #include <cstdint>
 #include <string>
 
+#include "dlr_exchange.h"
+
 namespace dlr {
 
 class Comm {
@@ -68,9 +70,21 @@ public:
     }
 };
 
+// One collective of a step's plan (dlr_exchange.h exchange_plan) on a
+// transport -- how dlr_train_step and dlr_rccl_trace issue every step
+// collective: ALL_TO_ALL send -> recv (op.words per peer); ALL_GATHER send
+// (op.words) -> recv; ALL_GATHER_PART in place on recv (rank blocks op.words
+// apart, op.count words at op.off of each).
+bool issue(Comm &comm, const CollOp &op, const void *send, void *recv, hipStream_t s, std::string &err);
+
 // RCCL communicator for rank `rank` of `world` (unique_id: the 128-byte
 // ncclUniqueId from rank 0; ignored and generated locally when world == 1).
 Comm *make_rccl_comm(int world, int rank, const void *unique_id, std::string &err);
+
+// TEST ONLY: rank `rank` of a `world`-rank RCCL transport with no
+// communicator, whose every RCCL call is appended to *log as a line instead
+// (dlr_rccl_trace).  No GPU, no RCCL initialisation.
+Comm *make_rccl_recorder(int world, int rank, std::string *log);
 
 // ncclGetUniqueId into out (DLR_UNIQUE_ID_BYTES).
 bool rccl_unique_id(void *out, std::string &err);

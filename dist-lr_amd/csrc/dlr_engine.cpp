@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "dlr_comm.h"
+#include "dlr_exchange.h"
 #include "dlr_internal.h"
 #include "dlr_kernels.h"
 
@@ -370,6 +371,13 @@ int fail(dlr_ctx *c, int code, const std::string &msg) {
     } while (0)
 
 // A collective of the context's transport (dlr_comm.h); bool result.
+// One collective of the step's plan (dlr::issue)
+#define XCHGC(c, op, send, recv, s)                                                                       \
+    do {                                                                                                  \
+        std::string e_;                                                                                   \
+        if (!dlr::issue(*(c)->comm, *(op), (send), (recv), (s), e_))                                      \
+            return fail((c), DLR_E_RCCL, std::string((c)->comm->kind()) + " " + e_);                      \
+    } while (0)
 #define COMMC(c, expr)                                                                                  \
     do {                                                                                                \
         std::string e_;                                                                                 \
@@ -779,6 +787,28 @@ int coll_agree_pieced(dlr_ctx *c) {
     t.xpieced = v == -1;
     return DLR_OK;
 }
+
+// The collectives of this context's world > 1 step (dlr_exchange.h
+// exchange_plan: the same on every rank), consumed in order by
+// dlr_train_step -- each collective's sizes come from the plan, and a step
+// that would issue another sequence fails instead of leaving the peers in
+// an unmatched collective.
+struct StepPlan {
+    std::vector<dlr::CollOp> ops;
+    size_t k = 0;
+    const dlr::CollOp *next(int64_t kind) { return k < ops.size() && ops[k].kind == kind ? &ops[k++] : nullptr; }
+};
+StepPlan step_plan(const dlr_ctx *c) {
+    const TrainShard &t = c->train;
+    StepPlan p;
+    p.ops = t.touched ? dlr::exchange_plan(dlr::kXTouched, c->D, c->world, 0, c->xcap)
+                      : dlr::exchange_plan(dlr::kXKeyRange, c->D, c->world, t.xpieced ? t.xpieces : 0, 0);
+    return p;
+}
+#define PLANC(c, op)                                                                                \
+    do {                                                                                            \
+        if (!(op)) return fail((c), DLR_E_STATE, "dlr_train_step: the exchange left its plan"); \
+    } while (0)
 
 inline int64_t pid(const std::vector<int32_t> &p, int64_t j) { return p.empty() ? j : (int64_t)p[(size_t)j]; }
 
@@ -2439,6 +2469,83 @@ int build_pm(dlr_ctx *c, const CsrView &src, const std::vector<dlr::BatchSpan> &
 
 extern "C" {
 
+int dlr_exchange_plan(int protocol, int64_t D, int world, int pieces, int64_t cap, int64_t *ops, int max_ops) {
+    if (D <= 0 || world < 1 || world > dlr::kMaxRanks || pieces < 0 || pieces > kXPiecesMax || cap < 0 ||
+        max_ops < 0 || (max_ops > 0 && !ops) || (protocol != DLR_EXCHANGE_KEY_RANGE && protocol != DLR_EXCHANGE_TOUCHED))
+        return fail(nullptr, DLR_E_ARG, "dlr_exchange_plan: bad argument");
+    const std::vector<dlr::CollOp> plan = dlr::exchange_plan(
+        protocol == DLR_EXCHANGE_TOUCHED ? dlr::kXTouched : dlr::kXKeyRange, D, world, pieces, cap);
+    for (size_t k = 0; k < plan.size() && (int)k < max_ops; ++k) {
+        ops[4 * k] = plan[k].kind;
+        ops[4 * k + 1] = plan[k].words;
+        ops[4 * k + 2] = plan[k].off;
+        ops[4 * k + 3] = plan[k].count;
+    }
+    return (int)plan.size();
+}
+
+int dlr_merge_range(const float *recv, int world, int64_t chunk, int64_t n, float *w_own, float lr, int mode) {
+    if (!recv || !w_own || world < 1 || n < 0 || chunk < n || mode < 0 || mode > 2)
+        return fail(nullptr, DLR_E_ARG, "dlr_merge_range: bad argument");
+    for (int64_t i = 0; i < n; ++i) w_own[i] = dlr::server_apply(w_own[i], recv + i, chunk, world, lr, mode, false);
+    return DLR_OK;
+}
+
+int dlr_merge_touched(const uint32_t *lists, int world, int64_t cap, const float *batch_rows, float *w, int64_t D,
+                      float lr, float C, int mode) {
+    if (!lists || !batch_rows || !w || world < 1 || world > dlr::kMaxRanks || cap < 0 || D <= 0 || mode < 0 ||
+        mode > 2)
+        return fail(nullptr, DLR_E_ARG, "dlr_merge_touched: bad argument");
+    dlr::RankSizes rs{};
+    rs.W = world;
+    for (int r = 0; r < world; ++r) rs.Bf[r] = batch_rows[r];
+    const int64_t stride = 1 + 2 * cap;
+    for (int r = 0; r < world; ++r) {
+        const uint32_t n = lists[(int64_t)r * stride];
+        if ((int64_t)n > cap) return fail(nullptr, DLR_E_ARG, "dlr_merge_touched: count above cap");
+        for (uint32_t s = 0; s < n; ++s)
+            if (lists[(int64_t)r * stride + 1 + s] >= (uint64_t)D)
+                return fail(nullptr, DLR_E_ARG, "dlr_merge_touched: column out of range");
+    }
+    // the engine's order: the owners' new weights from the OLD weights
+    // (k_sparse_merge), the L2-only update of all D (k_dense_l2), then the
+    // owners' weights over it (k_scatter)
+    std::vector<std::pair<uint32_t, float>> out;
+    for (int r = 0; r < world; ++r)
+        for (int64_t s = 0; s < cap; ++s) {
+            uint32_t col;
+            float v;
+            if (dlr::sparse_merge_entry(lists, cap, stride, w, rs, lr, C, mode, r, s, &col, &v)) out.push_back({col, v});
+        }
+    for (int64_t j = 0; j < D; ++j) w[j] = dlr::l2_only_update(w[j], rs, lr, C, mode);
+    for (const auto &cv : out) w[cv.first] = cv.second;
+    return DLR_OK;
+}
+
+int64_t dlr_rccl_trace(int protocol, int64_t D, int world, int rank, int pieces, int64_t cap, int steps, char *out,
+                       int64_t size) {
+    if (D <= 0 || world < 1 || world > dlr::kMaxRanks || rank < 0 || rank >= world || pieces < 0 ||
+        pieces > kXPiecesMax || cap < 0 || steps < 0 || size < 0 || (size > 0 && !out) ||
+        (protocol != DLR_EXCHANGE_KEY_RANGE && protocol != DLR_EXCHANGE_TOUCHED))
+        return fail(nullptr, DLR_E_ARG, "dlr_rccl_trace: bad argument");
+    std::string log;
+    std::unique_ptr<dlr::Comm> comm(dlr::make_rccl_recorder(world, rank, &log));
+    const std::vector<dlr::CollOp> plan = dlr::exchange_plan(
+        protocol == DLR_EXCHANGE_TOUCHED ? dlr::kXTouched : dlr::kXKeyRange, D, world, pieces, cap);
+    for (int st = 0; st < steps; ++st)
+        for (const dlr::CollOp &op : plan) {
+            std::string err;
+            if (!dlr::issue(*comm, op, nullptr, nullptr, nullptr, err))
+                return fail(nullptr, DLR_E_RCCL, "dlr_rccl_trace: " + err);
+        }
+    if (size > 0) {
+        const size_t n = std::min<size_t>(log.size(), (size_t)size - 1);
+        memcpy(out, log.data(), n);
+        out[n] = '\0';
+    }
+    return (int64_t)log.size() + 1;
+}
+
 const char *dlr_last_error(const dlr_ctx *ctx) { return ctx ? ctx->err.c_str() : dlr::thread_error(); }
 
 int dlr_get_unique_id(void *id_out) {
@@ -2662,7 +2769,7 @@ static int auto_pieces(int64_t chunk) {
 // on the engine stream as their weights land (the exchange
 // overlapped with the next batch's margin).  Ends with the engine stream
 // past every piece.
-int exchange_overlapped(dlr_ctx *c, int64_t b) {
+int exchange_overlapped(dlr_ctx *c, int64_t b, StepPlan &xp) {
     TrainShard &t = c->train;
     if (!c->xstream) {
         HIPC(c, hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
@@ -2681,7 +2788,9 @@ int exchange_overlapped(dlr_ctx *c, int64_t b) {
     if (t.xpieces == 1) {
         // one piece: the plain in-place all-gather (one collective), then
         // pass 1 of every other slice
-        COMMC(c, all_gather(c->w + (int64_t)c->rank * c->chunk, c->w, (size_t)c->chunk, c->xstream, e_));
+        const dlr::CollOp *op = xp.next(dlr::kCollAllGather);
+        PLANC(c, op);
+        XCHGC(c, op, c->w + (int64_t)c->rank * op->words, c->w, c->xstream);
         HIPC(c, hipEventRecord(c->ev_xpiece[0], c->xstream));
         HIPC(c, hipStreamWaitEvent(c->stream, c->ev_xpiece[0], 0));
         HIPC(c, pass1(1));
@@ -2689,8 +2798,9 @@ int exchange_overlapped(dlr_ctx *c, int64_t b) {
         return DLR_OK;
     }
     for (int k = 0; k < t.xpieces; ++k) {
-        const int64_t off = k * t.xsub, cnt = std::max<int64_t>(0, std::min(t.xsub, c->chunk - off));
-        COMMC(c, all_gather_part(c->w, (size_t)c->chunk, (size_t)off, (size_t)cnt, c->xstream, e_));
+        const dlr::CollOp *op = xp.next(dlr::kCollAllGatherPart);
+        PLANC(c, op);
+        XCHGC(c, op, nullptr, c->w, c->xstream);
         HIPC(c, hipEventRecord(c->ev_xpiece[k], c->xstream));
         HIPC(c, hipStreamWaitEvent(c->stream, c->ev_xpiece[k], 0));
         HIPC(c, pass1(k + 1));
@@ -3519,16 +3629,21 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
         HIPC(c, band_step_pipelined(c, b, bt.rows, c->comm ? c->g : nullptr, lr, C, !c->comm));
         time_end(c, 1, t0);
         if (c->comm) {
+            StepPlan xp = step_plan(c);
+            const dlr::CollOp *a2a = xp.next(dlr::kCollAllToAll);
+            PLANC(c, a2a);
             time_begin(c, &t0);
-            COMMC(c, all_to_all(c->g, c->recv, (size_t)c->chunk, c->stream, e_));
+            XCHGC(c, a2a, c->g, c->recv, c->stream);
             time_end(c, 3, t0);
             int64_t kb, ke;
             dlr_key_range(c->D, c->world, c->rank, &kb, &ke);
             time_begin(c, &t0);
             HIPC(c, dlr::launch_merge_update(c->recv, c->world, c->chunk, ke - kb, c->w + kb, lr, mode, c->stream));
             time_end(c, 2, t0);
+            const dlr::CollOp *ag = xp.next(dlr::kCollAllGather);
+            PLANC(c, ag);
             time_begin(c, &t0);
-            COMMC(c, all_gather(c->w + (int64_t)c->rank * c->chunk, c->w, (size_t)c->chunk, c->stream, e_));
+            XCHGC(c, ag, c->w + (int64_t)c->rank * ag->words, c->w, c->stream);
             time_end(c, 3, t0);
         }
     } else if (c->train.touched) {
@@ -3556,8 +3671,12 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
             time_end(c, 1, t0);
             HIPC(c, hipMemsetD32Async(c->xsend, (int)n, 1, c->stream));
             HIPC(c, hipMemcpyAsync(c->xsend + 1, cols, (size_t)n * 4, hipMemcpyDeviceToDevice, c->stream));
+            StepPlan xp = step_plan(c);
+            const dlr::CollOp *ag = xp.next(dlr::kCollAllGather);
+            PLANC(c, ag);
+            if (ag->words != stride) return fail(c, DLR_E_STATE, "dlr_train_step: touched block size");
             time_begin(c, &t0);
-            COMMC(c, all_gather(c->xsend, c->xrecv, (size_t)stride, c->stream, e_));
+            XCHGC(c, ag, c->xsend, c->xrecv, c->stream);
             time_end(c, 3, t0);
             time_begin(c, &t0);
             HIPC(c, dlr::launch_sparse_merge(c->xrecv, cap, stride, c->w, c->rs, lr, C, mode, c->xcols, c->xnewv,
@@ -3574,8 +3693,11 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
         time_begin(c, &t0);
         HIPC(c, launch_gradient(c, b, bt.rows, c->g, lr, C, false));
         time_end(c, 1, t0);
+        StepPlan xp = step_plan(c);
+        const dlr::CollOp *a2a = xp.next(dlr::kCollAllToAll);
+        PLANC(c, a2a);
         time_begin(c, &t0);
-        COMMC(c, all_to_all(c->g, c->recv, (size_t)c->chunk, c->stream, e_));
+        XCHGC(c, a2a, c->g, c->recv, c->stream);
         time_end(c, 3, t0);
         int64_t kb, ke;
         dlr_key_range(c->D, c->world, c->rank, &kb, &ke);
@@ -3585,10 +3707,12 @@ int dlr_train_step(dlr_ctx *c, int64_t b, float lr, float C, int mode) {
         time_begin(c, &t0);
         if (c->train.xpieced) {
             // (the exchange interval then includes the next batch's pass 1)
-            int rc = exchange_overlapped(c, b);
+            int rc = exchange_overlapped(c, b, xp);
             if (rc) return rc;
         } else {
-            COMMC(c, all_gather(c->w + (int64_t)c->rank * c->chunk, c->w, (size_t)c->chunk, c->stream, e_));
+            const dlr::CollOp *ag = xp.next(dlr::kCollAllGather);
+            PLANC(c, ag);
+            XCHGC(c, ag, c->w + (int64_t)c->rank * ag->words, c->w, c->stream);
         }
         time_end(c, 3, t0);
     }

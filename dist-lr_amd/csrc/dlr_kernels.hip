@@ -37,6 +37,7 @@
 #include <utility>
 
 #include "dlr_kernels.h"
+#include "dlr_exchange.h"
 
 namespace dlr {
 
@@ -2637,60 +2638,7 @@ __global__ __launch_bounds__(256) void k_band_finalize(const float *__restrict__
     }
 }
 
-// The server update of one weight given the W ranks' pushes g_r
-// (main.cc:57-84; modes as k_merge_update).  single: one rank, no merge
-// (w -= fl32(lr*g), main.cc:71/81 with W = 1).
-__device__ __forceinline__ float server_apply(float wj, const float *g, int W, float lr, int mode, bool single) {
-    if (single) {
-        const float step = lr * g[0];
-        return wj - step;
-    }
-    const float Wf = (float)W;
-    if (mode == 2) {
-        for (int r = 0; r < W; ++r) {
-            const float step = lr * g[r];
-            wj = wj - step;
-        }
-        return wj;
-    }
-    if (mode == 1) {
-        const float step = lr * g[W - 1];
-        return wj - step / Wf;
-    }
-    float m = 0.0f;
-    for (int r = 0; r < W; ++r) m = m + g[r];
-    const float step = lr * m;
-    return wj - step / Wf;
-}
-
-// The update of a weight no rank touched: every push is rank r's L2 term
-// l2_r = fl32(fl32(C*w)/(float)B_r) (server_apply with g_r = l2_r).
-__device__ __forceinline__ float l2_only_update(float wj, const RankSizes &rs, float lr, float C, int mode) {
-    const float cw = C * wj;
-    if (rs.W == 1) {
-        const float l2 = cw / rs.Bf[0];
-        const float step = lr * l2;
-        return wj - step;
-    }
-    const float Wf = (float)rs.W;
-    if (mode == 2) {
-        for (int r = 0; r < rs.W; ++r) {
-            const float l2 = cw / rs.Bf[r];
-            const float step = lr * l2;
-            wj = wj - step;
-        }
-        return wj;
-    }
-    if (mode == 1) {
-        const float l2 = cw / rs.Bf[rs.W - 1];
-        const float step = lr * l2;
-        return wj - step / Wf;
-    }
-    float m = 0.0f;
-    for (int r = 0; r < rs.W; ++r) m = m + cw / rs.Bf[r];
-    const float step = lr * m;
-    return wj - step / Wf;
-}
+// (server_apply, l2_only_update: dlr_exchange.h, shared with the host)
 
 // K4d: every weight gets the L2-only update of the W ranks; touched columns
 // are overwritten afterwards by K4s.  16-byte non-temporal loads and stores
@@ -2733,18 +2681,6 @@ __global__ __launch_bounds__(256) void k_scatter(float *__restrict__ w, const ui
     if (c != 0xFFFFFFFFu) w[c] = newv[s];
 }
 
-__device__ __forceinline__ int64_t find_col(const uint32_t *cols, int64_t n, uint32_t c) {
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (cols[mid] < c)
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    return (lo < n && cols[lo] == c) ? lo : -1;
-}
-
 // Sparse exchange merge (world > 1, touched layout).  The all-gathered
 // lists: rank r's block of `stride` words = [count | cols[cap] | g[cap]].
 // Entry (r, s) owns its column iff no lower rank touched it; the owner
@@ -2756,34 +2692,16 @@ __global__ __launch_bounds__(256) void k_sparse_merge(const uint32_t *__restrict
                                                       int mode, uint32_t *__restrict__ out_cols,
                                                       float *__restrict__ out_newv) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int W = rs.W;
-    if (idx >= (int64_t)W * cap) return;
+    if (idx >= (int64_t)rs.W * cap) return;
     const int r = (int)(idx / cap);
-    const int64_t s = idx - (int64_t)r * cap;
-    const uint32_t *blk = lists + (int64_t)r * stride;
-    const int64_t n = blk[0];
-    if (s >= n) {
+    uint32_t c;
+    float v;
+    if (sparse_merge_entry(lists, cap, stride, w, rs, lr, C, mode, r, idx - (int64_t)r * cap, &c, &v)) {
+        out_cols[idx] = c;
+        out_newv[idx] = v;
+    } else {
         out_cols[idx] = 0xFFFFFFFFu;
-        return;
     }
-    const uint32_t c = blk[1 + s];
-    for (int q = 0; q < r; ++q) {
-        const uint32_t *bq = lists + (int64_t)q * stride;
-        if (find_col(bq + 1, bq[0], c) >= 0) {
-            out_cols[idx] = 0xFFFFFFFFu;
-            return;
-        }
-    }
-    const float wj = w[c];
-    const float cw = C * wj;
-    float g[kMaxRanks];
-    for (int q = 0; q < W; ++q) {
-        const uint32_t *bq = lists + (int64_t)q * stride;
-        const int64_t k = q == r ? s : find_col(bq + 1, bq[0], c);
-        g[q] = k >= 0 ? __uint_as_float(bq[1 + cap + k]) : cw / rs.Bf[q];
-    }
-    out_cols[idx] = c;
-    out_newv[idx] = server_apply(wj, g, W, lr, mode, false);
 }
 
 // ---------------------------------------------------------------------------
@@ -4043,23 +3961,7 @@ __global__ __launch_bounds__(256) void k_merge_update(const float *__restrict__ 
                                                       int64_t n, float *__restrict__ w_own, float lr, int mode) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    float wi = w_own[i];
-    const float Wf = (float)W;
-    if (mode == 2) {  // async: each push applied in rank order (main.cc:80-82)
-        for (int r = 0; r < W; ++r) {
-            const float step = lr * recv[(int64_t)r * chunk + i];
-            wi = wi - step;
-        }
-    } else if (mode == 1) {  // sync as written: last push only (main.cc:71)
-        const float step = lr * recv[(int64_t)(W - 1) * chunk + i];
-        wi = wi - step / Wf;
-    } else {  // sync mean: merged = ((0 + g_0) + g_1) + ... (main.cc:59-65)
-        float m = 0.0f;
-        for (int r = 0; r < W; ++r) m = m + recv[(int64_t)r * chunk + i];
-        const float step = lr * m;
-        wi = wi - step / Wf;
-    }
-    w_own[i] = wi;
+    w_own[i] = server_apply(w_own[i], recv + i, chunk, W, lr, mode, false);
 }
 
 inline unsigned grid_for(int64_t n, int per_block) { return (unsigned)((n + per_block - 1) / per_block); }

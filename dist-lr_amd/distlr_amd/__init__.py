@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import numpy as np
 
@@ -47,6 +47,7 @@ SYMBOLS = [
     "dlr_dense_free",
     "dlr_num_batches", "dlr_batch_rows",
     "dlr_init_weight", "dlr_format_model", "dlr_key_range",
+    "dlr_exchange_plan", "dlr_merge_range", "dlr_merge_touched", "dlr_rccl_trace",
     "dlr_get_unique_id", "dlr_create", "dlr_create_group", "dlr_comm_abort", "dlr_comm_info", "dlr_destroy", "dlr_last_error",
     "dlr_set_weights", "dlr_get_weights", "dlr_load_train", "dlr_load_test", "dlr_load_train_dense",
     "dlr_load_test_dense", "dlr_set_residency", "dlr_train_residency",
@@ -180,6 +181,10 @@ _sig("dlr_batch_rows", C.c_int, i64, i64, i64, P)
 _sig("dlr_init_weight", C.c_int, C.c_int, P, i64)
 _sig("dlr_format_model", C.c_int, P, i64, C.c_char_p, i64, C.POINTER(i64))
 _sig("dlr_key_range", C.c_int, i64, C.c_int, C.c_int, C.POINTER(i64), C.POINTER(i64))
+_sig("dlr_exchange_plan", C.c_int, C.c_int, i64, C.c_int, C.c_int, i64, C.POINTER(i64), C.c_int)
+_sig("dlr_merge_range", C.c_int, P, C.c_int, i64, i64, P, C.c_float, C.c_int)
+_sig("dlr_merge_touched", C.c_int, P, C.c_int, i64, P, P, i64, C.c_float, C.c_float, C.c_int)
+_sig("dlr_rccl_trace", i64, C.c_int, i64, C.c_int, C.c_int, C.c_int, i64, C.c_int, C.c_char_p, i64)
 _sig("dlr_get_unique_id", C.c_int, P)
 _sig("dlr_create", C.c_int, C.c_int, C.c_int, C.c_int, P, i64, C.POINTER(P))
 _sig("dlr_create_group", C.c_int, C.c_int, C.c_int, i64, P)
@@ -472,6 +477,49 @@ def key_range(num_feature_dim: int, world: int, rank: int) -> Tuple[int, int]:
     b, e = i64(), i64()
     _check(lib.dlr_key_range(num_feature_dim, world, rank, C.byref(b), C.byref(e)))
     return b.value, e.value
+
+
+EXCHANGE_KEY_RANGE, EXCHANGE_TOUCHED = 0, 1
+COLL_ALL_TO_ALL, COLL_ALL_GATHER, COLL_ALL_GATHER_PART = 1, 2, 3
+
+
+def exchange_plan(protocol: int, num_feature_dim: int, world: int, pieces: int = 0,
+                  touched_cap: int = 0) -> List[Tuple[int, int, int, int]]:
+    """The collectives of one world > 1 step, in order, on every rank:
+    (kind, words, offset, count) each (dlr_exchange_plan)."""
+    ops = (i64 * (4 * 64))()
+    n = lib.dlr_exchange_plan(protocol, num_feature_dim, world, pieces, touched_cap, ops, 64)
+    _check(min(n, 0))
+    return [tuple(ops[4 * k:4 * k + 4]) for k in range(n)]
+
+
+def merge_range(recv: np.ndarray, w_own: np.ndarray, lr: float, mode: int) -> None:
+    """KVStoreDistServer::DataHandle on the owned keys, on the host, from the
+    kernels' own source (dlr_merge_range): recv is (world, chunk) fp32,
+    rank-major; w_own (n <= chunk) is updated in place."""
+    recv = np.ascontiguousarray(recv, dtype=np.float32)
+    assert w_own.dtype == np.float32 and w_own.flags.c_contiguous
+    _check(lib.dlr_merge_range(_ptr(recv), recv.shape[0], recv.shape[1], w_own.shape[0], _ptr(w_own), lr, mode))
+
+
+def merge_touched(lists: np.ndarray, cap: int, batch_rows, w: np.ndarray, lr: float, C_: float, mode: int) -> None:
+    """The touched-list exchange's update of all D weights on the host
+    (dlr_merge_touched): lists = (world, 1 + 2 * cap) uint32 blocks."""
+    lists = np.ascontiguousarray(lists, dtype=np.uint32)
+    br = np.ascontiguousarray(batch_rows, dtype=np.float32)
+    assert w.dtype == np.float32 and w.flags.c_contiguous
+    _check(lib.dlr_merge_touched(_ptr(lists), lists.shape[0], cap, _ptr(br), _ptr(w), w.shape[0], lr, C_, mode))
+
+
+def rccl_trace(protocol: int, num_feature_dim: int, world: int, rank: int, pieces: int = 0,
+               touched_cap: int = 0, steps: int = 1) -> List[str]:
+    """The RCCL calls rank `rank` makes for `steps` steps, recorded instead
+    of made (dlr_rccl_trace; no GPU)."""
+    n = lib.dlr_rccl_trace(protocol, num_feature_dim, world, rank, pieces, touched_cap, steps, None, 0)
+    _check(min(n, 0))
+    buf = C.create_string_buffer(int(n))
+    _check(min(lib.dlr_rccl_trace(protocol, num_feature_dim, world, rank, pieces, touched_cap, steps, buf, n), 0))
+    return buf.value.decode().splitlines()
 
 
 def get_unique_id() -> bytes:

@@ -176,6 +176,49 @@ int dlr_format_model(const float *w, int64_t num_feature_dim, char *out, int64_t
  * empty). */
 int dlr_key_range(int64_t num_feature_dim, int world, int rank, int64_t *begin, int64_t *end);
 
+/* The collectives ONE world > 1 training step issues, in order -- the same
+ * on every rank (dlr_train_step issues exactly these, through RCCL or the
+ * loopback group; replaces KVWorker::Push/Pull, lr.cc:116-132).
+ * protocol DLR_EXCHANGE_KEY_RANGE (dense, LDS, classic and band layouts:
+ * ALL_TO_ALL of every rank's pushed key ranges, the owned range merged,
+ * then ALL_GATHER -- or, pieces > 1, ALL_GATHER_PART per piece -- of the
+ * merged ranges) or DLR_EXCHANGE_TOUCHED (huge D: ALL_GATHER of each rank's
+ * [count | cols | g] block of 1 + 2 * touched_cap words).  ops[4k .. 4k+3]
+ * = (kind, words, offset, count): ALL_TO_ALL / ALL_GATHER move `words` per
+ * rank; ALL_GATHER_PART moves words [offset, offset + count) of every
+ * rank's `words`-word block.  Returns the op count (at most max_ops are
+ * written) or < 0.  Host only. */
+#define DLR_EXCHANGE_KEY_RANGE 0
+#define DLR_EXCHANGE_TOUCHED 1
+#define DLR_COLL_ALL_TO_ALL 1
+#define DLR_COLL_ALL_GATHER 2
+#define DLR_COLL_ALL_GATHER_PART 3
+int dlr_exchange_plan(int protocol, int64_t num_feature_dim, int world, int pieces, int64_t touched_cap,
+                      int64_t *ops, int max_ops);
+/* The server side of the exchange on the HOST, from the same source as the
+ * kernels (dist-lr_amd/csrc/dlr_exchange.h), for transports other than this
+ * engine's (tests drive it over torch.distributed gloo).
+ * dlr_merge_range: KVStoreDistServer::DataHandle (main.cc:57-84) on the
+ * owned keys: w_own[i] updated from the world ranks' pushes recv[r * chunk
+ * + i], r = 0 .. world-1, in rank order (k_merge_update), i < n.
+ * dlr_merge_touched: the touched-list exchange's update of all D weights
+ * (k_sparse_merge, k_dense_l2, k_scatter): lists = the world all-gathered
+ * [count | cols[cap] | g bits[cap]] blocks (rank-major, 1 + 2 * cap uint32
+ * each), batch_rows[r] = rank r's batch size (its L2 term's divisor). */
+int dlr_merge_range(const float *recv, int world, int64_t chunk, int64_t n, float *w_own, float learning_rate,
+                    int mode);
+int dlr_merge_touched(const uint32_t *lists, int world, int64_t cap, const float *batch_rows, float *w,
+                      int64_t num_feature_dim, float learning_rate, float C, int mode);
+/* TEST ONLY (no GPU, no RCCL): the RCCL calls rank `rank` of `world` makes
+ * for `steps` training steps -- dlr_exchange_plan's collectives issued the
+ * way dlr_train_step issues them, through the RCCL transport with each RCCL
+ * call recorded as a text line (name, count, peer, buffer offset) instead
+ * of made.  Writes at most size bytes to out; returns the full length or
+ * < 0.  Every rank's trace must pair up with the others' (same
+ * collectives and counts; each ncclSend to q matched by q's ncclRecv). */
+int64_t dlr_rccl_trace(int protocol, int64_t num_feature_dim, int world, int rank, int pieces, int64_t touched_cap,
+                       int steps, char *out, int64_t size);
+
 /* ------------------------------------------------------------------ */
 /* Device engine (gfx950)                                              */
 /* ------------------------------------------------------------------ */
