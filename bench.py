@@ -390,7 +390,10 @@ def run_loopback(args):
     import distlr_amd as dlr  # noqa: F811
     W, D, B = args.loopback_ranks, args.features, args.batch
     t0 = time.perf_counter()
-    shards = [make_shard(args, args.rows, r + 1) for r in range(W)]
+    shards = []
+    for r in range(W):  # (a line per shard: a long generation is not a hang)
+        shards.append(make_shard(args, args.rows, r + 1))
+        log(f"loopback: shard {r + 1} of {W} generated ({time.perf_counter() - t0:.1f}s)")
     log(f"loopback: {W} shards of {args.rows} x {D} generated in {time.perf_counter() - t0:.1f}s")
     engines = dlr.Engine.create_group(D, W, 0)
     w0 = dlr.init_weight(D)
@@ -405,6 +408,7 @@ def run_loopback(args):
             eng.set_weights(w0)
             nb = eng.load_train_dense(shards[r], B) if args.kind == "dense" else eng.load_train(shards[r], B)
             shards[r].free()
+            log(f"loopback: rank {r} loaded ({time.perf_counter() - t0:.1f}s)")
             k = 0
 
             def steps(n, instrumented):
@@ -442,7 +446,9 @@ def run_loopback(args):
                 off = {"ms_per_step": round(el_off / args.steps * 1000.0, 5),
                        "exchange_us_per_step": per_step(kt_off["exchange"]),
                        "margin_us_per_step": per_step(kt_off["margin"])}
-            res[r] = {"ms_per_step": round(el_on / args.steps * 1000.0, 5), "overlap": bool(overlap),
+            cnt = eng.stage_counters()  # (since the load: every step above)
+            res[r] = {"counters": cnt, "steps_run": k,
+                      "ms_per_step": round(el_on / args.steps * 1000.0, 5), "overlap": bool(overlap),
                       "pieces": pieces, "exchange_us_per_step": per_step(kt_on["exchange"]),
                       "merge_us_per_step": per_step(kt_on["merge"]), "margin_us_per_step": per_step(kt_on["margin"]),
                       "gradient_us_per_step": per_step(kt_on["grad_update"]), "without_overlap": off,
@@ -476,6 +482,13 @@ def run_loopback(args):
         "margin_us_per_step": r0["margin_us_per_step"], "gradient_us_per_step": r0["gradient_us_per_step"],
         "overlap": r0["overlap"], "pieces": r0["pieces"], "without_overlap": r0["without_overlap"],
         "per_rank_exchange_us": [x["exchange_us_per_step"] for x in res],
+        # the in-launch hand-offs under the world > 1 stream set (dlr_stage_counters, every rank, all steps
+        # since the load): hot-chain give-ups must be 0
+        "counters": {"steps_per_rank": r0["steps_run"],
+                     "hot_chain_launches_per_step": round(r0["counters"]["hot_chain_launches"] / max(1, r0["steps_run"]), 3),
+                     "hot_giveups_all_ranks": sum(x["counters"]["hot_giveups"] for x in res),
+                     "cowait_serialised_all_ranks": sum(x["counters"]["cowait_serialised"] for x in res),
+                     "mg_demoted_all_ranks": sum(x["counters"]["mg_demoted"] for x in res)},
         "ranks_agree": len({x["weights_sha1"] for x in res}) == 1,
         "note": "the W ranks share one GPU (their compute is serialised on it); the collectives are "
                 "event-ordered device copies, so xGMI/RCCL latency is NOT in these numbers: the exchange's "
@@ -620,6 +633,8 @@ def run_rank(args):
     # Every rank holds the replicated weights after the same 2K (+W) steps:
     # their checksums must agree (and, with --dump-weights, the tests compare
     # them with the oracle's W-worker run).
+    counters = eng.stage_counters()  # since the load: the warmup and both timed passes
+    steps_run = args.warmup + 2 * args.steps
     w_fin = eng.get_weights()
     digest = hashlib.sha1(w_fin.tobytes()).hexdigest()
     if args.dump_weights:
@@ -782,6 +797,13 @@ def run_rank(args):
                 "weights_sha1": digest,
                 "ranks_agree": len(set(digests)) == 1,
             },
+            # the in-launch hand-offs (dlr_stage_counters over the warmup + both timed passes): hot-chain
+            # give-ups must be 0; cowait_serialised counts launches ordered behind another context's
+            "counters": {"steps": steps_run,
+                         "hot_chain_launches_per_step": round(counters["hot_chain_launches"] / steps_run, 3),
+                         "hot_giveups": counters["hot_giveups"],
+                         "cowait_serialised": counters["cowait_serialised"],
+                         "mg_demoted": counters["mg_demoted"]},
             "cpu_baseline": cpu,
             "cpu_baseline_build": cpu_build,
         }

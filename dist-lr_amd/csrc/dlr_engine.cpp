@@ -1193,6 +1193,8 @@ void build_bands(const std::vector<uint32_t> &cptr, const std::vector<RowT> &cro
 // far above the ~0.1-0.3 ms between flags when the margins run beside it,
 // far below the 250 ms error bound
 constexpr uint32_t kHsGiveUpTicks = 2000000;  // 20 ms at 100 MHz
+// bands of a step's first hot-chain launch (band_step_pipelined)
+constexpr int64_t kHsFirstGroup = 4;
 // rows of a window of the band-mode product margin (TrainShard::pmw): the
 // product margin's 1,024 blocks of 64 rows
 constexpr int64_t kPmWinRows = (int64_t)dlr::kPmMaxBlocks * dlr::kPmRows;
@@ -2276,7 +2278,7 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
     if (e == hipSuccess && hot) e = hipStreamWaitEvent(c->hstream, c->ev_bstart, 0);
     dlr::DevHotOut ho{};
     dlr::DevHotChain hc{};
-    int64_t hc_end = 1;  // the band after which the next chain launch is queued
+    int64_t hc_end = kHsFirstGroup;  // the band after which the next chain launch is queued
     if (hs) {
         ++t.hs_seq;
         hc = dlr::DevHotChain{t.hs_cols + t.hsco[bb], t.hs_seg + t.hsso[bb], t.hs_buf, t.hs_flag, nh, nbands,
@@ -2297,15 +2299,20 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
                          : dlr::launch_margin_residual(sub, c->w, c->resid + r0, c->stream);
         if (e == hipSuccess && hs) e = dlr::launch_flag_store(t.hs_flag + k, t.hs_seq, c->stream);
         // the hot chains of bands [hc.b1, k + 1), queued after their margins
-        // (DevHotChain): groups of 1, 1, 2, 4, ... bands -- the first starts
-        // right after band 0's margin, and a later one waits behind the one
-        // before on hstream, so only a launch boundary per group is added
+        // (DevHotChain): two launches, the first bands', then the rest's
+        // after the last margin.  The host queues a band's launches ~4x
+        // faster than the GPU runs its margin, and a chain adds a band ~3x
+        // slower than the margins make one: the first launch is queued before
+        // band 0's margin ends and the second long before the first's chains
+        // end -- one launch boundary a step (C3: 5.78 ms; geometric groups,
+        // 6 launches: 5.95 ms, each boundary a sync of chains of unequal
+        // band lengths)
         if (e == hipSuccess && hs && (k + 1 == hc_end || k + 1 == nbands)) {
             hc.b0 = hc.b1;
             hc.b1 = k + 1;
             e = dlr::launch_hot_chain(hc, t.gacc, c->hstream);
             ++c->hcount[DLR_COUNT_HOT_CHAIN_LAUNCHES];
-            hc_end = 2 * (k + 1);
+            hc_end = nbands;
         }
         if (e == hipSuccess) e = hipEventRecord(c->ev_band[(size_t)k], c->stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(c->gstream, c->ev_band[(size_t)k], 0);

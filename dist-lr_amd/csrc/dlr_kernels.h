@@ -292,7 +292,7 @@ hipError_t launch_flag_store(uint32_t *flag, uint32_t seq, hipStream_t s);
 // stored to gacc[cols[h]] by the launch that adds the last band.  seg: per
 // (column h, band s) the segment's (start, count) in buf, h-major.
 // The engine queues the launch for bands [b0, b1) after the margin of band
-// b1 - 1 (geometric groups: 1, 1, 2, 4, ... bands), so the flags a launch
+// b1 - 1 (two launches: the first bands', then the rest), so the flags a launch
 // waits on come from margins queued BEFORE it: beside it on another
 // hardware queue, or ahead of it when the streams share one.  A flag not
 // up within `giveup` ticks (100 MHz) ends a launch that is not the last

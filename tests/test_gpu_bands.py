@@ -423,14 +423,9 @@ def test_hot_stream_valued_and_ragged_bands():
 
 
 def _chain_launches(nbands):
-    # k_hot_chain launches per step: one after the margins of bands 1, 2,
-    # 4, 8, ... and of the last band (DevHotChain)
-    n, end = 0, 1
-    for k in range(1, nbands + 1):
-        if k == end or k == nbands:
-            n += 1
-            end = 2 * k
-    return n
+    # k_hot_chain launches per step: one after the margins of band 4 (the
+    # first four bands'), one after the last margin (DevHotChain)
+    return 1 if nbands <= 4 else 2
 
 
 def test_hot_stream_serialised_kernels_no_giveup(tmp_path):
