@@ -112,8 +112,13 @@ struct TrainShard {
     // pass 2 per window; the weights do not change inside the step); the
     // DevPm arrays are the windows', window w of batch b at index
     // pmw_first[b] + w
+    // pmw_views: every window's DevPm (device memory, for the multi-window
+    // launches); pm_p then holds pmw_slots windows' products, pm_pstride
+    // floats apart (a band's windows: one pass-1 and one pass-2 launch)
     bool pmw = false;
     std::vector<int64_t> pmw_first;
+    dlr::DevPm *pmw_views = nullptr;
+    int64_t pmw_slots = 1, pm_pstride = 0;
     uint32_t *pm_cnt = nullptr;
     uint32_t pm_gen = 0;
     int64_t pmS = 0;
@@ -588,7 +593,7 @@ void free_train(dlr_ctx *c) {
                     (void *)t.lpslot, (void *)t.lpws, (void *)t.lprow, (void *)t.lpval, (void *)t.pm_lbeg,
                     (void *)t.pm_list, (void *)t.pm_pofs, (void *)t.pm_rg, (void *)t.pm_qoff, (void *)t.pm_val,
                     (void *)t.pm_p, (void *)t.pm_qs, (void *)t.xslices, (void *)t.rt_gq, (void *)t.rt_val,
-                    (void *)t.rt_cend, (void *)t.dref_sync, (void *)t.pm_cnt})
+                    (void *)t.rt_cend, (void *)t.dref_sync, (void *)t.pm_cnt, (void *)t.pmw_views})
         dev_free(c, p);
     t = TrainShard();
     c->pm_ready = -1;
@@ -2017,15 +2022,15 @@ hipError_t launch_pm_windows(dlr_ctx *c, int64_t b, int64_t r0, int64_t r1) {
     const dlr::DevBatch all = batch_view(c, b);
     r1 = std::min(r1, all.rows);
     hipError_t e = hipSuccess;
-    for (int64_t wr0 = r0; e == hipSuccess && wr0 < r1; wr0 += kPmWinRows) {
+    for (int64_t wr0 = r0; e == hipSuccess && wr0 < r1; wr0 += t.pmw_slots * kPmWinRows) {
         const int64_t wi = t.pmw_first[(size_t)b] + wr0 / kPmWinRows;
         dlr::DevBatch sub = all;
         sub.row_ptr = all.row_ptr + wr0;
         sub.label = all.label + wr0;
-        sub.rows = std::min(kPmWinRows, all.rows - wr0);
-        const dlr::DevPm pm = pm_view(c, wi);
-        e = dlr::launch_pm_products(pm, c->w, c->D, t.pm_p, c->stream);
-        if (e == hipSuccess) e = dlr::launch_pm_margin(pm, sub, t.pm_p, c->resid + wr0, c->stream);
+        sub.rows = std::min(t.pmw_slots * kPmWinRows, r1 - wr0);
+        const int64_t nwin = (sub.rows + kPmWinRows - 1) / kPmWinRows;
+        e = dlr::launch_pm_windows(t.pmw_views + wi, pm_view(c, wi), nwin, sub, c->w, c->D, t.pm_p, t.pm_pstride,
+                                   c->resid + wr0, c->stream);
     }
     return e;
 }
@@ -2341,9 +2346,10 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
 // batch's), or the 65,536-row WINDOWS of band-mode batches (TrainShard::
 // pmw) -- uploaded back to back; built = false (nothing uploaded) when a
 // span does not fit them or they would not leave the residency headroom
-// (force: DLR_PM=1, that is an error).
+// (force: DLR_PM=1, that is an error).  slots: spans whose products pm_p
+// holds at once (TrainShard::pm_pstride apart).
 int build_pm(dlr_ctx *c, const CsrView &src, const std::vector<dlr::BatchSpan> &spans, bool allow_rt, bool force,
-             int nthreads, int64_t &resid_need, int64_t &csc_bytes, bool &built) {
+             int nthreads, int64_t &resid_need, int64_t &csc_bytes, bool &built, int64_t slots = 1) {
     TrainShard &t = c->train;
     const int64_t ns = (int64_t)spans.size(), D = c->D;
     const int64_t S = (D + dlr::kPmSlice - 1) / dlr::kPmSlice;
@@ -2463,10 +2469,12 @@ int build_pm(dlr_ctx *c, const CsrView &src, const std::vector<dlr::BatchSpan> &
                 std::vector<uint16_t>().swap(q.cend);
             }
         }
-        if ((rc = dev_alloc(c, (void **)&t.pm_p, (size_t)(pcap + 64) * 4))) return rc;
-        HIPC(c, hipMemsetAsync(t.pm_p, 0, (size_t)(pcap + 64) * 4, c->stream));
+        t.pm_pstride = (pcap + 64 + 63) / 64 * 64;
+        const size_t pbytes = (size_t)t.pm_pstride * (size_t)std::max<int64_t>(1, slots) * 4;
+        if ((rc = dev_alloc(c, (void **)&t.pm_p, pbytes))) return rc;
+        HIPC(c, hipMemsetAsync(t.pm_p, 0, pbytes, c->stream));
         csc_bytes += (int64_t)(lbeg_n * 4 + t.pmo_list.back() * (t.unit ? 2 : 6) +
-                               t.pmo_pofs.back() * 4 + t.pmo_rg.back() * 8 + t.pmo_qs.back() * 2 + pcap * 4);
+                               t.pmo_pofs.back() * 4 + t.pmo_rg.back() * 8 + t.pmo_qs.back() * 2 + t.pm_pstride * std::max<int64_t>(1, slots) * 4);
         built = true;
     }
     return DLR_OK;
@@ -3384,10 +3392,18 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 t.pmw_first[(size_t)b + 1] = (int64_t)spans.size();
             }
             bool built = false;
+            // a band's windows share a launch (launch_pm_windows)
+            const int64_t slots = std::min<int64_t>(16, std::max<int64_t>(1, ((int64_t)1 << shift) / kPmWinRows));
             if ((rc = build_pm(c, src, spans, false, pme == 1, nthreads, resid_need, csc_bytes,
-                               built)))
+                               built, slots)))
                 return rc;
             t.pmw = built;
+            if (built) {
+                t.pmw_slots = slots;
+                std::vector<dlr::DevPm> views(spans.size());
+                for (size_t i = 0; i < spans.size(); ++i) views[i] = pm_view(c, (int64_t)i);
+                if ((rc = upload(c, &t.pmw_views, views.data(), views.size(), 0))) return rc;
+            }
             if (!built && pme == 1)
                 return fail(c, DLR_E_ARG, "dlr_load_train: DLR_PM=1 but the batches' windows do not fit the product margin");
         }

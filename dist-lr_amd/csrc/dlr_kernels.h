@@ -368,6 +368,13 @@ hipError_t launch_grad_lds(const DevPcsc &pc, int64_t D, int64_t B, const float 
 hipError_t launch_pm_products(const DevPm &pm, const float *w, int64_t D, float *p, hipStream_t s,
                               const uint32_t *slices = nullptr, int64_t nslices = 0);
 hipError_t launch_pm_margin(const DevPm &pm, const DevBatch &bt, const float *p, float *resid, hipStream_t s);
+// Pass 1 + pass 2 of nwin consecutive windows of kPmMaxBlocks * kPmRows rows
+// (band mode, TrainShard::pmw) in two launches: views[v] is window v's DevPm
+// (device memory), pm0 a host copy of views[0] (S, split, groups: the same
+// for every window), bt the windows' rows from the first's, window v's
+// products at p + v * pstride (pstride a multiple of 64 floats).
+hipError_t launch_pm_windows(const DevPm *views, const DevPm &pm0, int64_t nwin, const DevBatch &bt,
+                             const float *w, int64_t D, float *p, int64_t pstride, float *resid, hipStream_t s);
 // k_grad_lds (fused update) that also forms the products of the NEXT batch
 // (next: its product-margin view) from the weights it has just updated:
 // pass 1 for free in the gradient's workgroups (slice s = workgroup s).

@@ -1088,12 +1088,10 @@ struct PmPass1 {
 // adjacent (a region's chunks are ordered by XCD).
 // sl (optional): the slices to form, nsl of them (the exchange overlap forms
 // the slices whose weights have landed, group by group).
-__global__ __launch_bounds__(1024) void k_pm_products(DevPm pm, const float *__restrict__ w, int64_t D,
-                                                      float *__restrict__ p, const uint32_t *__restrict__ sl,
-                                                      int64_t nsl) {
-    __shared__ __attribute__((aligned(16))) float s_w[kPmSlice];
-    __shared__ uint32_t s_po[kPmMaxBlocks];
-    const int x = blockIdx.x, xcd = x & 7, k = x >> 3;
+__device__ __forceinline__ void pm_products_wg(const DevPm &pm, int x, const float *__restrict__ w, int64_t D,
+                                               float *__restrict__ p, const uint32_t *__restrict__ sl, int64_t nsl,
+                                               float *s_w, uint32_t *s_po) {
+    const int xcd = x & 7, k = x >> 3;
     const int i = (k / pm.split) * 8 + xcd, part = k % pm.split;
     if (i >= (sl ? nsl : pm.S)) return;  // whole workgroup
     const int s = sl ? (int)sl[i] : i;
@@ -1107,6 +1105,31 @@ __global__ __launch_bounds__(1024) void k_pm_products(DevPm pm, const float *__r
     pp.stage_offsets(s_po);
     __syncthreads();
     pp.store(pm, s_w, s_po, p);
+}
+__global__ __launch_bounds__(1024) void k_pm_products(DevPm pm, const float *__restrict__ w, int64_t D,
+                                                      float *__restrict__ p, const uint32_t *__restrict__ sl,
+                                                      int64_t nsl) {
+    __shared__ __attribute__((aligned(16))) float s_w[kPmSlice];
+    __shared__ uint32_t s_po[kPmMaxBlocks];
+    pm_products_wg(pm, blockIdx.x, w, D, p, sl, nsl, s_w, s_po);
+}
+
+// Pass 1 of several product-margin WINDOWS in one launch (band mode,
+// TrainShard::pmw: the weights are fixed for the whole step): window v's
+// workgroups are [v * G, (v + 1) * G), G = the one-window grid (a multiple
+// of 8, so k_pm_products' XCD mapping holds inside every window and each
+// XCD's L2 serves the same 1/8 of w for all of them); window v's products go
+// to p + v * pstride.  One launch instead of one per window: the windows'
+// 17 us launches were latency-bound (a thread's dozen entries in one round
+// trip), a band's 8 at once stream.
+__global__ __launch_bounds__(1024) void k_pm_products_win(const DevPm *__restrict__ views, int64_t G,
+                                                          const float *__restrict__ w, int64_t D,
+                                                          float *__restrict__ p, int64_t pstride) {
+    __shared__ __attribute__((aligned(16))) float s_w[kPmSlice];
+    __shared__ uint32_t s_po[kPmMaxBlocks];
+    const int64_t v = blockIdx.x / G;
+    const DevPm pm = views[v];
+    pm_products_wg(pm, (int)(blockIdx.x - v * G), w, D, p + v * pstride, nullptr, 0, s_w, s_po);
 }
 
 // Pass 2 of block blk (one wave; lane l owns row 64 blk + l of bt) in the
@@ -1183,6 +1206,28 @@ __global__ __launch_bounds__(256) void k_pm_margin(DevPm pm, DevBatch bt, const 
     const int64_t blk = (int64_t)blockIdx.x * 4 + wv;
     if (blk * kPmRows >= bt.rows) return;  // wave-uniform
     pm_rowsum<QG, false>(pm, bt, p, resid, blk, s_reg[wv], lane);
+}
+
+// Pass 2 of several windows in one launch (k_pm_products_win's): bt is the
+// windows' rows from the first's, window v = rows [v * kPmWinRows, + its
+// rows) with its products at p + v * pstride; G = kPmMaxBlocks / 4
+// workgroups a window (a wave per 64-row block).
+template <int QG>
+__global__ __launch_bounds__(256) void k_pm_margin_win(const DevPm *__restrict__ views, DevBatch bt,
+                                                       const float *__restrict__ p, int64_t pstride,
+                                                       float *__restrict__ resid) {
+    __shared__ __attribute__((aligned(16))) float s_reg[4][kPmCap];
+    constexpr int64_t G = kPmMaxBlocks / 4, kWinRows = (int64_t)kPmMaxBlocks * kPmRows;
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    const int64_t v = blockIdx.x / G;
+    const int64_t blk = (blockIdx.x - v * G) * 4 + wv;
+    DevBatch sub = bt;
+    sub.row_ptr = bt.row_ptr + v * kWinRows;
+    sub.label = bt.label + v * kWinRows;
+    sub.rows = min(kWinRows, bt.rows - v * kWinRows);
+    if (blk * kPmRows >= sub.rows) return;  // wave-uniform
+    const DevPm pm = views[v];
+    pm_rowsum<QG, false>(pm, sub, p + v * pstride, resid + v * kWinRows, blk, s_reg[wv], lane);
 }
 
 // PM (with FUSED): after the update, form the NEXT batch's products of this
@@ -4178,6 +4223,28 @@ hipError_t launch_pm_products(const DevPm &pm, const float *w, int64_t D, float 
     if (pm.nblk > kPmMaxBlocks || pm.split < 1) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)(((n + 7) / 8) * 8 * pm.split);
     hipLaunchKernelGGL(k_pm_products, dim3(grid), dim3(1024), 0, s, pm, w, D, p, slices, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_pm_windows(const DevPm *views, const DevPm &pm0, int64_t nwin, const DevBatch &bt,
+                             const float *w, int64_t D, float *p, int64_t pstride, float *resid, hipStream_t s) {
+    constexpr int64_t kWinRows = (int64_t)kPmMaxBlocks * kPmRows;
+    if (nwin <= 0 || bt.rows <= 0) return hipSuccess;
+    if (pm0.split < 1 || pstride % 64 != 0 || (nwin - 1) * kWinRows >= bt.rows || nwin * kWinRows < bt.rows)
+        return hipErrorInvalidValue;
+    const int64_t G = ((pm0.S + 7) / 8) * 8 * pm0.split;
+    hipLaunchKernelGGL(k_pm_products_win, dim3((unsigned)(nwin * G)), dim3(1024), 0, s, views, G, w, D, p, pstride);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const dim3 grid((unsigned)(nwin * (kPmMaxBlocks / 4)));
+    if (pm0.groups <= 4)
+        hipLaunchKernelGGL((k_pm_margin_win<4>), grid, dim3(256), 0, s, views, bt, p, pstride, resid);
+    else if (pm0.groups <= 8)
+        hipLaunchKernelGGL((k_pm_margin_win<8>), grid, dim3(256), 0, s, views, bt, p, pstride, resid);
+    else if (pm0.groups <= kPmMaxGroups)
+        hipLaunchKernelGGL((k_pm_margin_win<kPmMaxGroups>), grid, dim3(256), 0, s, views, bt, p, pstride, resid);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -440,7 +440,7 @@ def test_pm_margin_in_gradient_launch(monkeypatch, B):
     assert_same_weights(got[-1], w)
 
 
-@pytest.mark.parametrize("band_rows", ["262144"])
+@pytest.mark.parametrize("band_rows", ["262144", "524288"])
 def test_pm_windows_full_shard_batch(monkeypatch, band_rows):
     # B = -1 over > 2^20 rows (band mode): the margin as
     # the product margin over 65,536-row windows -- pass 1 and pass 2 per
