@@ -1038,6 +1038,9 @@ void build_csc(const CsrView &ds, const std::vector<dlr::BatchSpan> &plan, int64
 // classic copy (whose column segments are already in row order) in
 // parallel over column ranges; `ws` gets each band's entry-balanced wave
 // schedule (as the classic one: <= 64 pairs, ~kWin entries per wave).
+// entries of a band wave's window (dlr_kernels.hip kWin): the schedule's
+// wave size
+constexpr int64_t kWinEntries = 1024;
 template <typename RowT>
 struct BandBuild {
     std::vector<uint32_t> cols, ptr, ws, hw;
@@ -1045,6 +1048,7 @@ struct BandBuild {
     std::vector<float> val;
     std::vector<TrainShard::Band> bands;
     std::vector<int64_t> bfirst;
+    int64_t max_pair = 0;  // entries of the longest (column, band) pair
 };
 
 template <typename RowT>
@@ -1157,8 +1161,9 @@ void build_bands(const std::vector<uint32_t> &cptr, const std::vector<RowT> &cro
             bool prev_hot = false;
             for (int64_t q = 0; q < p; ++q) {
                 const int64_t cq = (int64_t)pp[q + 1] - (int64_t)pp[q];
+                out.max_pair = std::max(out.max_pair, cq);
                 const bool hq = hot(q);
-                if (cols > 0 && (hq || prev_hot || cols == 64 * dlr::kBandPairsPerLane || acc + cq > 1024)) {
+                if (cols > 0 && (hq || prev_hot || cols == 64 * dlr::kBandPairsPerLane || acc + cq > kWinEntries)) {
                     out.ws.push_back((uint32_t)q);
                     acc = 0;
                     cols = 0;
@@ -3308,7 +3313,12 @@ int dlr_load_train(dlr_ctx *c, const dlr_dataset *ds, int64_t batch_size, int64_
                 hot_min = hot_stream_threshold(c, cptr, nb, D, hot_min);
             build_bands(cptr, crow, cval, t.coff, nb, D, t.B, shift, t.unit, nthreads, hot_min, bb);
             t.band_shift = shift;
-            t.band_longrun = long_min == 0;
+            // the software-pipelined band kernel only where a pair spans
+            // windows (REFERENCE order keeps long runs in the bands: C3's
+            // Zipf heads); with every wave one window (C2 at B = -1: ~25
+            // entries a pair) its prefetches of the next two windows are
+            // clamped re-reads -- 3x the loads, 2x the gathers
+            t.band_longrun = long_min == 0 && bb.max_pair > kWinEntries;
             t.bands = std::move(bb.bands);
             t.bfirst = std::move(bb.bfirst);
             if ((r = upload(c, &t.bcols, bb.cols.data(), bb.cols.size(), 64))) return r;
