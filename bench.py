@@ -112,6 +112,8 @@ def parse_args():
     ap.add_argument("--features", type=int, default=None)
     ap.add_argument("--nnz", type=int, default=None)
     ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--value-mode", type=int, default=None,
+                    help="override the config's values (0: unit, 1: 4-decimal fp32; Dataset.generate)")
     ap.add_argument("--lr", type=float, default=0.2)
     ap.add_argument("--xpieces", type=int, default=0,
                     help="N > 1: pieces of the overlapped all-gather (dlr_set_exchange_pieces; 0 = auto, "
@@ -144,7 +146,8 @@ def parse_args():
     for k in ("rows", "features", "nnz", "batch", "steps", "warmup"):
         if getattr(args, k) is None:
             setattr(args, k, cfg[k])
-    args.value_mode = cfg["value_mode"]
+    if args.value_mode is None:
+        args.value_mode = cfg["value_mode"]
     args.label = cfg["label"]
     args.kind = cfg.get("kind", "uniform")
     args.residency = cfg.get("residency", "auto")
