@@ -20,6 +20,17 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD MI355X GPU (runs on the GPU box)")
+    config.addinivalue_line("markers", "full: full-size case (minutes); runs only with DLR_FULL=1 -- the final "
+                                       "tree's run, whose log is committed under profiles/")
+
+
+def pytest_collection_modifyitems(config, items):
+    if os.environ.get("DLR_FULL") == "1":
+        return
+    skip = pytest.mark.skip(reason="full-size case: set DLR_FULL=1")
+    for it in items:
+        if "full" in it.keywords:
+            it.add_marker(skip)
 
 
 def _ensure_built():

@@ -210,16 +210,18 @@ def test_residency_reporting():
         eng.close()
 
 
-def test_c4_blocked_gradient_epoch(monkeypatch):
+@pytest.mark.parametrize("rows,nbat", [(250_000, 4), pytest.param(1_048_576, 16, marks=pytest.mark.full)])
+def test_c4_blocked_gradient_epoch(monkeypatch, rows, nbat):
     # The FAST blocked gradient over a C4-shaped epoch at B = 65,536 (250,000
-    # rows = 4 batches, the last one wrapping to row 0), against the oracle's
+    # rows = 4 batches, the last one wrapping to row 0; full: C4's 16-batch
+    # epoch, DLR_FULL=1), against the oracle's
     # sequential sums step by step: the drift bound FAST_DRIFT (see
     # test_c4_shape_dense_steps -- the reference's own fp32 gradient moves a
     # weight ~3e-7 per step away from exact arithmetic); prints the count
     # outside the north-star bar.
     monkeypatch.setenv("DLR_DENSE_GRAD", "blocked")
     D, B, lr = 4096, 65536, 0.05
-    dd = dlr.DenseDataset.generate(250_000, D, seed=10, stream=2)
+    dd = dlr.DenseDataset.generate(rows, D, seed=10, stream=2)
     X, y = dd.arrays()
     w0 = dlr.init_weight(D)
     eng = dlr.Engine(D)
@@ -227,7 +229,7 @@ def test_c4_blocked_gradient_epoch(monkeypatch):
         eng.set_summation_order(dlr.ORDER_FAST)
         eng.set_weights(w0)
         nb = eng.load_train_dense(dd, B)
-        assert nb == 4
+        assert nb == nbat
         w = w0.copy()
         worst = worst_abs = 0.0
         for b in range(nb):
@@ -240,7 +242,7 @@ def test_c4_blocked_gradient_epoch(monkeypatch):
             worst_abs = max(worst_abs, float(np.max(np.abs(a - bb))))
             assert np.all(np.abs(a - bb) <= FAST_DRIFT[0] * np.abs(bb) + FAST_DRIFT[1]), f"step {b}"
         drift(eng.get_weights(), w, "C4 FAST blocked, 1 epoch")
-        print(f"\nC4 blocked gradient, 1 epoch (16 x 65,536 rows, D 4,096): vs oracle max rel weight diff "
+        print(f"\nC4 blocked gradient, 1 epoch ({nb} x 65,536 rows, D 4,096): vs oracle max rel weight diff "
               f"{worst:.3g} (weights >= 1e-2), max abs diff {worst_abs:.3g}")
     finally:
         eng.close()

@@ -122,7 +122,8 @@ def test_c3_eight_ranks_loopback(c3_w8, order):
         within_bar(got.w, orc.w, "W = 8, long-column phases")
 
 
-@pytest.mark.parametrize("order,W", [("reference", 2), ("reference", 4), ("fast", 2)])
+@pytest.mark.parametrize("order,W", [("reference", 2), ("reference", 4), ("fast", 2),
+                                     pytest.param("fast", 4, marks=pytest.mark.full)])
 def test_dense_c4_shape_ranks(monkeypatch, W, order):
     # C4's shape (D = 4,096, B = 65,536; 3 batches per epoch, the last
     # wrapping) on W loopback ranks at the bench's lr 0.2.  Reference order
@@ -147,8 +148,8 @@ def test_dense_c4_shape_ranks(monkeypatch, W, order):
     finally:
         eng.close()
     # (W = 4 runs one epoch -- its three batches, the last wrapping -- to
-    # keep the suite's time down)
-    epochs = 2 if W == 2 else 1
+    # keep the suite's time down; FAST at W = 4 two, DLR_FULL=1)
+    epochs = 2 if W == 2 or order == "fast" else 1
     got = run_group(shards, D, epochs, B, lr, dense=True, order=o)
     orc = oracle.run_worker(arrays, D, epochs, B, lr, sparse=False)
     if order == "reference":
