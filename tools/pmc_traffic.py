@@ -91,8 +91,10 @@ def main() -> int:
     # The product margin in the gradient's launch (k_grad_lds<F, true,
     # false, true, true>: pass 2 + gradient + update + next pass 1) is a step
     # of its own, like K6r.  A kernel counts in the first role that matches.
-    # (round 5 added a sixth template argument, DB: both spellings)
-    mg = [", true, false, true, true>", ", true, false, true, true, "]
+    # (round 5 added a sixth template argument, DB, round 6 removed it and
+    # the NT argument: k_grad_lds<FILL, FUSED, PM, MG>; all spellings)
+    mg = [", true, false, true, true>", ", true, false, true, true, ", "k_grad_lds<1, true, true, true>",
+          "k_grad_lds<2, true, true, true>", "k_grad_lds<4, true, true, true>", "k_grad_lds<8, true, true, true>"]
     roles = [("margin", ["k_margin", "k_pm_margin", "k_pm_products", "k_dense_fused", "k_dense_margin", "k_flag_store"]),
              ("step", ["k_dense_ref<", *mg]),  # one launch: margin + gradient + update
              ("grad", ["k_grad", "k_long_", "k_band_finalize", "k_band_hot", "k_hot_chain", "k_dense_grad",
