@@ -476,3 +476,40 @@ def test_pm_windows_full_shard_batch(monkeypatch, band_rows):
         g = oracle.grad_csr((rp, col, val), lab, np.arange(n), w)
         oracle.server_update(w, [g], 0.2)
     assert_same_weights(got, w, "windowed product margin vs oracle")
+
+
+def test_pm_windows_wrapping_batches(monkeypatch):
+    # Band mode with batches that are not the whole shard: B = 600,000 over
+    # 1.1M rows in 2^18-row bands -- per batch 2 full bands (4 windows each,
+    # one pass-1 and one pass-2 launch a band) and a 75,712-row band (2
+    # windows, the last partial); batch 1 wraps to row 0 (data_iter.h:49-52).
+    # Three steps (batches 0, 1, 0), bitwise the gather margin and the oracle.
+    monkeypatch.setenv("DLR_BAND_ROWS", "262144")
+    D, n, B = 1 << 20, 1_100_000, 600_000
+    ds = dlr.Dataset.generate(n, D, 50, value_mode=1, seed=9, stream=5)
+    seq = [0, 1, 0]
+
+    def run(pm):
+        monkeypatch.setenv("DLR_PM", pm)
+        eng = dlr.Engine(D)
+        try:
+            eng.set_weights(dlr.init_weight(D))
+            assert eng.load_train(ds, B) == 2
+            assert eng.train_band_rows() == 262144
+            kind = eng.train_product_margin()
+            for b in seq:
+                eng.train_step(b, 0.2, 1.0)
+            return eng.get_weights(), kind
+        finally:
+            eng.close()
+
+    got, kind = run("1")
+    assert kind == 1
+    ref, _ = run("0")
+    assert_same_weights(got, ref, "windowed product margin vs gathers (wrapping batches)")
+    rp, col, val, lab = ds.csr()
+    w = dlr.init_weight(D)
+    for b in seq:
+        g = oracle.grad_csr((rp, col, val), lab, oracle.batch_rows(n, B, b), w)
+        oracle.server_update(w, [g], 0.2)
+    assert_same_weights(got, w, "windowed product margin vs oracle (wrapping batches)")
