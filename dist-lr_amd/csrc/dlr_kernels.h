@@ -58,8 +58,7 @@ struct DevLong {
 
 // One batch column-major, PHASE-SPLIT for the LDS-resident gradient
 // kernel: rows fall in phases of R = fill*4,096 rows (grad_lds_phase_rows:
-// one phase of <= 16,384 rows, or up to four of 16,384 -- the
-// double-buffered form -- or, with DLR_GRAD_DB=0, up to two of 32,768).
+// one phase of <= 16,384 rows, or up to two of 32,768).
 // For 64-column group g and phase p, block (g*phases + p) holds the entries
 // of those columns whose row is in the phase, column by column, rows
 // ascending; base[blk] is its first entry (4-aligned), ends[blk*64 + l] the

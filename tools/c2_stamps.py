@@ -27,7 +27,6 @@ SLOTS = {11: "mg start", 12: "mg p2 pub", 14: "mg p2 pub w3", 13: "mg ph0 ok", 0
          3: "fill1 out", 4: "ph1 go", 5: "compute end", 6: "pass1 go", 7: "end"}
 # the double-buffered phases (k_grad_lds DB, batches of > 16,384 rows): slots 2
 # and 3 are phases 2 and 3 going (slot 10 is then unused)
-SLOTS_DB = {**SLOTS, 2: "ph2 go", 3: "ph3 go"}
 # the row-round kernel (k_grad_rt, the default for product-margin batches)
 SLOTS_RT = {0: "start", 1: "issued", **{2 + t: f"round {t} go" for t in range(8)}, 10: "rounds done",
             11: "col sums done", 12: "pass1 go", 13: "end"}
@@ -61,8 +60,6 @@ def main():
     eng.set_weights(dlr.init_weight(D))
     nb = eng.load_train(ds, a.batch)
     print(f"layout {eng.train_layout()} product margin {eng.train_product_margin()} batches {nb} grid {G}")
-    if a.lds and a.batch > 16384 and os.environ.get("DLR_GRAD_DB", "0") == "1":
-        SLOTS = SLOTS_DB
     k = 0
     rel = {s: [] for s in SLOTS}
     for rep in range(a.reps + 1):

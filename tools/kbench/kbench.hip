@@ -1092,8 +1092,7 @@ int main(int argc, char **argv) {
     int bad = 0;
     CK(hipMemcpy(d_w, w0.data(), D * 4, hipMemcpyHostToDevice));
     for (int seg : {16, 32, 64}) {
-        setenv("DLR_MARGIN_SEG", seg == 16 ? "16" : seg == 32 ? "32" : "64", 1);
-        // margin_seg caches the env var on first use: launch the template directly.
+        // each rows-per-wave form of the margin template, launched directly
         const dim3 blk(256);
         auto go = [&] {
             if (seg == 16)
