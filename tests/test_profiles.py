@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = [
     # round 5: the margin in the gradient's launch (one launch per step),
     # the round-5 issue order
-    ("traffic.json", "r05_pmc_c2", "D1000000_nnz50_B65536", "lds", 0),
+    ("traffic.json", "r06_pmc_c2", "D1000000_nnz50_B65536", "lds", 0),
     # round 5: C3 in the reference order (hot-column product stream); 14
     # step-equivalents (bench --steps 6 --warmup 2 --no-stage-pass: 2 + 6 +
     # 6 steps)
