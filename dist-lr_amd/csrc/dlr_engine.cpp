@@ -127,6 +127,7 @@ struct TrainShard {
     float *pm_val = nullptr, *pm_p = nullptr;
     uint16_t *pm_qs = nullptr;
     std::vector<int64_t> pmo_list, pmo_pofs, pmo_rg, pmo_qs;
+    std::vector<uint32_t> pm_rstride, pm_qstride;  // per span (DevPm)
     // row-round gradient (dlr_kernels.h DevRt) of every product-margin batch:
     // gq / val at rtoff[b] (pmS * rt_rounds * rt_cap[b] entries), cend at
     // b*pmS*kPmSlice; rt_rounds rounds per batch
@@ -1596,6 +1597,7 @@ struct PmBatch {
     std::vector<float> val;
     std::vector<uint16_t> qs;
     int groups = 0;
+    uint32_t rstride = 0, qstride = 0;  // DevPm: fixed region / slot-list strides (0: none)
     int64_t maxslice = 0;
     // the row-round gradient's view of the same batch (dlr_kernels.h DevRt);
     // empty when a slice holds more than kRtCap entries
@@ -1693,11 +1695,24 @@ bool pm_batch(const CsrView &ds, const dlr::BatchSpan &sp, int64_t D, bool unit,
         if (ds.row_ptr[r + 1] - ds.row_ptr[r] > 8 * dlr::kPmMaxGroups) return false;
         for (int64_t e = ds.row_ptr[r]; e < ds.row_ptr[r + 1]; ++e) ++cnt[(size_t)(k * S + ds.col[e] / dlr::kPmSlice)];
     }
-    // chunks padded to whole 4-slot groups (pass 1 stores 16 bytes per group)
+    // chunks padded to whole 4-slot groups (pass 1 stores 16 bytes per group).
+    // Regions at a FIXED stride (the batch's largest region) when that costs
+    // at most 1/8 more space than packing them -- uniform rows (C2) -- so
+    // pass 2 needs no offset load (DevPm::rstride)
+    uint32_t rmax = 0;
+    uint64_t rsum = 0;
+    for (int64_t k = 0; k < nblk; ++k) {
+        uint32_t n = 0;
+        for (int64_t q = 0; q < S; ++q) n += (cnt[(size_t)(k * S + q)] + 3) & ~3u;
+        rmax = std::max(rmax, n);
+        rsum += n;
+    }
+    o.rstride = (uint64_t)rmax * (uint64_t)nblk * 8 <= rsum * 9 ? rmax : 0u;
     std::vector<uint32_t> cofs((size_t)(nblk * S));
     o.rg.assign((size_t)nblk + 1, 0);
     uint32_t at = 0;
     for (int64_t k = 0; k < nblk; ++k) {
+        if (o.rstride) at = (uint32_t)k * o.rstride;
         o.rg[(size_t)k] = at;
         for (int64_t q : sorder) {
             const uint32_t n = (cnt[(size_t)(k * S + q)] + 3) & ~3u;
@@ -1708,7 +1723,7 @@ bool pm_batch(const CsrView &ds, const dlr::BatchSpan &sp, int64_t D, bool unit,
         }
         if (at - o.rg[(size_t)k] > (uint32_t)dlr::kPmCap) return false;
     }
-    o.rg[(size_t)nblk] = at;
+    o.rg[(size_t)nblk] = o.rstride ? (uint32_t)nblk * o.rstride : at;
     for (int64_t q = 0; q < S; ++q) {
         o.maxslice = std::max<int64_t>(o.maxslice, slice_n[(size_t)q + 1]);
         slice_n[(size_t)q + 1] += slice_n[(size_t)q];
@@ -1747,12 +1762,20 @@ bool pm_batch(const CsrView &ds, const dlr::BatchSpan &sp, int64_t D, bool unit,
     o.qoff.assign((size_t)nblk + 1, 0);
     o.qs.clear();
     o.groups = 0;
+    // slot lists at a fixed stride too (the batch's most groups; a block's
+    // extra groups are zeros its rows never take)
+    std::vector<int> gblk((size_t)nblk);
     for (int64_t k = 0; k < nblk; ++k) {
         const int64_t i0 = k * dlr::kPmRows, i1 = std::min(R, i0 + dlr::kPmRows);
         int64_t ml = 0;
         for (int64_t i = i0; i < i1; ++i) ml = std::max(ml, ds.row_ptr[row_of(i) + 1] - ds.row_ptr[row_of(i)]);
-        const int g = (int)((ml + 7) / 8);
-        o.groups = std::max(o.groups, g);
+        gblk[(size_t)k] = (int)((ml + 7) / 8);
+        o.groups = std::max(o.groups, gblk[(size_t)k]);
+    }
+    o.qstride = o.rstride ? (uint32_t)o.groups * 512u : 0u;
+    for (int64_t k = 0; k < nblk; ++k) {
+        const int64_t i0 = k * dlr::kPmRows, i1 = std::min(R, i0 + dlr::kPmRows);
+        const int g = o.qstride ? o.groups : gblk[(size_t)k];
         const size_t q0 = o.qs.size();
         o.qoff[(size_t)k] = (uint32_t)q0;
         o.qs.resize(q0 + (size_t)g * 512, 0);
@@ -1892,6 +1915,8 @@ dlr::DevPm pm_view(const dlr_ctx *c, int64_t b) {
     v.nblk = t.pmo_rg[(size_t)b + 1] - t.pmo_rg[(size_t)b] - 1;
     v.groups = t.pm_groups;
     v.split = t.pm_split;
+    v.rstride = t.pm_rstride[(size_t)b];
+    v.qstride = t.pm_qstride[(size_t)b];
     return v;
 }
 
@@ -2411,6 +2436,8 @@ int build_pm(dlr_ctx *c, const CsrView &src, const std::vector<dlr::BatchSpan> &
         t.pmo_pofs.assign((size_t)ns + 1, 0);
         t.pmo_rg.assign((size_t)ns + 1, 0);
         t.pmo_qs.assign((size_t)ns + 1, 0);
+        t.pm_rstride.clear();
+        t.pm_qstride.clear();
         int64_t pcap = 0, maxslice = 0;
         for (int64_t b = 0; b < ns; ++b) {
             const PmBatch &q = pm[(size_t)b];
@@ -2421,6 +2448,8 @@ int build_pm(dlr_ctx *c, const CsrView &src, const std::vector<dlr::BatchSpan> &
             pcap = std::max<int64_t>(pcap, q.rg.back());
             maxslice = std::max(maxslice, q.maxslice);
             t.pm_groups = std::max(t.pm_groups, q.groups);
+            t.pm_rstride.push_back(q.rstride);
+            t.pm_qstride.push_back(q.qstride);
         }
         t.pm_split = (int)std::min<int64_t>(16, std::max<int64_t>(1, (maxslice + 16383) / 16384));
         if (c->tune.pm_split != DLR_AUTO)  // pass-1 workgroups per slice (separate pass)

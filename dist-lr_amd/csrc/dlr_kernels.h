@@ -189,6 +189,10 @@ struct DevPm {
     int64_t S, nblk;
     int groups;            // max slot groups of a block (8 entries each)
     int split;             // pass-1 workgroups per slice (standalone pass)
+    // fixed strides (0: none): block k's region at k * rstride, its slot
+    // lists at k * qstride -- pass 2 then issues its region copy and slot
+    // list loads at once, without loading rg / qoff first
+    uint32_t rstride = 0, qstride = 0;
 };
 
 // The product margin's pass 2 run INSIDE the fused gradient (k_grad_lds MG,

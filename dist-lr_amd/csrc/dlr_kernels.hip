@@ -1140,8 +1140,11 @@ template <int QG, bool SC1>
 __device__ __forceinline__ void pm_rowsum(const DevPm &pm, const DevBatch &bt, const float *__restrict__ p,
                                           float *resid, int64_t blk, float *sr, int lane) {
     const int64_t r0 = blk * kPmRows;
-    const uint32_t a = pm.rg[blk], b = pm.rg[blk + 1];
-    const uint32_t q0 = pm.qoff[blk], q1 = pm.qoff[blk + 1];
+    // (fixed strides: no dependent load at the head of the hand-off chain)
+    const uint32_t a = pm.rstride ? (uint32_t)blk * pm.rstride : pm.rg[blk];
+    const uint32_t b = pm.rstride ? a + pm.rstride : pm.rg[blk + 1];
+    const uint32_t q0 = pm.qstride ? (uint32_t)blk * pm.qstride : pm.qoff[blk];
+    const uint32_t q1 = pm.qstride ? q0 + pm.qstride : pm.qoff[blk + 1];
     const int64_t my = r0 + lane;
     const bool valid = my < bt.rows;
     const int64_t mc = valid ? my : r0;
