@@ -1205,7 +1205,12 @@ void build_bands(const std::vector<uint32_t> &cptr, const std::vector<RowT> &cro
 // far below the 250 ms error bound
 constexpr uint32_t kHsGiveUpTicks = 2000000;  // 20 ms at 100 MHz
 // bands of a step's first hot-chain launch (band_step_pipelined)
-constexpr int64_t kHsFirstGroup = 4;
+// (C3, same box: 1 band 5.72-5.73 ms, 2 bands 5.72-5.73, 3 bands 5.77-5.78,
+// 4 bands 5.79-5.81; profiles/r06_c3_hot_first_group.txt)
+#ifndef DLR_HS_FIRST  // (A/B builds only: make variant VDEFS=-DDLR_HS_FIRST=n)
+#define DLR_HS_FIRST 2
+#endif
+constexpr int64_t kHsFirstGroup = DLR_HS_FIRST;
 // rows of a window of the band-mode product margin (TrainShard::pmw): the
 // product margin's 1,024 blocks of 64 rows
 constexpr int64_t kPmWinRows = (int64_t)dlr::kPmMaxBlocks * dlr::kPmRows;
@@ -2339,7 +2344,7 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
         // faster than the GPU runs its margin, and a chain adds a band ~3x
         // slower than the margins make one: the first launch is queued before
         // band 0's margin ends and the second long before the first's chains
-        // end -- one launch boundary a step (C3: 5.78 ms; geometric groups,
+        // end -- one launch boundary a step (C3: 5.72 ms; geometric groups,
         // 6 launches: 5.95 ms, each boundary a sync of chains of unequal
         // band lengths)
         if (e == hipSuccess && hs && (k + 1 == hc_end || k + 1 == nbands)) {

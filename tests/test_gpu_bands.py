@@ -423,9 +423,9 @@ def test_hot_stream_valued_and_ragged_bands():
 
 
 def _chain_launches(nbands):
-    # k_hot_chain launches per step: one after the margins of band 4 (the
-    # first four bands'), one after the last margin (DevHotChain)
-    return 1 if nbands <= 4 else 2
+    # k_hot_chain launches per step: one after the margins of band 2 (the
+    # first two bands'), one after the last margin (DevHotChain)
+    return 1 if nbands <= 2 else 2
 
 
 def test_hot_stream_serialised_kernels_no_giveup(tmp_path):
