@@ -1201,12 +1201,15 @@ __device__ __forceinline__ void pm_rowsum(const DevPm &pm, const DevBatch &bt, c
 }
 
 // Pass 2: a wave per block.
-template <int QG>
-__global__ __launch_bounds__(256) void k_pm_margin(DevPm pm, DevBatch bt, const float *__restrict__ p,
-                                                   float *__restrict__ resid) {
-    __shared__ __attribute__((aligned(16))) float s_reg[4][kPmCap];
+// NW waves (blocks) per workgroup: 4, or 1 for a small batch (B <= 8,192:
+// 128 blocks), whose blocks would otherwise share 32 CUs' memory paths --
+// each block pulls ~20 KB (region + slot lists) at once
+template <int QG, int NW = 4>
+__global__ __launch_bounds__(NW *kWave) void k_pm_margin(DevPm pm, DevBatch bt, const float *__restrict__ p,
+                                                         float *__restrict__ resid) {
+    __shared__ __attribute__((aligned(16))) float s_reg[NW][kPmCap];
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
-    const int64_t blk = (int64_t)blockIdx.x * 4 + wv;
+    const int64_t blk = (int64_t)blockIdx.x * NW + wv;
     if (blk * kPmRows >= bt.rows) return;  // wave-uniform
     pm_rowsum<QG, false>(pm, bt, p, resid, blk, s_reg[wv], lane);
 }
@@ -4251,18 +4254,31 @@ hipError_t launch_pm_windows(const DevPm *views, const DevPm &pm0, int64_t nwin,
     return hipGetLastError();
 }
 
+namespace {
+int device_cus();
+}  // namespace
+
 hipError_t launch_pm_margin(const DevPm &pm, const DevBatch &bt, const float *p, float *resid, hipStream_t s) {
     if (bt.rows <= 0) return hipSuccess;
     if ((bt.rows + kPmRows - 1) / kPmRows != pm.nblk) return hipErrorInvalidValue;
-    const dim3 grid((unsigned)((pm.nblk + 3) / 4));
-    if (pm.groups <= 4)
-        hipLaunchKernelGGL((k_pm_margin<4>), grid, dim3(256), 0, s, pm, bt, p, resid);
-    else if (pm.groups <= 8)
-        hipLaunchKernelGGL((k_pm_margin<8>), grid, dim3(256), 0, s, pm, bt, p, resid);
-    else if (pm.groups <= kPmMaxGroups)
-        hipLaunchKernelGGL((k_pm_margin<kPmMaxGroups>), grid, dim3(256), 0, s, pm, bt, p, resid);
-    else
+    // one block per workgroup while the blocks fit the device's CUs twice
+    const bool one = pm.nblk <= 2 * (int64_t)device_cus();
+    const dim3 grid((unsigned)(one ? pm.nblk : (pm.nblk + 3) / 4)), blk(one ? kWave : 4 * kWave);
+#define DLR_PMM(G)                                                                   \
+    if (one)                                                                         \
+        hipLaunchKernelGGL((k_pm_margin<G, 1>), grid, blk, 0, s, pm, bt, p, resid); \
+    else                                                                             \
+        hipLaunchKernelGGL((k_pm_margin<G, 4>), grid, blk, 0, s, pm, bt, p, resid);
+    if (pm.groups <= 4) {
+        DLR_PMM(4)
+    } else if (pm.groups <= 8) {
+        DLR_PMM(8)
+    } else if (pm.groups <= kPmMaxGroups) {
+        DLR_PMM(kPmMaxGroups)
+    } else {
         return hipErrorInvalidValue;
+    }
+#undef DLR_PMM
     return hipGetLastError();
 }
 
