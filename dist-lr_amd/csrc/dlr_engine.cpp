@@ -349,6 +349,7 @@ struct dlr_ctx {
     // ... and the hot pairs' stream (k_band_hot, band after band)
     hipStream_t hstream = nullptr;
     hipEvent_t ev_hdone = nullptr;
+    hipEvent_t ev_hmargins = nullptr;  // after a step's last margin (the final hot-chain launch waits on it)
     hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
     std::vector<void *> allocs;
     // timing
@@ -2290,6 +2291,7 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
     if (hot && !c->hstream) {
         e = hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_hdone, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_hmargins, hipEventDisableTiming);
         if (e != hipSuccess) return e;
     }
     while ((int64_t)c->ev_band.size() < nbands) {
@@ -2340,6 +2342,7 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
         if (e == hipSuccess && hs) e = dlr::launch_flag_store(t.hs_flag + k, t.hs_seq, c->stream);
         // the hot chains of bands [hc.b1, k + 1), queued after their margins
         // (DevHotChain): two launches, the first bands', then the rest's
+        // (and the final one below)
         // after the last margin.  The host queues a band's launches ~4x
         // faster than the GPU runs its margin, and a chain adds a band ~3x
         // slower than the margins make one: the first launch is queued before
@@ -2364,6 +2367,22 @@ hipError_t band_step_pipelined(dlr_ctx *c, int64_t b, int64_t B, float *gout, fl
         // stream, beside the next band's margin and the other columns
         if (e == hipSuccess && hot && !hs) e = hipStreamWaitEvent(c->hstream, c->ev_band[(size_t)k], 0);
         if (e == hipSuccess && hot && !hs) e = dlr::launch_band_hot(dv, t.bhw + bd.hw, bd.nhot, c->resid, t.gacc, c->hstream, c->d_err, c->fault);
+    }
+    // the final chain launch, ordered after the last margin by an event:
+    // empty unless a launch above gave up on a flag (kernels run one at a
+    // time, e.g. under counter collection, in an order the streams do not
+    // fix) -- then it adds the rest; only it reports a missing flag
+    if (e == hipSuccess && hs) {
+        e = hipEventRecord(c->ev_hmargins, c->stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(c->hstream, c->ev_hmargins, 0);
+        if (e == hipSuccess) {
+            dlr::DevHotChain fin = hc;
+            fin.b0 = nbands;
+            fin.b1 = nbands;
+            fin.final_launch = 1;
+            e = dlr::launch_hot_chain(fin, t.gacc, c->hstream);
+            ++c->hcount[DLR_COUNT_HOT_CHAIN_LAUNCHES];
+        }
     }
     if (e == hipSuccess) e = hipEventRecord(c->ev_bdone, c->gstream);
     if (e == hipSuccess && hot) e = hipEventRecord(c->ev_hdone, c->hstream);
@@ -2734,6 +2753,7 @@ void dlr_destroy(dlr_ctx *ctx) {
     if (ctx->ev_bdone) (void)hipEventDestroy(ctx->ev_bdone);
     if (ctx->gstream) (void)hipStreamDestroy(ctx->gstream);
     if (ctx->ev_hdone) (void)hipEventDestroy(ctx->ev_hdone);
+    if (ctx->ev_hmargins) (void)hipEventDestroy(ctx->ev_hmargins);
     if (ctx->hstream) (void)hipStreamDestroy(ctx->hstream);
     if (ctx->ev_xmerged) (void)hipEventDestroy(ctx->ev_xmerged);
     for (hipEvent_t e : ctx->ev_xpiece)

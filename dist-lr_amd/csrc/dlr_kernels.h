@@ -298,9 +298,13 @@ hipError_t launch_flag_store(uint32_t *flag, uint32_t seq, hipStream_t s);
 // b1 - 1 (two launches: the first bands', then the rest), so the flags a launch
 // waits on come from margins queued BEFORE it: beside it on another
 // hardware queue, or ahead of it when the streams share one.  A flag not
-// up within `giveup` ticks (100 MHz) ends a launch that is not the last
-// (stats[kStatHotGiveUps] += 1 per column; the next launch adds the rest,
-// the same chain, the same bits); the last launch records kErrHotFlag.
+// up within `giveup` ticks (100 MHz) ends such a launch (stats[
+// kStatHotGiveUps] += 1 per column; a later launch adds the rest, the same
+// chain, the same bits).  Then a FINAL launch (final = 1, b0 = b1 =
+// nbands) that the stream orders after the last margin by an event: empty
+// when the chains are done (the usual case), it adds what a launch gave up
+// on -- kernels run one at a time, as counter collection runs them, in
+// whatever order across streams -- and only it records kErrHotFlag.
 struct DevHotChain {
     const uint32_t *cols;
     const uint2 *seg;
@@ -314,6 +318,7 @@ struct DevHotChain {
     int64_t b0, b1;
     uint32_t giveup;
     uint32_t *stats;  // host-mapped counters (kStat*), or null
+    int final_launch = 0;  // ordered after every margin: a missing flag is an error
 };
 constexpr int kHotChunkF = 256;  // floats of one stream chunk (a band segment starts at a multiple)
 hipError_t launch_hot_chain(const DevHotChain &hc, float *gacc, hipStream_t s);

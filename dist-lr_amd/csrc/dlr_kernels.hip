@@ -2293,7 +2293,7 @@ __global__ __launch_bounds__(2 * kHcCols * kWave) void k_hot_chain(DevHotChain h
         acc0 = __uint_as_float(st.y);
     }
     if (s0 >= hc.b1) return;  // (wave-uniform; state stays as it is)
-    const bool last = hc.b1 >= hc.nbands;
+    const bool last = hc.final_launch != 0;
     Spin spin(hc.err, kErrHotLds);
     if (wv >= kHcCols) {
         // the loader: chunk g of the column's stream (bands in order) into
@@ -2326,8 +2326,8 @@ __global__ __launch_bounds__(2 * kHcCols * kWave) void k_hot_chain(DevHotChain h
                     __builtin_amdgcn_s_sleep(8);
                 }
                 if (!up) {
-                    // (the last launch runs after every margin: a flag it
-                    // does not see is an error)
+                    // (the final launch runs after every margin: a flag
+                    // it does not see is an error)
                     if (last && hc.err && lane == 0)
                         __hip_atomic_store(hc.err + kErrHotFlag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     if (!last && hc.stats && lane == 0)

@@ -424,8 +424,9 @@ def test_hot_stream_valued_and_ragged_bands():
 
 def _chain_launches(nbands):
     # k_hot_chain launches per step: one after the margins of band 2 (the
-    # first two bands'), one after the last margin (DevHotChain)
-    return 1 if nbands <= 2 else 2
+    # first two bands'), one after the last margin, and the final one the
+    # stream orders after the last margin (DevHotChain)
+    return (1 if nbands <= 2 else 2) + 1
 
 
 def test_hot_stream_serialised_kernels_no_giveup(tmp_path):

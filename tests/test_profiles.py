@@ -20,7 +20,7 @@ CASES = [
     # round 5: C3 in the reference order (hot-column product stream); 14
     # step-equivalents (bench --steps 6 --warmup 2 --no-stage-pass: 2 + 6 +
     # 6 steps)
-    ("traffic_c3.json", "r05_pmc_c3", "D16777216_nnz39_B-1", "classic", 14),
+    ("traffic_c3.json", "r06_pmc_c3", "D16777216_nnz39_B-1", "classic", 14),
     # round 3: C3 in the FAST order (c3f); the band-pipelined margin is
     # dispatched per band; 20 step-equivalents (bench --steps 6 --warmup 2:
     # 2 + 6 timed + 6 + 6 stage and breakdown steps)
