@@ -465,11 +465,13 @@ int dlr_stage_time(dlr_ctx *ctx, int stage, int64_t first_batch, int64_t count, 
 /* Event counts of the steps since the training shard was loaded (n <= 
  * DLR_COUNTERS entries into out; syncs the context's streams first):
  *   DLR_COUNT_HOT_CHAIN_LAUNCHES  k_hot_chain launches queued (C3's hot
- *                                 columns: a few per step, each after the
- *                                 margins of its last band);
+ *                                 columns: three per step -- two after the
+ *                                 margins of their last band, and a final
+ *                                 one ordered after the last margin, empty
+ *                                 unless a launch gave up);
  *   DLR_COUNT_HOT_GIVEUPS         hot chains that stopped at a band flag not
- *                                 up within 20 ms and left the band to the
- *                                 next launch (same bits, but the step ran
+ *                                 up within 20 ms and left the band to a
+ *                                 later launch (same bits, but the step ran
  *                                 serialised behind that wait; 0 in a
  *                                 healthy run);
  *   DLR_COUNT_COWAIT_SERIALISED   co-waiting launches (one-launch step, K6r,
