@@ -4118,6 +4118,16 @@ int dlr_train_product_margin(dlr_ctx *c) {
     return c->train.pm ? (c->train.pm_fused ? (c->train.pm_mg ? 3 : 2) : 1) : c->train.pmw ? 1 : 0;
 }
 
+int dlr_train_pm_strided(dlr_ctx *c) {
+    if (!c) return DLR_E_ARG;
+    if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_pm_strided: no training shard loaded");
+    const TrainShard &t = c->train;
+    if (!t.pm && !t.pmw) return 0;
+    size_t n = 0;
+    for (uint32_t r : t.pm_rstride) n += r != 0;
+    return n == 0 ? 0 : n == t.pm_rstride.size() ? 1 : 2;
+}
+
 int dlr_train_row_rounds(dlr_ctx *c) {
     if (!c) return DLR_E_ARG;
     if (!c->train.loaded) return fail(c, DLR_E_STATE, "dlr_train_row_rounds: no training shard loaded");

@@ -55,7 +55,7 @@ SYMBOLS = [
     "dlr_summation_order",
     "dlr_train_step", "dlr_train_epoch", "dlr_worker_gradient", "dlr_server_apply", "dlr_predict", "dlr_sync",
     "dlr_set_fault",
-    "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_stage_counters", "dlr_train_layout", "dlr_train_band_rows", "dlr_train_relabeled", "dlr_train_unit_values", "dlr_train_product_margin", "dlr_train_hot_columns", "dlr_train_row_rounds",
+    "dlr_timing", "dlr_kernel_time", "dlr_stage_time", "dlr_stage_counters", "dlr_train_layout", "dlr_train_band_rows", "dlr_train_relabeled", "dlr_train_unit_values", "dlr_train_product_margin", "dlr_train_pm_strided", "dlr_train_hot_columns", "dlr_train_row_rounds",
     "dlr_set_exchange_overlap", "dlr_exchange_overlap", "dlr_set_exchange_pieces", "dlr_exchange_pieces",
     "dlr_memory_info", "dlr_stream_bytes",
 ]
@@ -216,6 +216,7 @@ _sig("dlr_train_band_rows", C.c_int, P)
 _sig("dlr_train_relabeled", C.c_int, P)
 _sig("dlr_train_unit_values", C.c_int, P)
 _sig("dlr_train_product_margin", C.c_int, P)
+_sig("dlr_train_pm_strided", C.c_int, P)
 _sig("dlr_train_hot_columns", C.c_int, P)
 _sig("dlr_train_row_rounds", C.c_int, P)
 _sig("dlr_set_exchange_overlap", C.c_int, P, C.c_int)
@@ -726,6 +727,13 @@ class Engine:
         product margin with pass 1 fused into the previous step's gradient
         (dlr_train_product_margin)."""
         rc = lib.dlr_train_product_margin(self._h)
+        self._c(min(rc, 0))
+        return rc
+
+    def train_pm_strided(self) -> int:
+        """1: every batch's product-margin regions at fixed strides; 0: none
+        (packed, or no product margin); 2: some (dlr_train_pm_strided)."""
+        rc = lib.dlr_train_pm_strided(self._h)
         self._c(min(rc, 0))
         return rc
 

@@ -550,6 +550,12 @@ int dlr_train_unit_values(dlr_ctx *ctx);
  * margin run it over windows of 65,536 rows (pass 1 and pass 2 per window:
  * reported as 1). */
 int dlr_train_product_margin(dlr_ctx *ctx);
+/* The product margin's region layout of the loaded shard: 1 when every
+ * batch (or window) keeps its regions and slot lists at fixed strides
+ * (uniform rows: pass 2 then loads no offsets first), 0 when none does
+ * (packed: ragged rows), 2 when some do; 0 without the product margin.
+ * Either way the same products and sums. */
+int dlr_train_pm_strided(dlr_ctx *ctx);
 
 /* Band mode, REFERENCE order: the hot columns (>= DLR_BAND_HOT entries in a
  * batch, default 2^17: C3's Zipf heads) whose chains run from the HOT-COLUMN

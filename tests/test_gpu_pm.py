@@ -513,3 +513,34 @@ def test_pm_windows_wrapping_batches(monkeypatch):
         g = oracle.grad_csr((rp, col, val), lab, oracle.batch_rows(n, B, b), w)
         oracle.server_update(w, [g], 0.2)
     assert_same_weights(got, w, "windowed product margin vs oracle (wrapping batches)")
+
+
+def _strided_of(ds, D, B):
+    eng = dlr.Engine(D)
+    try:
+        eng.set_weights(dlr.init_weight(D))
+        eng.load_train(ds, B)
+        return eng.train_product_margin(), eng.train_pm_strided()
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("shape", ["uniform", "ragged"])
+def test_pm_region_strides(pm_on, shape):
+    # The product margin's regions and slot lists at fixed strides (uniform
+    # rows: pass 2 loads no offsets first) and packed (ragged rows: the
+    # largest region is far above the mean), every pass-2 form (pm_on):
+    # both bitwise the oracle.
+    D = 300_000
+    if shape == "uniform":
+        ds = dlr.Dataset.generate(3000, D, 50, value_mode=1, seed=11, stream=2)
+    else:
+        ds = _ragged(9, D, 3000, max_len=90)  # (a block's region stays within kPmCap)
+    B = 1024
+    mode, strided = _strided_of(ds, D, B)
+    assert mode > 0
+    # (ragged: 0, or 2 if some batch's blocks happen to be even)
+    assert strided == 1 if shape == "uniform" else strided in (0, 2), strided
+    eng = run_engine([ds], D, 3, B, 0.2)
+    orc = oracle.run_worker([oracle_shard(ds, D)], D, 3, B, 0.2)
+    compare_runs(eng, orc)
